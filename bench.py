@@ -1,0 +1,239 @@
+"""bench.py -- MI355X monotonic RNN-T loss+grad throughput (BASELINE.json metric).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config headline|c2|ragged]
+
+One step = forward (log-softmax row reduce + alpha/beta DP) + backward (logit gradient, dL/dcost fused)
+over one batch through the autograd surface (monotonic_rnnt_loss(...).sum().backward()), plus, for N > 1,
+the single RCCL all-reduce of the summed loss. Inputs are synthetic and resident in HBM before timing.
+Scaling is weak: every rank owns its own B utterances (batch sharding, no data-path collective).
+
+Rank 0 prints ONE JSON line with the contract fields plus:
+  roofline     : the gradient kernel (dominant), algorithmic bytes (N_v + N) * V * 4 per launch divided by its
+                 average duration from HIP events recorded around each launch on its stream in the timed region
+  cpu_baseline : the reference's own CpuRNNTComputer<float> (oracle/_ref) -- or the oracle port when the reference
+                 build is absent -- timed on a bounded sample of the same workload on the host cores
+  kernels      : per-kernel average ms and achieved GB/s
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "monotonic-rnnt_amd", "pytorch_binding"))
+
+METRIC = "utterances/sec + achieved HBM GB/s, (B,T,S,V)=(64,1000,200,1024)"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
+
+
+def lengths_for(config, rank, world):
+    """Per-rank utterance lengths (weak scaling: each rank owns its own B utterances)."""
+    if config == "headline":  # BASELINE.json configs[2]
+        B, T, S, V = 64, 1000, 200, 1024
+        return np.full(B, T, np.int32), np.full(B, S, np.int32), V, "B=64,T=1000,S=200,V=1024 (configs[2], headline)"
+    if config == "c2":  # configs[1]
+        B, T, S, V = 16, 200, 40, 256
+        return np.full(B, T, np.int32), np.full(B, S, np.int32), V, "B=16,T=200,S=40,V=256 (configs[1])"
+    if config == "ragged":  # configs[3]: B=512 global, T~U[200,1600], S~U[20,min(300,T)], sharded over ranks
+        rng = np.random.default_rng(0)
+        Tg = rng.integers(200, 1601, 512).astype(np.int32)
+        Sg = np.array([rng.integers(20, min(300, t) + 1) for t in Tg], np.int32)
+        lo, hi = shard_bounds(Tg.astype(np.int64) * (Sg + 1), world)[rank]
+        return Tg[lo:hi], Sg[lo:hi], 1024, f"B=512 ragged (T~U[200,1600], S~U[20,min(300,T)]), V=1024, rank slice [{lo},{hi})"
+    raise SystemExit(f"unknown config {config}")
+
+
+def shard_bounds(cost, world):
+    """Contiguous utterance ranges with balanced sum of rows (greedy prefix split)."""
+    cum = np.concatenate([[0], np.cumsum(cost)])
+    total = cum[-1]
+    bounds, lo = [], 0
+    for r in range(world):
+        hi = len(cost) if r == world - 1 else int(np.searchsorted(cum, total * (r + 1) / world))
+        hi = max(hi, lo)
+        bounds.append((lo, hi))
+        lo = hi
+    return bounds
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="headline", choices=["headline", "c2", "ragged"])
+    ap.add_argument("--cpu-sample", type=int, default=8, help="utterances in the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import monotonic_rnnt_op as op
+    import _mrnnt_lib as L
+
+    lib = L.load()
+    T, S, V, workload = lengths_for(args.config, rank, world)
+    B = len(T)
+    rows = int(np.sum(T.astype(np.int64) * (S + 1)))
+    n_band = int(np.sum((S.astype(np.int64) + 1) * (T - S + 1) - 1))  # in-band rows N_v
+    # global row offset of this rank's first utterance, so every rank streams different synthetic data
+    all_rows = [rows]
+    if world > 1:
+        t = torch.tensor([rows], dtype=torch.int64, device=dev)
+        g = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(g, t)
+        all_rows = [int(x.item()) for x in g]
+    row0 = sum(all_rows[:rank])
+
+    stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    acts = torch.empty((rows, V), dtype=torch.float32, device=dev)
+    L.check(lib.mrnnt_synth_acts(ctypes.c_void_p(acts.data_ptr()), row0 * V, rows * V, 0, 1, stream), "synth")
+    rng = np.random.default_rng(1 + rank)
+    labels = torch.from_numpy(rng.integers(1, V, (B, max(1, int(S.max())))).astype(np.int32)).to(dev)
+    T_t = torch.from_numpy(T)
+    S_t = torch.from_numpy(S)
+    acts.requires_grad_(True)
+    torch.cuda.synchronize()
+
+    def step():
+        acts.grad = None
+        costs = op.monotonic_rnnt_loss(acts, labels, T_t, S_t, blank_label=0)
+        loss = costs.sum()
+        loss.backward()
+        if world > 1:
+            tot = loss.detach().clone()
+            dist.all_reduce(tot)  # the one RCCL exchange of the path: 4 bytes over xGMI
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    L.profile_enable(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    prof = L.profile_read()
+    L.profile_enable(False)
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    total_utts = torch.tensor([B], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(total_utts)
+    total_utts = int(total_utts.item())
+
+    grad_bytes = (n_band + rows) * V * 4  # algorithmic: read in-band acts rows once, write every grads row once
+    softmax_bytes = n_band * V * 4
+    step_bytes = (2 * n_band + rows) * V * 4
+
+    def avg_ms(name):
+        ms, n = prof[name]
+        return ms / n if n else None
+
+    g_ms = avg_ms("grad")
+    s_ms = avg_ms("log_softmax")
+    d_ms = avg_ms("alpha_beta")
+    achieved = grad_bytes / (g_ms * 1e-3) / 1e9 if g_ms else None
+
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_grad_traffic.json")
+    if os.path.exists(pmc_path):
+        try:
+            pm = json.load(open(pmc_path))
+            if pm.get("config") == args.config:
+                traffic = pm.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu and args.cpu_sample > 0:
+        cpu = cpu_baseline(lib, L, acts, labels, T, S, V, args.cpu_sample, stream)
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(total_utts * args.steps / elapsed, 3),
+            "unit": "utt/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: counter-hash N(0,1)-like acts (seed 0), labels U[1,V-1] (seed 1+rank); inputs resident in HBM",
+            "config": {"workload": workload, "utterances_per_gpu": B, "global_batch": total_utts,
+                       "rows_per_gpu": rows, "inband_rows_per_gpu": n_band, "V": V,
+                       "parallelism": f"dp{world} (batch-sharded, one 4-byte RCCL loss all-reduce)"},
+            "achieved_hbm_gbps_step": round(step_bytes * total_utts / B * args.steps / elapsed / 1e9, 1),
+            "roofline": {"kernel": "grad_vec_kernel (logit gradient)", "bound": "hbm",
+                         "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4) if achieved else None,
+                         "traffic": traffic, "algorithmic_bytes_per_launch": grad_bytes,
+                         "avg_launch_ms": round(g_ms, 4) if g_ms else None},
+            "kernels": {
+                "log_softmax": {"avg_ms": round(s_ms, 4) if s_ms else None,
+                                "gbps": round(softmax_bytes / (s_ms * 1e-3) / 1e9, 1) if s_ms else None},
+                "alpha_beta": {"avg_ms": round(d_ms, 4) if d_ms else None},
+                "grad": {"avg_ms": round(g_ms, 4) if g_ms else None, "gbps": round(achieved, 1) if achieved else None},
+            },
+            "cpu_baseline": cpu,
+            "loss_check": float(loss.item()),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(lib, L, acts, labels, T, S, V, n_sample, stream):
+    """Time the reference CPU path on the first n_sample utterances of the same synthetic workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    try:
+        import oracle as O
+    except Exception as e:  # pragma: no cover
+        return {"error": f"oracle unavailable: {e}"}
+    n = min(n_sample, len(T))
+    rows = int(np.sum(T[:n].astype(np.int64) * (S[:n] + 1)))
+    if rows * V >= 2 ** 31 and O.ref_available():  # reference's 32-bit offsets (cpu_workspace_manager.h:48)
+        while n > 1 and int(np.sum(T[:n].astype(np.int64) * (S[:n] + 1))) * V >= 2 ** 31:
+            n -= 1
+        rows = int(np.sum(T[:n].astype(np.int64) * (S[:n] + 1)))
+    host = acts.detach()[:rows].cpu().numpy()
+    lab = labels[:n].cpu().numpy()
+    threads = n
+    kind = "reference" if O.ref_available() else "port"
+    fn = O.ref_rnnt if kind == "reference" else O.oracle_rnnt
+    t0 = time.perf_counter()
+    costs, _ = fn(host, lab, T[:n], S[:n], precision="f32", num_threads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 4), "unit": "utt/s", "cores": threads, "kind": kind,
+            "sample": f"{n} utterances of the same workload (T={int(T[0])}, S={int(S[0])}, V={V}), "
+                      f"cost_and_grad at fp32, OpenMP over utterances ({threads} threads), {dt:.2f} s",
+            "finite": bool(np.all(np.isfinite(costs)))}
+
+
+if __name__ == "__main__":
+    main()

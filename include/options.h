@@ -1,0 +1,27 @@
+/* options.h -- RNNTOptions, field-for-field the reference's struct (include/options.h:12-24).
+ * The only change: `stream` is a HIP stream (the reference forward-declares CUstream). The typedef
+ * below is the same one hip_runtime_api.h makes, so this header needs no HIP include. */
+#ifndef MONOTONIC_RNNT_OPTIONS_H
+#define MONOTONIC_RNNT_OPTIONS_H
+
+typedef struct ihipStream_t *hipStream_t;
+
+typedef enum { RNNT_CPU = 0, RNNT_GPU = 1 } rnntComputeLocation;
+
+struct RNNTOptions {
+    /* The maximum number of threads that can be used (CPU only in the reference; ignored here) */
+    int num_threads;
+
+    /* HIP stream the kernels are launched on (0 = legacy default stream) */
+    hipStream_t stream;
+
+    /* the label value/index that the RNNT calculation should use as the blank label */
+    int blank_label;
+
+    /* where the calculation should take place. This build executes RNNT_GPU only; RNNT_CPU returns
+     * RNNT_STATUS_EXECUTION_FAILED (mirrors the reference's behaviour for a location it was not built
+     * for, src/rnnt_entrypoint.cpp:41-43). */
+    rnntComputeLocation loc;
+};
+
+#endif /* MONOTONIC_RNNT_OPTIONS_H */

@@ -1,0 +1,501 @@
+// mrnnt_capi.cpp -- host side of libmonotonic_rnnt_amd.so: validation, workspace plan, kernel
+// orchestration on the caller's stream, the flat C ABI (include/mrnnt.h), and the reference-shaped
+// C++ surface (include/rnnt_entrypoint.h, gpu_workspace_manager.h, gpu_rnnt.h).
+//
+// No host synchronisation happens inside mrnnt_forward / mrnnt_backward (the reference synchronises
+// after each reduce and copies T/S/band arrays to the host every call: reduce.h:162,
+// gpu_rnnt.h:28-35). The only sync is in the reference-compatible compute_rnnt_loss /
+// GpuRNNTComputer path, whose contract returns host costs (gpu_rnnt.h:229).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "gpu_rnnt.h"
+#include "gpu_workspace_manager.h"
+#include "mrnnt.h"
+#include "mrnnt_internal.h"
+#include "rnnt_entrypoint.h"
+
+using namespace mrnnt;
+
+namespace {
+
+thread_local std::string g_last_error = "no error";
+
+RNNTStatus fail(RNNTStatus st, const std::string &msg) {
+    g_last_error = msg;
+    return st;
+}
+
+RNNTStatus fail_hip(hipError_t e, const char *where) {
+    return fail(RNNT_STATUS_EXECUTION_FAILED, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+constexpr size_t kAlign = 256;
+size_t align_up(size_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
+
+struct Plan {
+    int B = 0, V = 0, S_max = 0, T_max = 0;
+    int64_t N = 0, cols = 0;
+    bool align = false;
+    size_t off_row, off_col, off_mtmp, off_min, off_max, off_den, off_lpb, off_lpe, off_alpha, off_beta, off_ll,
+        off_llb, total;
+};
+
+RNNTStatus make_plan(const mrnnt_problem *p, Plan *pl) {
+    if (!p) return fail(RNNT_STATUS_INVALID_VALUE, "null problem");
+    if (p->B <= 0) return fail(RNNT_STATUS_INVALID_VALUE, "B must be > 0");
+    if (p->V <= 0) return fail(RNNT_STATUS_INVALID_VALUE, "V must be > 0");
+    if (!p->T_host || !p->S_host) return fail(RNNT_STATUS_INVALID_VALUE, "host lengths are required");
+    if (p->blank < 0 || p->blank >= p->V) return fail(RNNT_STATUS_INVALID_VALUE, "blank label out of range [0, V)");
+    Plan q;
+    q.B = p->B;
+    q.V = p->V;
+    for (int b = 0; b < p->B; ++b) {
+        const int T = p->T_host[b], S = p->S_host[b];
+        // reference validation: cpu_workspace_manager.h:103-107 / gpu_workspace_manager.h:235-239
+        if (T <= 0 || S < 0 || T < S)
+            return fail(RNNT_STATUS_INVALID_VALUE, "invalid lengths at utterance " + std::to_string(b) + ": T=" +
+                                                       std::to_string(T) + " S=" + std::to_string(S) +
+                                                       " (need T > 0, S >= 0, T >= S)");
+        q.N += (int64_t)T * (S + 1);
+        q.cols += T;
+        q.S_max = std::max(q.S_max, S);
+        q.T_max = std::max(q.T_max, T);
+    }
+    if (q.S_max + 1 > kMaxLabelsPlusOne)
+        return fail(RNNT_STATUS_INVALID_VALUE, "max label length " + std::to_string(q.S_max) + " exceeds " +
+                                                   std::to_string(kMaxLabelsPlusOne - 1));
+    if (p->num_rows >= 0 && p->num_rows != q.N)
+        return fail(RNNT_STATUS_INVALID_VALUE, "acts has " + std::to_string(p->num_rows) + " rows but sum_b T_b(S_b+1) = " +
+                                                   std::to_string(q.N));
+    q.align = p->alignment != nullptr;
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        const size_t at = o;
+        o = align_up(o + bytes);
+        return at;
+    };
+    q.off_row = take(sizeof(int64_t) * (q.B + 1));
+    q.off_col = take(sizeof(int64_t) * (q.B + 1));
+    q.off_mtmp = q.align ? take(sizeof(int) * (q.cols + q.B)) : 0;
+    q.off_min = q.align ? take(sizeof(int) * q.cols) : 0;
+    q.off_max = q.align ? take(sizeof(int) * q.cols) : 0;
+    q.off_den = take(sizeof(float) * q.N);
+    q.off_lpb = take(sizeof(double) * (q.N + 2 * kLpPad));
+    q.off_lpe = take(sizeof(double) * (q.N + 2 * kLpPad));
+    q.off_alpha = take(sizeof(double) * q.N);
+    q.off_beta = take(sizeof(double) * q.N);
+    q.off_ll = take(sizeof(double) * q.B);
+    q.off_llb = take(sizeof(double) * q.B);
+    q.total = o;
+    *pl = q;
+    return RNNT_STATUS_SUCCESS;
+}
+
+DevProblem make_dev(const mrnnt_problem *p, const Plan &pl, const void *ws) {
+    char *w = static_cast<char *>(const_cast<void *>(ws));
+    DevProblem d;
+    d.acts = p->acts;
+    d.labels = p->labels;
+    d.label_stride = p->label_stride;
+    d.T = p->T_dev;
+    d.S = p->S_dev;
+    d.row_off = reinterpret_cast<const int64_t *>(w + pl.off_row);
+    d.col_off = reinterpret_cast<const int64_t *>(w + pl.off_col);
+    d.min_s = pl.align ? reinterpret_cast<const int *>(w + pl.off_min) : nullptr;
+    d.max_s = pl.align ? reinterpret_cast<const int *>(w + pl.off_max) : nullptr;
+    d.B = pl.B;
+    d.V = pl.V;
+    d.blank = p->blank;
+    d.num_cols = pl.cols;
+    d.den = reinterpret_cast<float *>(w + pl.off_den);
+    d.lpb = reinterpret_cast<double *>(w + pl.off_lpb) + kLpPad;
+    d.lpe = reinterpret_cast<double *>(w + pl.off_lpe) + kLpPad;
+    d.alpha = reinterpret_cast<double *>(w + pl.off_alpha);
+    d.beta = reinterpret_cast<double *>(w + pl.off_beta);
+    d.ll = reinterpret_cast<double *>(w + pl.off_ll);
+    d.llb = reinterpret_cast<double *>(w + pl.off_llb);
+    return d;
+}
+
+RNNTStatus check_pointers(const mrnnt_problem *p) {
+    if (!p->acts) return fail(RNNT_STATUS_INVALID_VALUE, "acts is null");
+    if (!p->T_dev || !p->S_dev) return fail(RNNT_STATUS_INVALID_VALUE, "device lengths are required");
+    if (!p->labels) return fail(RNNT_STATUS_INVALID_VALUE, "labels is null");
+    return RNNT_STATUS_SUCCESS;
+}
+
+// ---- device properties -------------------------------------------------------------------------
+
+int streaming_grid(int64_t cols) {
+    static int cu_count[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    if (cu_count[dev] == 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cu_count[dev] = n;
+    }
+    // persistent grid: 8 workgroups of 4 waves per CU (32 waves/CU), never more than the columns
+    const int64_t g = (int64_t)cu_count[dev] * 8;
+    return (int)std::max<int64_t>(1, std::min<int64_t>(g, cols));
+}
+
+// ---- profiling ---------------------------------------------------------------------------------
+
+struct ProfRec {
+    int id;
+    hipEvent_t a, b;
+};
+std::mutex g_prof_mu;
+bool g_prof_on = false;
+std::vector<ProfRec> g_prof;
+
+template <class F>
+hipError_t timed(int id, hipStream_t s, F &&launch) {
+    bool on;
+    {
+        std::lock_guard<std::mutex> lk(g_prof_mu);
+        on = g_prof_on;
+    }
+    if (!on) return launch();
+    ProfRec r{id, nullptr, nullptr};
+    if (hipEventCreate(&r.a) != hipSuccess || hipEventCreate(&r.b) != hipSuccess) return launch();
+    (void)hipEventRecord(r.a, s);
+    const hipError_t e = launch();
+    (void)hipEventRecord(r.b, s);
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    g_prof.push_back(r);
+    return e;
+}
+
+}  // namespace
+
+// =================================================================================================
+// flat C ABI
+
+extern "C" {
+
+int mrnnt_version(void) { return MRNNT_VERSION; }
+
+const char *mrnnt_last_error(void) { return g_last_error.c_str(); }
+
+RNNTStatus mrnnt_workspace_size(const mrnnt_problem *p, size_t *bytes) {
+    if (!bytes) return fail(RNNT_STATUS_INVALID_VALUE, "null size pointer");
+    Plan pl;
+    const RNNTStatus st = make_plan(p, &pl);
+    if (st != RNNT_STATUS_SUCCESS) return st;
+    *bytes = pl.total;
+    return RNNT_STATUS_SUCCESS;
+}
+
+RNNTStatus mrnnt_forward(const mrnnt_problem *p, void *ws, size_t ws_bytes, float *costs_dev, int with_beta,
+                         hipStream_t stream) {
+    Plan pl;
+    RNNTStatus st = make_plan(p, &pl);
+    if (st != RNNT_STATUS_SUCCESS) return st;
+    if ((st = check_pointers(p)) != RNNT_STATUS_SUCCESS) return st;
+    if (!ws || ws_bytes < pl.total)
+        return fail(RNNT_STATUS_INVALID_VALUE, "workspace too small: need " + std::to_string(pl.total) + " bytes");
+    DevProblem d = make_dev(p, pl, ws);
+    char *w = static_cast<char *>(ws);
+    hipError_t e;
+    e = timed(K_SETUP, stream, [&] {
+        return launch_setup(p->T_dev, p->S_dev, pl.B, reinterpret_cast<int64_t *>(w + pl.off_row),
+                            reinterpret_cast<int64_t *>(w + pl.off_col), stream);
+    });
+    if (e != hipSuccess) return fail_hip(e, "setup kernel");
+    if (pl.align) {
+        e = timed(K_BAND, stream, [&] {
+            return launch_align(d, p->alignment, p->align_stride, p->align_blank, p->max_shift,
+                                reinterpret_cast<int *>(w + pl.off_mtmp), reinterpret_cast<int *>(w + pl.off_min),
+                                reinterpret_cast<int *>(w + pl.off_max), stream);
+        });
+        if (e != hipSuccess) return fail_hip(e, "alignment band kernels");
+    }
+    const int grid = streaming_grid(pl.cols);
+    e = timed(K_SOFTMAX, stream, [&] { return launch_softmax(d, grid, stream); });
+    if (e != hipSuccess) return fail_hip(e, "log-softmax kernel");
+    e = timed(K_DP, stream, [&] { return launch_dp(d, pl.S_max, with_beta ? 1 : 0, costs_dev, stream); });
+    if (e != hipSuccess) return fail_hip(e, "alpha/beta kernel");
+    return RNNT_STATUS_SUCCESS;
+}
+
+RNNTStatus mrnnt_backward(const mrnnt_problem *p, const void *ws, const float *grad_scale, float *grads,
+                          hipStream_t stream) {
+    Plan pl;
+    RNNTStatus st = make_plan(p, &pl);
+    if (st != RNNT_STATUS_SUCCESS) return st;
+    if ((st = check_pointers(p)) != RNNT_STATUS_SUCCESS) return st;
+    if (!ws) return fail(RNNT_STATUS_INVALID_VALUE, "workspace is null");
+    if (!grads) return fail(RNNT_STATUS_INVALID_VALUE, "grads is null");
+    DevProblem d = make_dev(p, pl, ws);
+    const int grid = streaming_grid(pl.cols);
+    const hipError_t e = timed(K_GRAD, stream, [&] { return launch_grad(d, grad_scale, grads, grid, stream); });
+    if (e != hipSuccess) return fail_hip(e, "gradient kernel");
+    return RNNT_STATUS_SUCCESS;
+}
+
+RNNTStatus mrnnt_cost_and_grad(const mrnnt_problem *p, void *ws, size_t ws_bytes, float *costs_dev, float *grads,
+                               const float *grad_scale, hipStream_t stream) {
+    RNNTStatus st = mrnnt_forward(p, ws, ws_bytes, costs_dev, grads != nullptr, stream);
+    if (st != RNNT_STATUS_SUCCESS || grads == nullptr) return st;
+    return mrnnt_backward(p, ws, grad_scale, grads, stream);
+}
+
+RNNTStatus mrnnt_read_loglik(const mrnnt_problem *p, const void *ws, double *ll_fwd_dev, double *ll_bwd_dev,
+                             hipStream_t stream) {
+    Plan pl;
+    RNNTStatus st = make_plan(p, &pl);
+    if (st != RNNT_STATUS_SUCCESS) return st;
+    const char *w = static_cast<const char *>(ws);
+    if (ll_fwd_dev && hipMemcpyAsync(ll_fwd_dev, w + pl.off_ll, sizeof(double) * pl.B, hipMemcpyDeviceToDevice,
+                                     stream) != hipSuccess)
+        return fail(RNNT_STATUS_MEMOPS_FAILED, "copy ll_fwd");
+    if (ll_bwd_dev && hipMemcpyAsync(ll_bwd_dev, w + pl.off_llb, sizeof(double) * pl.B, hipMemcpyDeviceToDevice,
+                                     stream) != hipSuccess)
+        return fail(RNNT_STATUS_MEMOPS_FAILED, "copy ll_bwd");
+    return RNNT_STATUS_SUCCESS;
+}
+
+void mrnnt_profile_enable(int enable) {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    for (auto &r : g_prof) {
+        (void)hipEventDestroy(r.a);
+        (void)hipEventDestroy(r.b);
+    }
+    g_prof.clear();
+    g_prof_on = enable != 0;
+}
+
+int mrnnt_profile_read(double *total_ms, int64_t *launches, int n) {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    for (int i = 0; i < n; ++i) {
+        if (total_ms) total_ms[i] = 0.0;
+        if (launches) launches[i] = 0;
+    }
+    int bad = 0;
+    for (auto &r : g_prof) {
+        if (hipEventSynchronize(r.b) != hipSuccess) {
+            ++bad;
+            continue;
+        }
+        float ms = 0.0f;
+        if (hipEventElapsedTime(&ms, r.a, r.b) != hipSuccess) {
+            ++bad;
+            continue;
+        }
+        if (r.id < n) {
+            if (total_ms) total_ms[r.id] += ms;
+            if (launches) launches[r.id] += 1;
+        }
+    }
+    return bad;
+}
+
+RNNTStatus mrnnt_synth_acts(float *out, int64_t begin, int64_t count, uint64_t seed, int normal, hipStream_t stream) {
+    const hipError_t e = launch_synth(out, begin, count, seed, normal, stream);
+    if (e != hipSuccess) return fail_hip(e, "synth kernel");
+    return RNNT_STATUS_SUCCESS;
+}
+
+}  // extern "C"
+
+// =================================================================================================
+// reference-shaped C++ surface: GpuRNNTWorkspaceManager<float>, GpuRNNTComputer<float>,
+// compute_rnnt_loss (reference gpu_workspace_manager.h, gpu_rnnt.h, src/rnnt_entrypoint.cpp)
+
+struct mrnnt_gpu_ws_state {
+    const float *acts;
+    const int *labels;
+    int B, V;
+    const int *T_dev;
+    const int *S_dev;
+    void *workspace = nullptr;
+    bool owned = false;
+    const int *alignment = nullptr;
+    int max_shift = 0;
+    int align_blank = 0;
+};
+
+namespace {
+
+// Host copies of T/S (the reference does the same blocking D2H copies, gpu_workspace_manager.h:87-96).
+bool host_lengths(const mrnnt_gpu_ws_state *s, std::vector<int> &T, std::vector<int> &S) {
+    T.assign(s->B, 0);
+    S.assign(s->B, 0);
+    if (s->B <= 0) return true;
+    if (hipMemcpy(T.data(), s->T_dev, sizeof(int) * s->B, hipMemcpyDeviceToHost) != hipSuccess) return false;
+    if (hipMemcpy(S.data(), s->S_dev, sizeof(int) * s->B, hipMemcpyDeviceToHost) != hipSuccess) return false;
+    return true;
+}
+
+mrnnt_problem problem_of(const mrnnt_gpu_ws_state *s, const std::vector<int> &T, const std::vector<int> &S,
+                         int blank) {
+    mrnnt_problem p;
+    std::memset(&p, 0, sizeof(p));
+    p.B = s->B;
+    p.V = s->V;
+    p.blank = blank;
+    p.T_host = T.data();
+    p.S_host = S.data();
+    p.T_dev = s->T_dev;
+    p.S_dev = s->S_dev;
+    p.acts = s->acts;
+    p.labels = s->labels;
+    // reference quirks kept on this surface: label row stride = max(S) (gpu_rnnt_kernel.h:133),
+    // alignment row stride = max(T) (gpu_workspace_manager.h:200)
+    p.label_stride = S.empty() ? 0 : *std::max_element(S.begin(), S.end());
+    p.alignment = s->alignment;
+    p.align_stride = T.empty() ? 0 : *std::max_element(T.begin(), T.end());
+    p.align_blank = s->align_blank;
+    p.max_shift = s->max_shift;
+    p.num_rows = -1;
+    return p;
+}
+
+// The manager's workspace = the flat plan + B device floats for the costs.
+RNNTStatus manager_size(const mrnnt_gpu_ws_state *s, const std::vector<int> &T, const std::vector<int> &S,
+                        size_t *bytes, size_t *costs_off) {
+    mrnnt_problem p = problem_of(s, T, S, 0);
+    // size only depends on lengths and the alignment flag; blank range is checked at compute time
+    size_t b = 0;
+    const RNNTStatus st = mrnnt_workspace_size(&p, &b);
+    if (st != RNNT_STATUS_SUCCESS) return st;
+    *costs_off = align_up(b);
+    *bytes = *costs_off + align_up(sizeof(float) * std::max(1, s->B));
+    return RNNT_STATUS_SUCCESS;
+}
+
+RNNTStatus manager_compute(GpuRNNTWorkspaceManager<float> &wm, int blank, hipStream_t stream, float *costs,
+                           float *grads) {
+    mrnnt_gpu_ws_state *s = wm.state();
+    if (!costs) return fail(RNNT_STATUS_INVALID_VALUE, "costs is null");
+    if (!s->workspace) return fail(RNNT_STATUS_INVALID_VALUE, "workspace not set (set_workspace/create_workspace)");
+    std::vector<int> T, S;
+    if (!host_lengths(s, T, S)) return fail(RNNT_STATUS_MEMOPS_FAILED, "copying lengths to host");
+    size_t bytes = 0, coff = 0;
+    RNNTStatus st = manager_size(s, T, S, &bytes, &coff);
+    if (st != RNNT_STATUS_SUCCESS) return st;
+    mrnnt_problem p = problem_of(s, T, S, blank);
+    float *costs_dev = reinterpret_cast<float *>(static_cast<char *>(s->workspace) + coff);
+    st = mrnnt_cost_and_grad(&p, s->workspace, coff, costs_dev, grads, nullptr, stream);
+    if (st != RNNT_STATUS_SUCCESS) return st;
+    hipError_t e = hipMemcpyAsync(costs, costs_dev, sizeof(float) * s->B, hipMemcpyDeviceToHost, stream);
+    if (e != hipSuccess) return fail(RNNT_STATUS_MEMOPS_FAILED, std::string("costs D2H: ") + hipGetErrorString(e));
+    e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) return fail_hip(e, "stream synchronize");
+    return RNNT_STATUS_SUCCESS;
+}
+
+}  // namespace
+
+GpuRNNTWorkspaceManager<float>::GpuRNNTWorkspaceManager(const float *const acts, const int *const labels, const int B,
+                                                        const int *T, const int *S, const int V)
+    : st_(new mrnnt_gpu_ws_state) {
+    st_->acts = acts;
+    st_->labels = labels;
+    st_->B = B;
+    st_->V = V;
+    st_->T_dev = T;
+    st_->S_dev = S;
+}
+
+GpuRNNTWorkspaceManager<float>::~GpuRNNTWorkspaceManager() { delete st_; }
+
+RNNTStatus GpuRNNTWorkspaceManager<float>::get_workspace_size(size_t *size_bytes) const {
+    if (st_->B <= 0) return fail(RNNT_STATUS_INVALID_VALUE, "B must be > 0");
+    std::vector<int> T, S;
+    if (!host_lengths(st_, T, S)) return fail(RNNT_STATUS_MEMOPS_FAILED, "copying lengths to host");
+    size_t coff = 0;
+    // alignment may be registered later: size for the restricted layout so either works
+    mrnnt_gpu_ws_state tmp = *st_;
+    int dummy = 0;
+    tmp.alignment = &dummy;
+    return manager_size(&tmp, T, S, size_bytes, &coff);
+}
+
+void GpuRNNTWorkspaceManager<float>::set_workspace(void *workspace) {
+    if (st_->owned && st_->workspace && st_->workspace != workspace) (void)hipFree(st_->workspace);
+    st_->workspace = workspace;
+    st_->owned = false;
+}
+
+RNNTStatus GpuRNNTWorkspaceManager<float>::create_workspace() {
+    size_t bytes = 0;
+    const RNNTStatus st = get_workspace_size(&bytes);
+    if (st != RNNT_STATUS_SUCCESS) return st;
+    void *w = nullptr;
+    if (hipMalloc(&w, bytes) != hipSuccess) return fail(RNNT_STATUS_MEMOPS_FAILED, "hipMalloc workspace");
+    set_workspace(w);
+    st_->owned = true;
+    return RNNT_STATUS_SUCCESS;
+}
+
+void GpuRNNTWorkspaceManager<float>::free_workspace() {
+    if (st_->workspace) (void)hipFree(st_->workspace);
+    st_->workspace = nullptr;
+    st_->owned = false;
+}
+
+void GpuRNNTWorkspaceManager<float>::restrict_to_alignment(const int *const alignments, int max_shift, int blank_idx) {
+    st_->alignment = alignments;
+    st_->max_shift = max_shift;
+    st_->align_blank = blank_idx;
+}
+
+int GpuRNNTWorkspaceManager<float>::B_host() const { return st_->B; }
+int GpuRNNTWorkspaceManager<float>::V_host() const { return st_->V; }
+
+std::vector<int> GpuRNNTWorkspaceManager<float>::T_host() const {
+    std::vector<int> T, S;
+    host_lengths(st_, T, S);
+    return T;
+}
+
+std::vector<int> GpuRNNTWorkspaceManager<float>::S_host() const {
+    std::vector<int> T, S;
+    host_lengths(st_, T, S);
+    return S;
+}
+
+int GpuRNNTWorkspaceManager<float>::num_denoms() const {
+    std::vector<int> T, S;
+    host_lengths(st_, T, S);
+    int64_t n = 0;
+    for (size_t b = 0; b < T.size(); ++b) n += (int64_t)T[b] * (S[b] + 1);
+    return (int)n;
+}
+
+GpuRNNTComputer<float>::GpuRNNTComputer(GpuRNNTWorkspaceManager<float> &workspace_manager, int blank,
+                                        hipStream_t stream)
+    : workspace_manager_(workspace_manager), blank_(blank), stream_(stream) {}
+
+RNNTStatus GpuRNNTComputer<float>::cost_and_grad(float *costs, float *grads) {
+    return manager_compute(workspace_manager_, blank_, stream_, costs, grads);
+}
+
+RNNTStatus GpuRNNTComputer<float>::cost(float *costs) {
+    return manager_compute(workspace_manager_, blank_, stream_, costs, nullptr);
+}
+
+extern "C" RNNTStatus compute_rnnt_loss(RNNTWorkspaceManager &workspace_manager, RNNTOptions options, float *costs,
+                                        float *gradients) {
+    // src/rnnt_entrypoint.cpp:16-48
+    if (costs == nullptr) return fail(RNNT_STATUS_INVALID_VALUE, "costs is null");
+    if (options.loc == RNNT_CPU) {
+        std::fprintf(stderr, "CPU execution requested, but this is the MI355X (HIP) build of monotonic RNN-T\n");
+        return fail(RNNT_STATUS_EXECUTION_FAILED, "CPU execution requested, but this is the MI355X (HIP) build");
+    }
+    if (options.loc != RNNT_GPU) return fail(RNNT_STATUS_INVALID_VALUE, "unknown compute location");
+    auto *gm = dynamic_cast<GpuRNNTWorkspaceManager<float> *>(&workspace_manager);
+    if (!gm) return fail(RNNT_STATUS_INVALID_VALUE, "workspace manager is not a GpuRNNTWorkspaceManager<float>");
+    GpuRNNTComputer<float> computer(*gm, options.blank_label, options.stream);
+    return gradients != nullptr ? computer.cost_and_grad(costs, gradients) : computer.cost(costs);
+}

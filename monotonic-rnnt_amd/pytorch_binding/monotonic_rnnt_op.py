@@ -1,0 +1,225 @@
+"""PyTorch autograd surface of the MI355X monotonic RNN-T loss.
+
+Same public names, signatures and return conventions as the reference's
+pytorch_binding/monotonic_rnnt_op.py:
+  MonotonicRNNTFunction.apply(acts, labels, input_lengths, label_lengths,
+                              alignment=None, max_distance_from_alignment=0, blank_label=0) -> costs [B]
+  monotonic_rnnt_loss(...)                    (reference :121-163)
+  MonotonicRNNTLoss(blank_label=0)            (reference :166-217)
+  monotonic_rnnt_cpp.gpu_monotonic_rnnt(...) / .gpu_monotonic_rnnt_align_restrict(...)
+                                              (reference pybind names, monotonic_rnnt.cu:81-152)
+
+Execution goes through the C ABI of libmonotonic_rnnt_amd.so (HIP kernels on the current torch stream);
+there is no CPU or eager-PyTorch fallback -- CPU tensors raise.
+
+Behavioural differences from the reference, all deliberate:
+  * forward runs the log-softmax reduce and the alpha/beta recursion; the logit gradient is produced
+    in backward with dL/dcost[b] fused into the kernel (the reference writes grads in forward into a
+    zeros_like(acts) and rescales them in backward: 3 extra passes over an N x V tensor, :32-36, :96-118);
+  * costs are computed on the device (the reference computes into a host tensor and copies, :37, :90);
+  * labels / alignment use their true row strides (the reference assumes max(S) / max(T));
+  * MonotonicRNNTLoss.forward uses self.blank_label (the reference reads a missing self.blank, :214).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import numpy as np
+import torch
+
+try:
+    from . import _mrnnt_lib as _L
+except ImportError:  # imported with pytorch_binding/ on sys.path, like the reference's tests do
+    import _mrnnt_lib as _L
+
+_L.load()  # fail loudly at import if the HIP library is missing
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+class _Prepared:
+    """Device/host views of one call's inputs plus the filled mrnnt_problem."""
+
+    def __init__(self, acts, labels, input_lengths, label_lengths, alignment, max_shift, blank_label):
+        if not acts.is_cuda:
+            raise RuntimeError("monotonic_rnnt (MI355X build): acts must be a GPU tensor; "
+                               "this build has no CPU implementation")
+        if acts.dtype != torch.float32:
+            raise RuntimeError("monotonic_rnnt: acts must be float32 (reference monotonic_rnnt.cu:19,84)")
+        if acts.dim() != 2:
+            raise RuntimeError("monotonic_rnnt: acts must be packed 2-D [sum_b T_b (S_b+1), V]")
+        dev = acts.device
+        self.acts = acts.contiguous()
+        B = labels.size(0)
+        self.T_host = np.ascontiguousarray(input_lengths.detach().to("cpu", torch.int32).numpy()).reshape(-1)
+        self.S_host = np.ascontiguousarray(label_lengths.detach().to("cpu", torch.int32).numpy()).reshape(-1)
+        if self.T_host.size != B or self.S_host.size != B:
+            raise RuntimeError(f"monotonic_rnnt: expected {B} input/label lengths, "
+                               f"got {self.T_host.size}/{self.S_host.size}")
+        self.T_dev = input_lengths.detach().to(dev, torch.int32).contiguous()
+        self.S_dev = label_lengths.detach().to(dev, torch.int32).contiguous()
+        lab = labels.detach().to(dev, torch.int32)
+        if lab.dim() == 1:
+            lab = lab.view(B, -1)
+        self.labels = lab.contiguous() if lab.numel() else torch.zeros(B, 1, dtype=torch.int32, device=dev)
+        self.alignment = None
+        if alignment is not None:
+            al = alignment.detach().to(dev, torch.int32)
+            self.alignment = (al.view(B, -1) if al.dim() == 1 else al).contiguous()
+        p = _L.MrnntProblem()
+        p.B = B
+        p.V = self.acts.size(1)
+        p.blank = int(blank_label)
+        p.max_shift = int(max_shift)
+        p.T_host = self.T_host.ctypes.data
+        p.S_host = self.S_host.ctypes.data
+        p.T_dev = self.T_dev.data_ptr()
+        p.S_dev = self.S_dev.data_ptr()
+        p.acts = self.acts.data_ptr()
+        p.labels = self.labels.data_ptr()
+        p.label_stride = self.labels.size(1)
+        p.alignment = self.alignment.data_ptr() if self.alignment is not None else None
+        p.align_stride = self.alignment.size(1) if self.alignment is not None else 0
+        p.align_blank = int(blank_label)  # the reference parses the alignment with the same blank (monotonic_rnnt.cu:144)
+        p.num_rows = self.acts.size(0)
+        self.problem = p
+        self.device = dev
+
+    def workspace(self) -> torch.Tensor:
+        n = ctypes.c_size_t(0)
+        _L.check(_L.load().mrnnt_workspace_size(ctypes.byref(self.problem), ctypes.byref(n)), "workspace_size")
+        return torch.empty(max(1, n.value), dtype=torch.uint8, device=self.device)
+
+    def stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+
+def _forward(prep: _Prepared, with_beta: bool):
+    ws = prep.workspace()
+    costs = torch.empty(prep.problem.B, dtype=torch.float32, device=prep.device)
+    _L.check(_L.load().mrnnt_forward(ctypes.byref(prep.problem), _ptr(ws), ws.numel(), _ptr(costs),
+                                     1 if with_beta else 0, prep.stream()), "mrnnt_forward")
+    return costs, ws
+
+
+def _backward(prep: _Prepared, ws: torch.Tensor, grad_scale: Optional[torch.Tensor]) -> torch.Tensor:
+    grads = torch.empty_like(prep.acts)
+    if grad_scale is not None:
+        grad_scale = grad_scale.detach().to(prep.device, torch.float32).contiguous()
+    _L.check(_L.load().mrnnt_backward(ctypes.byref(prep.problem), _ptr(ws), _ptr(grad_scale), _ptr(grads),
+                                      prep.stream()), "mrnnt_backward")
+    return grads
+
+
+class MonotonicRNNTFunction(torch.autograd.Function):
+    """reference pytorch_binding/monotonic_rnnt_op.py:18-118"""
+
+    @staticmethod
+    def forward(ctx, acts: torch.Tensor, labels: torch.Tensor, input_lengths: torch.Tensor,
+                label_lengths: torch.Tensor, alignment: Optional[torch.Tensor] = None,
+                max_distance_from_alignment: int = 0, blank_label: int = 0) -> torch.Tensor:
+        prep = _Prepared(acts, labels, input_lengths, label_lengths, alignment, max_distance_from_alignment,
+                         blank_label)
+        need_grad = bool(ctx.needs_input_grad[0])
+        costs, ws = _forward(prep, with_beta=need_grad)
+        if need_grad:
+            # acts is re-read by the gradient kernel; saving it lets autograd catch in-place edits
+            ctx.save_for_backward(acts)
+            ctx.prep = prep
+            ctx.ws = ws
+        return costs
+
+    @staticmethod
+    def backward(ctx, grad_outputs):
+        (acts,) = ctx.saved_tensors
+        prep, ws = ctx.prep, ctx.ws
+        grads = _backward(prep, ws, grad_outputs)
+        ctx.prep = None
+        ctx.ws = None
+        return grads, None, None, None, None, None, None
+
+
+def monotonic_rnnt_loss(acts: torch.Tensor, labels: torch.Tensor, input_lengths: torch.Tensor,
+                        label_lengths: torch.Tensor, alignment: Optional[torch.Tensor] = None,
+                        max_distance_from_alignment: int = 0, blank_label: int = 0) -> torch.Tensor:
+    """Computes the monotonic RNN-T loss between a sequence of activations and a ground truth labeling.
+
+    Args (reference monotonic_rnnt_op.py:130-160):
+        acts:           packed 2-D float32 GPU tensor of logits, (sum_b T_b*(S_b+1), V), utterance b
+                        contiguous, then t-major, then s. Softmax is applied internally.
+        labels:         2-D int tensor [B, max_b S_b] of padded label sequences.
+        input_lengths:  1-D int tensor [B] of T_b.
+        label_lengths:  1-D int tensor [B] of S_b.
+        alignment:      optional [B, max_b T_b] int tensor; restricts paths to within
+                        max_distance_from_alignment frames of it.
+        blank_label:    index of the blank symbol.
+    Returns:
+        1-D float tensor [B] of costs (negative log probabilities) on acts.device.
+    """
+    result = MonotonicRNNTFunction.apply(acts, labels, input_lengths, label_lengths, alignment,
+                                         max_distance_from_alignment, blank_label)
+    assert result is not None
+    return result
+
+
+class MonotonicRNNTLoss(torch.nn.Module):
+    """reference monotonic_rnnt_op.py:166-217 (with the self.blank -> self.blank_label fix)."""
+
+    def __init__(self, blank_label: int = 0) -> None:
+        super().__init__()
+        self.blank_label = blank_label
+        self.loss = MonotonicRNNTFunction.apply
+
+    def forward(self, acts: torch.Tensor, labels: torch.Tensor, input_lengths: torch.Tensor,
+                label_lengths: torch.Tensor, alignment: Optional[torch.Tensor] = None,
+                max_distance_from_alignment: int = 0) -> torch.Tensor:
+        loss = self.loss(acts, labels, input_lengths, label_lengths, alignment, max_distance_from_alignment,
+                         self.blank_label)
+        assert loss is not None
+        return loss
+
+
+class _Ext:
+    """The reference's pybind extension functions (monotonic_rnnt.cu:155-164), same argument order.
+
+    gpu_*: costs may live on any device (the reference takes a host tensor); grads [N, V] on the GPU
+    (an empty tensor = cost only). Return 0 (RNNT_STATUS_SUCCESS) or raise RuntimeError.
+    cpu_*: not available in this build (raises).
+    """
+
+    @staticmethod
+    def _run(acts, labels, input_lengths, label_lengths, alignment, k, costs, grads, blank_label):
+        prep = _Prepared(acts, labels, input_lengths, label_lengths, alignment, k, blank_label)
+        want = grads is not None and grads.numel() > 0
+        c, ws = _forward(prep, with_beta=want)
+        if want:
+            if not grads.is_cuda or grads.dtype != torch.float32 or not grads.is_contiguous():
+                raise RuntimeError("grads must be a contiguous float32 GPU tensor")
+            _L.check(_L.load().mrnnt_backward(ctypes.byref(prep.problem), _ptr(ws), None, _ptr(grads),
+                                              prep.stream()), "mrnnt_backward")
+        costs.copy_(c)
+        return _L.RNNT_STATUS_SUCCESS
+
+    def gpu_monotonic_rnnt(self, acts, labels, input_lengths, label_lengths, costs, grads, blank_label,
+                           num_threads=0):
+        return self._run(acts, labels, input_lengths, label_lengths, None, 0, costs, grads, blank_label)
+
+    def gpu_monotonic_rnnt_align_restrict(self, acts, labels, input_lengths, label_lengths, alignment,
+                                          max_distance_from_alignment, costs, grads, blank_label, num_threads=0):
+        return self._run(acts, labels, input_lengths, label_lengths, alignment, max_distance_from_alignment,
+                         costs, grads, blank_label)
+
+    def cpu_monotonic_rnnt(self, *args, **kwargs):
+        raise RuntimeError("cpu_monotonic_rnnt: this is the MI355X (HIP) build; move tensors to the GPU")
+
+    def cpu_monotonic_rnnt_align_restrict(self, *args, **kwargs):
+        raise RuntimeError("cpu_monotonic_rnnt_align_restrict: this is the MI355X (HIP) build; "
+                           "move tensors to the GPU")
+
+
+monotonic_rnnt_cpp = _Ext()
+
+__all__ = ["MonotonicRNNTFunction", "monotonic_rnnt_loss", "MonotonicRNNTLoss", "monotonic_rnnt_cpp"]

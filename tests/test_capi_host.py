@@ -1,0 +1,120 @@
+"""Host-side tests of the C-ABI library (no GPU needed): it loads, exports every symbol the headers in
+include/ declare, and the host-only planning/validation behaves like the reference
+(cpu_workspace_manager.h:99-107 / gpu_workspace_manager.h:228-239)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+INC = os.path.join(ROOT, "include")
+LIB = os.path.join(ROOT, "monotonic-rnnt_amd", "libmonotonic_rnnt_amd.so")
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(LIB):
+        subprocess.run(["make", "-s", "-j8", "-C", os.path.join(ROOT, "monotonic-rnnt_amd")], check=True)
+    import _mrnnt_lib
+    return _mrnnt_lib.load()
+
+
+def _exported():
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True, check=True).stdout
+    dem = subprocess.run(["c++filt"], input=out, capture_output=True, text=True, check=True).stdout
+    return dem
+
+
+def _declared_c_functions():
+    names = set()
+    for h in ("mrnnt.h", "rnnt_entrypoint.h"):
+        src = open(os.path.join(INC, h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        src = re.sub(r"//[^\n]*", "", src)
+        for m in re.finditer(r"\b(mrnnt_\w+|compute_rnnt_loss)\s*\(", src):
+            names.add(m.group(1))
+    return names
+
+
+def test_library_exports_every_declared_c_symbol(lib):
+    exported = _exported()
+    declared = _declared_c_functions()
+    assert "compute_rnnt_loss" in declared and "mrnnt_forward" in declared
+    missing = [n for n in sorted(declared) if not re.search(r"\sT\s" + n + r"\b", exported)]
+    assert not missing, missing
+
+
+def test_library_exports_reference_cpp_classes(lib):
+    exported = _exported()
+    for method in ["GpuRNNTWorkspaceManager<float>::GpuRNNTWorkspaceManager(float const*, int const*, int, int const*, int const*, int)",
+                   "GpuRNNTWorkspaceManager<float>::get_workspace_size(unsigned long*) const",
+                   "GpuRNNTWorkspaceManager<float>::set_workspace(void*)",
+                   "GpuRNNTWorkspaceManager<float>::create_workspace()",
+                   "GpuRNNTWorkspaceManager<float>::free_workspace()",
+                   "GpuRNNTWorkspaceManager<float>::restrict_to_alignment(int const*, int, int)",
+                   "GpuRNNTComputer<float>::cost_and_grad(float*, float*)",
+                   "GpuRNNTComputer<float>::cost(float*)",
+                   "GpuRNNTComputer<float>::GpuRNNTComputer(GpuRNNTWorkspaceManager<float>&, int, ihipStream_t*)"]:
+        assert method in exported, method
+
+
+def test_c_header_compiles_as_c():
+    # the flat ABI header must be consumable from plain C (cgo / JNI / N-API stubs)
+    src = '#include "mrnnt.h"\nint main(void){ mrnnt_problem p; (void)p; return (int)RNNT_STATUS_SUCCESS; }\n'
+    r = subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", "-I", INC, "-x", "c", "-", "-fsyntax-only"],
+                       input=src, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+def _problem(T, S, V=8, blank=0, rows=-1):
+    import _mrnnt_lib as L
+    T = np.asarray(T, np.int32)
+    S = np.asarray(S, np.int32)
+    p = L.MrnntProblem()
+    p.B, p.V, p.blank = len(T), V, blank
+    p.T_host, p.S_host = T.ctypes.data, S.ctypes.data
+    p.num_rows = rows
+    return p, (T, S)
+
+
+def test_workspace_size_and_validation(lib):
+    import _mrnnt_lib as L
+    n = ctypes.c_size_t(0)
+    p, keep = _problem([4, 7], [2, 7])
+    assert lib.mrnnt_workspace_size(ctypes.byref(p), ctypes.byref(n)) == L.RNNT_STATUS_SUCCESS
+    rows = 4 * 3 + 7 * 8
+    assert n.value >= rows * (4 + 4 * 8)  # den + lpb/lpe/alpha/beta
+    for T, S in (([4], [5]), ([0], [0]), ([3], [-1])):  # T < S, T == 0, S < 0 -> INVALID_VALUE
+        p, keep = _problem(T, S)
+        assert lib.mrnnt_workspace_size(ctypes.byref(p), ctypes.byref(n)) == L.RNNT_STATUS_INVALID_VALUE
+        assert b"invalid lengths" in lib.mrnnt_last_error()
+    p, keep = _problem([4], [2], rows=11)  # acts rows disagree with lengths
+    assert lib.mrnnt_workspace_size(ctypes.byref(p), ctypes.byref(n)) == L.RNNT_STATUS_INVALID_VALUE
+    p, keep = _problem([4], [2], V=3, blank=3)  # blank out of range
+    assert lib.mrnnt_workspace_size(ctypes.byref(p), ctypes.byref(n)) == L.RNNT_STATUS_INVALID_VALUE
+
+
+def test_forward_rejects_bad_arguments_without_touching_gpu(lib):
+    import _mrnnt_lib as L
+    p, keep = _problem([4], [2])  # no device pointers -> INVALID_VALUE before any HIP call
+    assert lib.mrnnt_forward(ctypes.byref(p), None, 0, None, 1, None) == L.RNNT_STATUS_INVALID_VALUE
+
+
+def test_status_strings_match_reference_enum():
+    src = open(os.path.join(INC, "status.h")).read()
+    for name, val in (("SUCCESS", 0), ("MEMOPS_FAILED", 1), ("INVALID_VALUE", 2), ("EXECUTION_FAILED", 3),
+                      ("UNKNOWN_ERROR", 4)):
+        assert re.search(rf"RNNT_STATUS_{name}\s*=\s*{val}", src)
+
+
+def test_torch_op_rejects_cpu_tensors():
+    import torch
+    import monotonic_rnnt_op as op
+    acts = torch.zeros(12, 3)
+    with pytest.raises(RuntimeError, match="GPU"):
+        op.monotonic_rnnt_loss(acts, torch.tensor([[1, 2]], dtype=torch.int32), torch.tensor([4]), torch.tensor([2]))
+    with pytest.raises(RuntimeError):
+        op.monotonic_rnnt_cpp.cpu_monotonic_rnnt(acts, None, None, None, None, None, 0, 0)

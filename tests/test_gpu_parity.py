@@ -1,0 +1,242 @@
+"""Parity of the HIP path (through the C ABI, via the autograd surface) against the oracle.
+
+Oracle = oracle/rnnt_oracle.c at double precision = cpu_rnnt.h<double> on the same fp32 inputs
+(pinned bit-exact to the reference in tests/test_oracle.py). Tolerances (north star):
+    costs : |dc| <= 1e-4 * max(1, |c|)      (relative for large costs: 1e-4 abs is < 1 ulp at |c| ~ 1e3)
+    grads : max |dg| <= 1e-4                 (absolute, fp32)
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+FIXTURES = sorted(glob.glob(os.path.join(GOLD, "*.npz")))
+COST_TOL = 1e-4
+GRAD_TOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def op():
+    import monotonic_rnnt_op
+    return monotonic_rnnt_op
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    return torch.device("cuda:0")
+
+
+def run_gpu(op, dev, acts, labels, T, S, blank=0, alignment=None, k=0, scale=None, grads=True):
+    a = torch.from_numpy(np.ascontiguousarray(acts, np.float32)).to(dev).requires_grad_(grads)
+    lab = torch.from_numpy(np.ascontiguousarray(labels, np.int32)).to(dev)
+    Tt = torch.from_numpy(np.asarray(T, np.int32)).to(dev)
+    St = torch.from_numpy(np.asarray(S, np.int32)).to(dev)
+    al = None if alignment is None else torch.from_numpy(np.asarray(alignment, np.int32)).to(dev)
+    costs = op.monotonic_rnnt_loss(a, lab, Tt, St, al, k, blank)
+    g = None
+    if grads:
+        sc = torch.ones(len(T), device=dev) if scale is None else torch.as_tensor(scale, dtype=torch.float32,
+                                                                                  device=dev)
+        (costs * sc).sum().backward()
+        g = a.grad.detach().cpu().numpy()
+    torch.cuda.synchronize()
+    return costs.detach().cpu().numpy().astype(np.float64), g
+
+
+def assert_costs(c, ref):
+    fin = np.isfinite(ref)
+    assert np.array_equal(np.isfinite(c), fin), (c, ref)
+    if fin.any():
+        err = np.abs(c[fin] - ref[fin]) / np.maximum(1.0, np.abs(ref[fin]))
+        assert err.max() <= COST_TOL, (err.max(), c, ref)
+
+
+def assert_grads(g, ref):
+    assert g.shape == ref.shape
+    fin = np.isfinite(ref)
+    assert np.array_equal(np.isfinite(g), fin)
+    err = np.abs(g[fin] - ref[fin]).max() if fin.any() else 0.0
+    assert err <= GRAD_TOL, err
+
+
+def random_problem(rng, B, Trange, Smax, V, dist="normal", force=None):
+    T = rng.integers(Trange[0], Trange[1] + 1, B).astype(np.int32)
+    S = np.array([rng.integers(0, min(t, Smax) + 1) for t in T], np.int32)
+    for b, (t, s) in (force or {}).items():
+        T[b], S[b] = t, s
+    rows = int(np.sum(T.astype(np.int64) * (S + 1)))
+    acts = (rng.standard_normal((rows, V)) if dist == "normal" else rng.random((rows, V))).astype(np.float32)
+    labels = rng.integers(1, V, (B, max(1, int(S.max())))).astype(np.int32)
+    return acts, labels, T, S
+
+
+# ---------------------------------------------------------------------------------------------
+# golden vectors from the reference (tests/golden)
+
+@pytest.mark.parametrize("path", FIXTURES, ids=[os.path.basename(p)[:-4] for p in FIXTURES])
+def test_golden_cost_and_grad(op, dev, path):
+    fx = dict(np.load(path))
+    kw = dict(blank=int(fx["blank"]), alignment=fx.get("alignment"), k=int(fx.get("max_shift", 0)))
+    c, g = run_gpu(op, dev, fx["acts"], fx["labels"], fx["T"], fx["S"], **kw)
+    assert_costs(c, fx["costs_f64"])
+    assert_grads(g, fx["grads_f64"])
+    c_only, _ = run_gpu(op, dev, fx["acts"], fx["labels"], fx["T"], fx["S"], grads=False, **kw)
+    assert_costs(c_only, fx["costs_only_f64"])
+
+
+def test_reference_known_answers(op, dev):
+    fx = dict(np.load(os.path.join(GOLD, "toy.npz")))
+    c, g = run_gpu(op, dev, fx["acts"], fx["labels"], fx["T"], fx["S"])
+    assert abs(c[0] - (-np.log(0.363))) < 1e-4  # tests/test_gpu.cu fwd_test
+    # pytorch_binding/test.py:64-66 expected grads at 1e-2
+    expected = np.array([0.04, -0.14, 0.1, 0, 0, 0, 0, 0, 0, 0.13, -0.19, 0.06, -0.04, 0.04, -0.01, 0, 0, 0,
+                         0.06, -0.1, 0.04, 0.01, 0.07, -0.08, -0.06, 0.04, 0.02, 0, 0, 0, 0.14, 0.05, -0.19,
+                         -0.11, 0.05, 0.05]).reshape(12, 3)
+    assert np.abs(g - expected).max() < 1e-2
+    # pytorch_binding/test.py:71-130
+    c1, _ = run_gpu(op, dev, fx["acts"], fx["labels"], fx["T"], fx["S"], alignment=[[0, 1, 0, 2]], k=1)
+    assert abs(c1[0] - 1.22) < 1e-2
+    c2, _ = run_gpu(op, dev, fx["acts"], fx["labels"], fx["T"], fx["S"], alignment=[[1, 2, 0, 0]], k=0)
+    assert abs(c2[0] - 2.7) < 1e-2
+
+
+def test_out_of_band_rows_are_exact_zero(op, dev):
+    fx = dict(np.load(os.path.join(GOLD, "toy.npz")))
+    _, g = run_gpu(op, dev, fx["acts"], fx["labels"], fx["T"], fx["S"])
+    for r in (1, 2, 5, 9):  # (t,s) = (0,1) (0,2) (1,2) (3,0)
+        assert np.all(g[r] == 0.0)
+
+
+# ---------------------------------------------------------------------------------------------
+# random problems vs the oracle
+
+@pytest.mark.parametrize("V", [3, 15, 16, 64, 100, 256, 1000, 1001, 1024, 2052])
+def test_random_ragged_vs_oracle(op, dev, V):
+    rng = np.random.default_rng(V)
+    acts, labels, T, S = random_problem(rng, 5, (1, 40), 12, V, force={0: (1, 0), 1: (9, 9), 2: (17, 0)})
+    blank = 0 if V % 2 else V - 1
+    if blank:
+        labels = np.where(labels == blank, 0, labels).astype(np.int32)
+    c, g = run_gpu(op, dev, acts, labels, T, S, blank=blank)
+    cr, gr = O.oracle_rnnt(acts, labels, T, S, blank=blank)
+    assert_costs(c, cr)
+    assert_grads(g, gr)
+
+
+@pytest.mark.parametrize("k", [0, 1, 3])
+def test_alignment_restricted_vs_oracle(op, dev, k):
+    rng = np.random.default_rng(100 + k)
+    acts, labels, T, S = random_problem(rng, 4, (10, 50), 10, 64)
+    al = np.zeros((4, int(T.max()) + 3), np.int32)  # wider than max(T): true row stride is honoured
+    for b in range(4):
+        pos = np.sort(rng.choice(T[b], S[b], replace=False))
+        al[b, pos] = labels[b, : S[b]]
+    c, g = run_gpu(op, dev, acts, labels, T, S, alignment=al, k=k)
+    cr, gr = O.oracle_rnnt(acts, labels, T, S, alignment=al, max_shift=k)
+    assert_costs(c, cr)
+    assert_grads(g, gr)
+
+
+def test_grad_output_scaling_fused(op, dev):
+    rng = np.random.default_rng(5)
+    acts, labels, T, S = random_problem(rng, 4, (5, 30), 8, 128)
+    scale = np.array([2.5, -1.0, 0.0, 0.3], np.float32)
+    c, g = run_gpu(op, dev, acts, labels, T, S, scale=scale)
+    cr, gr = O.oracle_rnnt(acts, labels, T, S)
+    gr = gr * np.repeat(scale.astype(np.float64), T * (S + 1))[:, None]
+    assert_costs(c, cr)
+    assert_grads(g, gr)
+
+
+def test_reference_extension_functions(op, dev):
+    """monotonic_rnnt_cpp.gpu_monotonic_rnnt[_align_restrict] (reference monotonic_rnnt.cu:81-152)."""
+    fx = dict(np.load(os.path.join(GOLD, "multibatch.npz")))
+    acts = torch.from_numpy(fx["acts"]).to(dev)
+    labels = torch.from_numpy(fx["labels"]).to(dev)
+    T = torch.from_numpy(fx["T"]).to(dev)
+    S = torch.from_numpy(fx["S"]).to(dev)
+    costs = torch.zeros(2)  # host tensor, as the reference passes it
+    grads = torch.zeros_like(acts)
+    assert op.monotonic_rnnt_cpp.gpu_monotonic_rnnt(acts, labels, T, S, costs, grads, 0, 0) == 0
+    assert_costs(costs.numpy().astype(np.float64), fx["costs_f64"])
+    assert_grads(grads.cpu().numpy(), fx["grads_f64"])
+    fx = dict(np.load(os.path.join(GOLD, "align_multibatch_k1.npz")))
+    acts = torch.from_numpy(fx["acts"]).to(dev)
+    costs = torch.zeros(2)
+    grads = torch.zeros_like(acts)
+    rc = op.monotonic_rnnt_cpp.gpu_monotonic_rnnt_align_restrict(
+        acts, torch.from_numpy(fx["labels"]).to(dev), torch.from_numpy(fx["T"]).to(dev),
+        torch.from_numpy(fx["S"]).to(dev), torch.from_numpy(fx["alignment"]).to(dev), 1, costs, grads, 0, 0)
+    assert rc == 0
+    assert_costs(costs.numpy().astype(np.float64), fx["costs_f64"])
+    assert_grads(grads.cpu().numpy(), fx["grads_f64"])
+
+
+def test_invalid_lengths_raise(op, dev):
+    acts = torch.zeros(12, 3, device=dev)
+    with pytest.raises(RuntimeError, match="invalid"):
+        op.monotonic_rnnt_loss(acts, torch.tensor([[1, 2, 1]], dtype=torch.int32, device=dev),
+                               torch.tensor([2], dtype=torch.int32), torch.tensor([3], dtype=torch.int32))
+    with pytest.raises(RuntimeError, match="rows"):
+        op.monotonic_rnnt_loss(acts[:11], torch.tensor([[1, 2]], dtype=torch.int32, device=dev),
+                               torch.tensor([4], dtype=torch.int32), torch.tensor([2], dtype=torch.int32))
+
+
+def test_loglik_forward_equals_backward(op, dev):
+    """beta(0,0) == alpha(T-1,S): the two recursions run independently (cpu_rnnt.h:257-259 check)."""
+    import ctypes
+    import _mrnnt_lib as L
+    rng = np.random.default_rng(9)
+    acts, labels, T, S = random_problem(rng, 6, (50, 300), 60, 96)
+    a = torch.from_numpy(acts).to(dev)
+    prep = op._Prepared(a, torch.from_numpy(labels), torch.from_numpy(T), torch.from_numpy(S), None, 0, 0)
+    costs, ws = op._forward(prep, with_beta=True)
+    llf = torch.empty(6, dtype=torch.float64, device=dev)
+    llb = torch.empty(6, dtype=torch.float64, device=dev)
+    L.check(L.load().mrnnt_read_loglik(ctypes.byref(prep.problem), ctypes.c_void_p(ws.data_ptr()),
+                                       ctypes.c_void_p(llf.data_ptr()), ctypes.c_void_p(llb.data_ptr()),
+                                       prep.stream()), "read_loglik")
+    torch.cuda.synchronize()
+    d = (llf - llb).abs().max().item()
+    assert d < 1e-6 * max(1.0, llf.abs().max().item()), d
+    assert np.allclose(-llf.cpu().numpy(), costs.cpu().numpy(), rtol=1e-6)
+
+
+# ---------------------------------------------------------------------------------------------
+# BASELINE.json configs
+
+def synth_problem(B, T, S, V, seed=0):
+    T = np.full(B, T, np.int32)
+    S = np.full(B, S, np.int32)
+    return T, S
+
+
+def test_config_c2_vs_oracle(op, dev):
+    """configs[1]: B=16, T=200, S=40, V=256 (grad check <= 1e-4), synthetic N(0,1) acts, seed 0."""
+    import _mrnnt_lib as L
+    import ctypes
+    B, Tn, Sn, V = 16, 200, 40, 256
+    T = np.full(B, Tn, np.int32)
+    S = np.full(B, Sn, np.int32)
+    rows = int(np.sum(T * (S + 1)))
+    acts = O.synth_acts(0, rows * V, seed=0).reshape(rows, V)
+    rng = np.random.default_rng(1)
+    labels = rng.integers(1, V, (B, Sn)).astype(np.int32)
+    # the device generator must reproduce the host twin bit for bit (bench parity relies on it)
+    d = torch.empty(rows * V, dtype=torch.float32, device=dev)
+    L.check(L.load().mrnnt_synth_acts(ctypes.c_void_p(d.data_ptr()), 0, rows * V, 0, 1,
+                                      ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)), "synth")
+    torch.cuda.synchronize()
+    assert np.array_equal(d.cpu().numpy(), acts.reshape(-1))
+    c, g = run_gpu(op, dev, acts, labels, T, S)
+    cr, gr = O.oracle_rnnt(acts, labels, T, S, num_threads=16)
+    assert_costs(c, cr)
+    assert_grads(g, gr)
