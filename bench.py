@@ -44,22 +44,10 @@ def lengths_for(config, rank, world):
         rng = np.random.default_rng(0)
         Tg = rng.integers(200, 1601, 512).astype(np.int32)
         Sg = np.array([rng.integers(20, min(300, t) + 1) for t in Tg], np.int32)
+        from distributed import shard_bounds
         lo, hi = shard_bounds(Tg.astype(np.int64) * (Sg + 1), world)[rank]
         return Tg[lo:hi], Sg[lo:hi], 1024, f"B=512 ragged (T~U[200,1600], S~U[20,min(300,T)]), V=1024, rank slice [{lo},{hi})"
     raise SystemExit(f"unknown config {config}")
-
-
-def shard_bounds(cost, world):
-    """Contiguous utterance ranges with balanced sum of rows (greedy prefix split)."""
-    cum = np.concatenate([[0], np.cumsum(cost)])
-    total = cum[-1]
-    bounds, lo = [], 0
-    for r in range(world):
-        hi = len(cost) if r == world - 1 else int(np.searchsorted(cum, total * (r + 1) / world))
-        hi = max(hi, lo)
-        bounds.append((lo, hi))
-        lo = hi
-    return bounds
 
 
 def main():

@@ -83,6 +83,14 @@ int mrnnt_version(void);
 void mrnnt_profile_enable(int enable);
 int mrnnt_profile_read(double *total_ms, int64_t *launches, int n);
 
+/* Launch-shape knobs for experiments (defaults are the tuned values): "softmax_variant" (0 row-at-a-time,
+ * 1 pipelined), "grad_variant" (0/1), "softmax_grid_per_cu" / "grad_grid_per_cu" (persistent workgroups per
+ * CU, 0 = one workgroup per lattice column; "grid_per_cu" sets both), "nt_store" (0/1), "dp_variant"
+ * (0 one wave per utterance and direction, 1 four waves).
+ * Sets `key` to `value` (value < 0: query only) and returns the previous value, or -1 for an unknown key.
+ * Process-global; not thread-safe against concurrent launches. */
+int mrnnt_tune(const char *key, int value);
+
 /* Bench helper: fill out[0..count) with the counter-based synthetic generator (bit-identical to the
  * host twin in oracle/rnnt_oracle.c): element i gets hash(seed, begin + i) as N(0,1)-like
  * (normal=1) or U[0,1) (normal=0). */

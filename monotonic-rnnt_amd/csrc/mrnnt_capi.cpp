@@ -133,7 +133,7 @@ RNNTStatus check_pointers(const mrnnt_problem *p) {
 
 // ---- device properties -------------------------------------------------------------------------
 
-int streaming_grid(int64_t cols) {
+int streaming_grid(int64_t cols, int per_cu) {
     static int cu_count[64] = {0};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
@@ -142,8 +142,9 @@ int streaming_grid(int64_t cols) {
         if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
         cu_count[dev] = n;
     }
-    // persistent grid: 8 workgroups of 4 waves per CU (32 waves/CU), never more than the columns
-    const int64_t g = (int64_t)cu_count[dev] * 8;
+    // per_cu workgroups of 4 waves per CU walking the columns grid-stride, never more than the columns;
+    // per_cu == 0: one workgroup per column (hardware-scheduled)
+    const int64_t g = per_cu <= 0 ? std::min<int64_t>(cols, 0x7fffffff) : (int64_t)cu_count[dev] * per_cu;
     return (int)std::max<int64_t>(1, std::min<int64_t>(g, cols));
 }
 
@@ -219,7 +220,7 @@ RNNTStatus mrnnt_forward(const mrnnt_problem *p, void *ws, size_t ws_bytes, floa
         });
         if (e != hipSuccess) return fail_hip(e, "alignment band kernels");
     }
-    const int grid = streaming_grid(pl.cols);
+    const int grid = streaming_grid(pl.cols, tuning().softmax_grid_per_cu);
     e = timed(K_SOFTMAX, stream, [&] { return launch_softmax(d, grid, stream); });
     if (e != hipSuccess) return fail_hip(e, "log-softmax kernel");
     e = timed(K_DP, stream, [&] { return launch_dp(d, pl.S_max, with_beta ? 1 : 0, costs_dev, stream); });
@@ -236,7 +237,7 @@ RNNTStatus mrnnt_backward(const mrnnt_problem *p, const void *ws, const float *g
     if (!ws) return fail(RNNT_STATUS_INVALID_VALUE, "workspace is null");
     if (!grads) return fail(RNNT_STATUS_INVALID_VALUE, "grads is null");
     DevProblem d = make_dev(p, pl, ws);
-    const int grid = streaming_grid(pl.cols);
+    const int grid = streaming_grid(pl.cols, tuning().grad_grid_per_cu);
     const hipError_t e = timed(K_GRAD, stream, [&] { return launch_grad(d, grad_scale, grads, grid, stream); });
     if (e != hipSuccess) return fail_hip(e, "gradient kernel");
     return RNNT_STATUS_SUCCESS;
@@ -297,6 +298,27 @@ int mrnnt_profile_read(double *total_ms, int64_t *launches, int n) {
         }
     }
     return bad;
+}
+
+int mrnnt_tune(const char *key, int value) {
+    if (!key) return -1;
+    int *slot = nullptr;
+    Tuning &t = tuning();
+    if (!std::strcmp(key, "softmax_variant")) slot = &t.softmax_variant;
+    else if (!std::strcmp(key, "grad_variant")) slot = &t.grad_variant;
+    else if (!std::strcmp(key, "softmax_grid_per_cu")) slot = &t.softmax_grid_per_cu;
+    else if (!std::strcmp(key, "grad_grid_per_cu")) slot = &t.grad_grid_per_cu;
+    else if (!std::strcmp(key, "grid_per_cu")) {  // both streaming kernels
+        const int prev = t.grad_grid_per_cu;
+        if (value >= 0) t.softmax_grid_per_cu = t.grad_grid_per_cu = value;
+        return prev;
+    }
+    else if (!std::strcmp(key, "nt_store")) slot = &t.nt_store;
+    else if (!std::strcmp(key, "dp_variant")) slot = &t.dp_variant;
+    if (!slot) return -1;
+    const int prev = *slot;
+    if (value >= 0) *slot = value;
+    return prev;
 }
 
 RNNTStatus mrnnt_synth_acts(float *out, int64_t begin, int64_t count, uint64_t seed, int normal, hipStream_t stream) {

@@ -30,6 +30,17 @@ struct DevProblem {
     double *llb;                // [B]  beta(0, 0)
 };
 
+// Launch-shape knobs (experiment hook: mrnnt_tune in mrnnt_capi.cpp). Defaults are the tuned values.
+struct Tuning {
+    int softmax_variant = 0;  // 0 = row-at-a-time, 1 = software-pipelined (next chunk in flight)
+    int grad_variant = 0;     // 0 = row-at-a-time, 1 = software-pipelined
+    int softmax_grid_per_cu = 0;  // workgroups (of 4 waves) per CU; 0 = one workgroup per lattice column
+    int grad_grid_per_cu = 32;    // same for the gradient kernel
+    int nt_store = 1;         // nontemporal stores of grads
+    int dp_variant = 1;       // 0 = one wave per (utterance, direction), 1 = four waves (DPP + LDS boundary)
+};
+Tuning &tuning();
+
 // Kernel-family ids for the profiling counters (mrnnt_profile_read order).
 enum KernelId { K_BAND = 0, K_SOFTMAX = 1, K_DP = 2, K_GRAD = 3, K_SETUP = 4, K_COUNT = 5 };
 

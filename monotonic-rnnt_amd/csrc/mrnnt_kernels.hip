@@ -167,6 +167,16 @@ __global__ __launch_bounds__(256) void align_band_kernel(DevProblem p, int k, co
     }
 }
 
+// Rows of the column outside the log-softmax band get lpb = lpe = 0 (finite), so the recursion can add
+// them to a -inf predecessor without a guard (a never-written row could hold NaN).
+__device__ __forceinline__ void zero_fill_outside_band(const DevProblem &p, int64_t rowc, int S, int lo, int hi) {
+    for (int s = threadIdx.x; s <= S; s += blockDim.x)
+        if (s < lo || s > hi) {
+            p.lpb[rowc + s] = 0.0;
+            p.lpe[rowc + s] = 0.0;
+        }
+}
+
 // ------------------------------------------------------------------------------------------------
 // log-softmax row reduce (vector path: V % 4 == 0 and 16-B aligned rows)
 //
@@ -195,6 +205,7 @@ __global__ __launch_bounds__(256) void softmax_vec_kernel(DevProblem p) {
         const int lo = max(0, t - (T - S));
         const int hi = min(t, S);
         const int *__restrict__ lab_b = p.labels + (int64_t)b * p.label_stride;
+        zero_fill_outside_band(p, rowc, S, lo, hi);
 
         for (int s = lo + wave * R; s <= hi; s += 4 * R) {
             float m[R], sum[R], zb[R], ze[R];
@@ -265,6 +276,118 @@ __global__ __launch_bounds__(256) void softmax_vec_kernel(DevProblem p) {
     }
 }
 
+
+// Software-pipelined variant: a wave walks its (row, chunk) sequence with the NEXT chunk's loads (and
+// the next row's label) already in flight while it reduces the current one, so every wave keeps
+// U * 1 KiB of loads outstanding through its reduce/epilogue instead of draining between rows.
+template <int U>
+__device__ __forceinline__ void load_chunk(const f4 *__restrict__ acts4, int64_t row, int V4, int ch, int lane,
+                                           f4 (&x)[U]) {
+    const int base = ch * 64 * U;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int j4 = base + lane + 64 * u;
+        if (j4 < V4)
+            x[u] = acts4[row * (int64_t)V4 + j4];
+        else
+            x[u] = (f4){NEG_INF_F, NEG_INF_F, NEG_INF_F, NEG_INF_F};
+    }
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void softmax_pipe_kernel(DevProblem p) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int V4 = p.V >> 2;
+    const int nch = (V4 + 64 * U - 1) / (64 * U);
+    const f4 *__restrict__ acts4 = reinterpret_cast<const f4 *>(p.acts);
+    const int blank = p.blank;
+    const int blank4 = blank >> 2;
+    const int blank_c = blank & 3;
+    const int blank_lane = blank4 & 63;
+
+    Cursor cur;
+    cur.init(p.col_off, p.B, blockIdx.x);
+    for (int64_t c = blockIdx.x; c < p.num_cols; c += gridDim.x) {
+        cur.advance(p.col_off, c);
+        const int b = cur.b;
+        const int T = p.T[b], S = p.S[b];
+        const int t = (int)(c - p.col_off[b]);
+        const int64_t rowc = p.row_off[b] + (int64_t)t * (S + 1);
+        const int lo = max(0, t - (T - S));
+        const int hi = min(t, S);
+        const int *__restrict__ lab_b = p.labels + (int64_t)b * p.label_stride;
+        zero_fill_outside_band(p, rowc, S, lo, hi);
+
+        int s = lo + wave;
+        if (s > hi) continue;
+        int ch = 0;
+        int lab = s < S ? lab_b[s] : -1;
+        f4 xa[U];
+        load_chunk<U>(acts4, rowc + s, V4, 0, lane, xa);
+        float m = NEG_INF_F, sum = 0.0f, zb = 0.0f, ze = 0.0f;
+        for (;;) {
+            int ns = s, nc = ch + 1;
+            if (nc == nch) {
+                nc = 0;
+                ns = s + 4;
+            }
+            const bool more = ns <= hi;
+            f4 xb[U];
+            int nlab = lab;
+            if (more) {
+                load_chunk<U>(acts4, rowc + ns, V4, nc, lane, xb);
+                if (nc == 0) nlab = ns < S ? lab_b[ns] : -1;
+            }
+            {
+                const int base = ch * 64 * U;
+                float cm = NEG_INF_F;
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int j4 = base + lane + 64 * u;
+                    if (j4 == blank4) zb = pick4(xa[u], blank_c);
+                    if (lab >= 0 && j4 == (lab >> 2)) ze = pick4(xa[u], lab & 3);
+                    cm = fmaxf(cm, max4(xa[u]));
+                }
+                const float mn = fmaxf(m, cm);
+                const float mr = (mn == NEG_INF_F) ? 0.0f : mn;
+                float acc = sum * fast_exp2((m - mr) * kLog2e);
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    acc += fast_exp2((xa[u].x - mr) * kLog2e);
+                    acc += fast_exp2((xa[u].y - mr) * kLog2e);
+                    acc += fast_exp2((xa[u].z - mr) * kLog2e);
+                    acc += fast_exp2((xa[u].w - mr) * kLog2e);
+                }
+                sum = acc;
+                m = mn;
+            }
+            if (ch == nch - 1) {
+                wave_reduce_max_sum(m, sum);
+                const float zbv = __shfl(zb, blank_lane);
+                const float zev = lab >= 0 ? __shfl(ze, (lab >> 2) & 63) : 0.0f;
+                const double den = -(double)m - log((double)sum);
+                if (lane == 0) {
+                    const int64_t row = rowc + s;
+                    p.den[row] = (float)den;
+                    p.lpb[row] = (double)zbv + den;
+                    p.lpe[row] = (double)zev + den;
+                }
+                m = NEG_INF_F;
+                sum = 0.0f;
+                zb = 0.0f;
+                ze = 0.0f;
+            }
+            if (!more) break;
+#pragma unroll
+            for (int u = 0; u < U; ++u) xa[u] = xb[u];
+            s = ns;
+            ch = nc;
+            lab = nlab;
+        }
+    }
+}
+
 // scalar path (any V, any alignment): one row per wave, lanes stride over v
 __global__ __launch_bounds__(256) void softmax_scalar_kernel(DevProblem p) {
     const int lane = threadIdx.x & 63;
@@ -282,6 +405,7 @@ __global__ __launch_bounds__(256) void softmax_scalar_kernel(DevProblem p) {
         const int lo = max(0, t - (T - S));
         const int hi = min(t, S);
         const int *__restrict__ lab_b = p.labels + (int64_t)b * p.label_stride;
+        zero_fill_outside_band(p, rowc, S, lo, hi);
         for (int s = lo + wave; s <= hi; s += 4) {
             const int lab = s < S ? lab_b[s] : -1;
             const float *__restrict__ z = p.acts + (rowc + s) * (int64_t)V;
@@ -484,6 +608,205 @@ __global__ __launch_bounds__(64) void dp_kernel(DevProblem p, int with_beta, flo
         alpha_pass<K, D>(p, b, costs);
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// Four-wave recursion: 256 lanes per (utterance, direction), K cells per lane (s = 256-lane blocks).
+// The s-1 (alpha) / s+1 (beta) neighbour crosses lanes with a DPP wave shift (v_mov_b32_dpp
+// wave_shr:1 / wave_shl:1, no LDS round trip) and crosses waves through a double-buffered LDS slot,
+// one s_barrier per step. The lp arrays are finite on every row of [0, S] (the log-softmax kernels
+// zero-fill out-of-band rows), so a predecessor at -inf stays -inf without guards; the only
+// non-finite case left in the LSE is both inputs at -inf.
+
+__device__ __forceinline__ double dpp_shr1(double v) {  // lane i <- lane i-1 (lane 0 <- 0)
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x138, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x138, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ double dpp_shl1(double v) {  // lane i <- lane i+1 (lane 63 <- 0)
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x130, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x130, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+
+// log(e^x + e^y) for x, y in [-inf, +inf): m + log1p(exp(-|x - y|)); one -inf input gives d = -inf,
+// e = 0, r = m exactly; both -inf is the only NaN case and is patched to -inf.
+__device__ __forceinline__ double lse2(double x, double y) {
+    const double m = fmax(x, y);
+    const float d = (float)(-fabs(x - y));
+    const float e = fast_exp2(d * kLog2e);
+    const float u = 1.0f + e;
+    const float corr = ((u - 1.0f) - e) * __builtin_amdgcn_rcpf(u);
+    const float c = fast_log2(u) * kLn2 - corr;
+    const double r = m + (double)c;
+    return (m == NEG_INF_D) ? NEG_INF_D : r;
+}
+
+template <int K, int D>
+__device__ __forceinline__ void alpha_pass4(const DevProblem &p, int b, float *__restrict__ costs, double (*xb)[4]) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int T = p.T[b], S = p.S[b], W = S + 1;
+    const int64_t r0 = p.row_off[b], c0 = p.col_off[b];
+    const int s0 = (wave * 64 + lane) * K;
+    const bool band = p.min_s != nullptr;
+
+    double a[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) a[k] = (s0 + k == 0) ? 0.0 : NEG_INF_D;
+    if (lane == 0) xb[1][wave] = NEG_INF_D;  // alpha(-1, s) for the cross-wave neighbour of step 0
+
+    double pb[D][K], pe[D][K];
+    int mn[D], mx[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        const int tt = min(d, T - 1);
+        const double *rb = p.lpb + r0 + (int64_t)tt * W + s0;
+        const double *re = p.lpe + r0 + (int64_t)tt * W + s0 - 1;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            pb[d][k] = rb[k];
+            pe[d][k] = re[k];
+        }
+        mn[d] = band ? p.min_s[c0 + tt] : 0;
+        mx[d] = band ? p.max_s[c0 + tt] : S;
+    }
+    __syncthreads();
+
+    for (int t0 = 0; t0 < T; t0 += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const int t = t0 + d;
+            if (t >= T) break;
+            const int lo = max(max(t - (T - 1 - S), mn[d]), 0);
+            const int hi = min(min(t + 1, S), mx[d]);
+            double carry = dpp_shr1(a[K - 1]);
+            if (lane == 0) carry = (wave == 0) ? NEG_INF_D : xb[(t + 1) & 1][wave - 1];
+            double na[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int s = s0 + k;
+                const double am1 = (k == 0) ? carry : a[k - 1];
+                const double v = lse2(a[k] + pb[d][k], am1 + pe[d][k]);
+                na[k] = (s >= lo && s <= hi) ? v : NEG_INF_D;
+            }
+            double *out = p.alpha + r0 + (int64_t)t * W + s0;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                a[k] = na[k];
+                if (s0 + k < W) out[k] = na[k];
+            }
+            if (lane == 63) xb[t & 1][wave] = na[K - 1];
+            const int tn = min(t + D, T - 1);
+            const double *rb = p.lpb + r0 + (int64_t)tn * W + s0;
+            const double *re = p.lpe + r0 + (int64_t)tn * W + s0 - 1;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                pb[d][k] = rb[k];
+                pe[d][k] = re[k];
+            }
+            mn[d] = band ? p.min_s[c0 + tn] : 0;
+            mx[d] = band ? p.max_s[c0 + tn] : S;
+            __syncthreads();
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        if (s0 + k == S) {
+            p.ll[b] = a[k];
+            if (costs) costs[b] = (float)(-a[k]);
+        }
+}
+
+template <int K, int D>
+__device__ __forceinline__ void beta_pass4(const DevProblem &p, int b, double (*xb)[4]) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int T = p.T[b], S = p.S[b], W = S + 1;
+    const int64_t r0 = p.row_off[b], c0 = p.col_off[b];
+    const int s0 = (wave * 64 + lane) * K;
+    const bool band = p.min_s != nullptr;
+
+    double bn[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) bn[k] = (s0 + k == S) ? 0.0 : NEG_INF_D;  // beta(T, s)
+    // beta(T, s) of the first cell of every wave, read by the previous wave's lane 63 at step T-1
+    if (lane == 0) xb[(T - 1 + 1) & 1][wave] = bn[0];
+
+    double pb[D][K], pe[D][K];
+    int mn[D], mx[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        const int tt = max(T - 1 - d, 0);
+        const double *rb = p.lpb + r0 + (int64_t)tt * W + s0;
+        const double *re = p.lpe + r0 + (int64_t)tt * W + s0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            pb[d][k] = rb[k];
+            pe[d][k] = re[k];
+        }
+        mn[d] = (band && tt > 0) ? p.min_s[c0 + tt - 1] : 0;
+        mx[d] = (band && tt > 0) ? p.max_s[c0 + tt - 1] : S;
+    }
+    __syncthreads();
+
+    for (int t0 = T - 1; t0 >= 0; t0 -= D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const int t = t0 - d;
+            if (t < 0) break;
+            int lo, hi;
+            if (t == 0) {
+                lo = 0;
+                hi = 0;
+            } else {
+                lo = max(max(t - (T - S), mn[d]), 0);
+                hi = min(min(t, S), mx[d]);
+            }
+            double carry = dpp_shl1(bn[0]);
+            if (lane == 63) carry = (wave == 3) ? NEG_INF_D : xb[(t + 1) & 1][wave + 1];
+            double nb[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int s = s0 + k;
+                const double bp1 = (k == K - 1) ? carry : bn[k + 1];
+                const double v = lse2(bn[k] + pb[d][k], bp1 + pe[d][k]);
+                nb[k] = (s >= lo && s <= hi) ? v : NEG_INF_D;
+            }
+            double *out = p.beta + r0 + (int64_t)t * W + s0;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                bn[k] = nb[k];
+                if (s0 + k < W) out[k] = nb[k];
+            }
+            if (lane == 0) xb[t & 1][wave] = nb[0];
+            const int tn = max(t - D, 0);
+            const double *rb = p.lpb + r0 + (int64_t)tn * W + s0;
+            const double *re = p.lpe + r0 + (int64_t)tn * W + s0;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                pb[d][k] = rb[k];
+                pe[d][k] = re[k];
+            }
+            mn[d] = (band && tn > 0) ? p.min_s[c0 + tn - 1] : 0;
+            mx[d] = (band && tn > 0) ? p.max_s[c0 + tn - 1] : S;
+            __syncthreads();
+        }
+    }
+    if (threadIdx.x == 0) p.llb[b] = bn[0];
+}
+
+template <int K, int D>
+__global__ __launch_bounds__(256) void dp4_kernel(DevProblem p, int with_beta, float *__restrict__ costs) {
+    __shared__ double xb[2][4];
+    const int b = with_beta ? (int)(blockIdx.x >> 1) : (int)blockIdx.x;
+    const bool bwd = with_beta && (blockIdx.x & 1);
+    if (bwd)
+        beta_pass4<K, D>(p, b, xb);
+    else
+        alpha_pass4<K, D>(p, b, costs, xb);
+}
+
 // ------------------------------------------------------------------------------------------------
 // logit gradient (cpu_rnnt.h:216-236 / gpu_rnnt_kernel.h:239-288):
 //   g[v] = exp(z[v] + den + alpha(t-1,s) + beta(t,s) - ll)
@@ -596,6 +919,139 @@ __global__ __launch_bounds__(256) void grad_vec_kernel(DevProblem p, const float
     }
 }
 
+
+// Software-pipelined gradient: the next (row, chunk)'s acts loads and the next row's recursion state
+// (scalar loads) are issued before the current chunk is computed and stored; the fp64 coefficient math
+// of the next row runs after the current chunk's stores are queued.
+struct RowRaw {
+    double am, b0, b1, b2, lpb, lpe;
+    float den;
+    int lab;
+};
+
+__device__ __forceinline__ RowRaw row_raw(const DevProblem &p, int t, int T, int S, int s, int64_t row,
+                                          const int *__restrict__ lab_b) {
+    const int W = S + 1;
+    RowRaw r;
+    r.am = (t == 0) ? (s == 0 ? 0.0 : NEG_INF_D) : p.alpha[row - W];
+    r.b0 = p.beta[row];
+    r.b1 = (t == T - 1) ? (s == S ? 0.0 : NEG_INF_D) : p.beta[row + W];
+    r.b2 = (s == S) ? NEG_INF_D : ((t == T - 1) ? (s + 1 == S ? 0.0 : NEG_INF_D) : p.beta[row + W + 1]);
+    r.lpb = p.lpb[row];
+    r.lpe = p.lpe[row];
+    r.den = p.den[row];
+    r.lab = (s < S) ? lab_b[s] : -1;
+    return r;
+}
+
+__device__ __forceinline__ RowCoef row_finish(const RowRaw &r, double ll, int S, int s) {
+    const double base = r.am - ll;
+    RowCoef rc;
+    rc.c2 = (float)(((double)r.den + base + r.b0) * kLog2eD);
+    rc.cb = (float)exp(r.lpb + base + r.b1);
+    rc.ce = (s < S) ? (float)exp(r.lpe + base + r.b2) : 0.0f;
+    rc.lab = r.lab;
+    return rc;
+}
+
+__device__ __forceinline__ f4 grad_chunk(const f4 &x, const RowCoef &rc, int j4, int blank, float sc) {
+    f4 g;
+    const float c2 = rc.c2;
+    g.x = fast_exp2(fmaf(x.x, kLog2e, c2));
+    g.y = fast_exp2(fmaf(x.y, kLog2e, c2));
+    g.z = fast_exp2(fmaf(x.z, kLog2e, c2));
+    g.w = fast_exp2(fmaf(x.w, kLog2e, c2));
+    const int v0 = j4 * 4;
+    const int db = blank - v0;
+    const int de = (rc.lab >= 0 && rc.lab != blank) ? rc.lab - v0 : -1;
+    g.x -= (db == 0 ? rc.cb : 0.0f) + (de == 0 ? rc.ce : 0.0f);
+    g.y -= (db == 1 ? rc.cb : 0.0f) + (de == 1 ? rc.ce : 0.0f);
+    g.z -= (db == 2 ? rc.cb : 0.0f) + (de == 2 ? rc.ce : 0.0f);
+    g.w -= (db == 3 ? rc.cb : 0.0f) + (de == 3 ? rc.ce : 0.0f);
+    g.x *= sc;
+    g.y *= sc;
+    g.z *= sc;
+    g.w *= sc;
+    return g;
+}
+
+template <bool NT>
+__device__ __forceinline__ void store4(f4 *ptr, const f4 &v) {
+    if constexpr (NT)
+        __builtin_nontemporal_store(v, ptr);
+    else
+        *ptr = v;
+}
+
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void grad_pipe_kernel(DevProblem p, const float *__restrict__ scale,
+                                                        float *__restrict__ grads) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int V4 = p.V >> 2;
+    const int nch = (V4 + 64 * U - 1) / (64 * U);
+    const int blank = p.blank;
+    const f4 *__restrict__ acts4 = reinterpret_cast<const f4 *>(p.acts);
+    f4 *__restrict__ g4 = reinterpret_cast<f4 *>(grads);
+
+    Cursor cur;
+    cur.init(p.col_off, p.B, blockIdx.x);
+    for (int64_t c = blockIdx.x; c < p.num_cols; c += gridDim.x) {
+        cur.advance(p.col_off, c);
+        const int b = cur.b;
+        const int T = p.T[b], S = p.S[b];
+        const int t = (int)(c - p.col_off[b]);
+        const int64_t rowc = p.row_off[b] + (int64_t)t * (S + 1);
+        const int lo = max(0, t - (T - S));
+        const int hi = min(t, S);
+        const double ll = p.ll[b];
+        const float sc = scale ? scale[b] : 1.0f;
+        const float zf = 0.0f * sc;
+        const f4 z4 = (f4){zf, zf, zf, zf};
+        const int *__restrict__ lab_b = p.labels + (int64_t)b * p.label_stride;
+
+        int s = wave;
+        if (s > S) continue;
+        int ch = 0;
+        bool inb = s >= lo && s <= hi;
+        RowCoef rc = RowCoef{0.0f, 0.0f, 0.0f, -1};
+        f4 xa[U];
+        if (inb) {
+            rc = row_finish(row_raw(p, t, T, S, s, rowc + s, lab_b), ll, S, s);
+            load_chunk<U>(acts4, rowc + s, V4, 0, lane, xa);
+        }
+        for (;;) {
+            int ns = s, nc = ch + 1;
+            if (nc == nch) {
+                nc = 0;
+                ns = s + 4;
+            }
+            const bool more = ns <= S;
+            const bool ninb = more && ns >= lo && ns <= hi;
+            f4 xb[U];
+            RowRaw nraw;
+            if (ninb) {
+                load_chunk<U>(acts4, rowc + ns, V4, nc, lane, xb);
+                if (nc == 0) nraw = row_raw(p, t, T, S, ns, rowc + ns, lab_b);
+            }
+            const int base = ch * 64 * U;
+            f4 *__restrict__ out = g4 + (rowc + s) * (int64_t)V4;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int j4 = base + lane + 64 * u;
+                if (j4 < V4) store4<NT>(out + j4, inb ? grad_chunk(xa[u], rc, j4, blank, sc) : z4);
+            }
+            if (!more) break;
+            if (nc == 0) rc = ninb ? row_finish(nraw, ll, S, ns) : RowCoef{0.0f, 0.0f, 0.0f, -1};
+#pragma unroll
+            for (int u = 0; u < U; ++u) xa[u] = xb[u];
+            s = ns;
+            ch = nc;
+            inb = ninb;
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void grad_scalar_kernel(DevProblem p, const float *__restrict__ scale,
                                                           float *__restrict__ grads) {
     const int lane = threadIdx.x & 63;
@@ -685,8 +1141,21 @@ static bool vec_ok(const DevProblem &p, const void *extra) {
            (extra == nullptr || reinterpret_cast<uintptr_t>(extra) % 16 == 0);
 }
 
+Tuning &tuning() {
+    static Tuning t;
+    return t;
+}
+
 hipError_t launch_softmax(const DevProblem &p, int grid, hipStream_t stream) {
-    if (vec_ok(p, nullptr)) {
+    if (vec_ok(p, nullptr) && tuning().softmax_variant == 1) {
+        const int V4 = p.V / 4;
+        if (V4 >= 192)
+            softmax_pipe_kernel<4><<<grid, 256, 0, stream>>>(p);
+        else if (V4 >= 96)
+            softmax_pipe_kernel<2><<<grid, 256, 0, stream>>>(p);
+        else
+            softmax_pipe_kernel<1><<<grid, 256, 0, stream>>>(p);
+    } else if (vec_ok(p, nullptr)) {
         const int V4 = p.V / 4;
         if (V4 >= 192)
             softmax_vec_kernel<4, 1><<<grid, 256, 0, stream>>>(p);
@@ -708,8 +1177,25 @@ static void dp_launch_k(const DevProblem &p, int with_beta, float *costs, hipStr
     dp_kernel<K, D><<<blocks, 64, 0, stream>>>(p, with_beta, costs);
 }
 
+template <int K>
+static void dp4_launch_k(const DevProblem &p, int with_beta, float *costs, hipStream_t stream) {
+    constexpr int D = K <= 2 ? 8 : (K <= 4 ? 4 : 2);
+    const int blocks = with_beta ? 2 * p.B : p.B;
+    dp4_kernel<K, D><<<blocks, 256, 0, stream>>>(p, with_beta, costs);
+}
+
 hipError_t launch_dp(const DevProblem &p, int S_max, int with_beta, float *costs, hipStream_t stream) {
     const int W = S_max + 1;
+    if (tuning().dp_variant == 1) {
+        if (W <= 256) dp4_launch_k<1>(p, with_beta, costs, stream);
+        else if (W <= 512) dp4_launch_k<2>(p, with_beta, costs, stream);
+        else if (W <= 768) dp4_launch_k<3>(p, with_beta, costs, stream);
+        else if (W <= 1024) dp4_launch_k<4>(p, with_beta, costs, stream);
+        else if (W <= 1536) dp4_launch_k<6>(p, with_beta, costs, stream);
+        else if (W <= kMaxLabelsPlusOne) dp4_launch_k<8>(p, with_beta, costs, stream);
+        else return hipErrorInvalidValue;
+        return hipGetLastError();
+    }
     if (W <= 64) dp_launch_k<1>(p, with_beta, costs, stream);
     else if (W <= 128) dp_launch_k<2>(p, with_beta, costs, stream);
     else if (W <= 192) dp_launch_k<3>(p, with_beta, costs, stream);
@@ -725,8 +1211,24 @@ hipError_t launch_dp(const DevProblem &p, int S_max, int with_beta, float *costs
     return hipGetLastError();
 }
 
+template <bool NT>
+static void grad_pipe_launch(const DevProblem &p, const float *scale, float *grads, int grid, hipStream_t stream) {
+    const int V4 = p.V / 4;
+    if (V4 >= 192)
+        grad_pipe_kernel<4, NT><<<grid, 256, 0, stream>>>(p, scale, grads);
+    else if (V4 >= 96)
+        grad_pipe_kernel<2, NT><<<grid, 256, 0, stream>>>(p, scale, grads);
+    else
+        grad_pipe_kernel<1, NT><<<grid, 256, 0, stream>>>(p, scale, grads);
+}
+
 hipError_t launch_grad(const DevProblem &p, const float *scale, float *grads, int grid, hipStream_t stream) {
-    if (vec_ok(p, grads)) {
+    if (vec_ok(p, grads) && tuning().grad_variant == 1) {
+        if (tuning().nt_store)
+            grad_pipe_launch<true>(p, scale, grads, grid, stream);
+        else
+            grad_pipe_launch<false>(p, scale, grads, grid, stream);
+    } else if (vec_ok(p, grads)) {
         const int V4 = p.V / 4;
         if (V4 >= 192)
             grad_vec_kernel<4, 1><<<grid, 256, 0, stream>>>(p, scale, grads);

@@ -78,6 +78,7 @@ def load() -> ctypes.CDLL:
             "mrnnt_profile_enable": (None, [i]),
             "mrnnt_profile_read": (i, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64), i]),
             "mrnnt_synth_acts": (i, [vp, i64, i64, ctypes.c_uint64, i, vp]),
+            "mrnnt_tune": (i, [ctypes.c_char_p, i]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -91,6 +92,11 @@ def check(status: int, where: str) -> None:
     if status != RNNT_STATUS_SUCCESS:
         msg = load().mrnnt_last_error()
         raise MrnntError(status, where, msg.decode() if msg else "")
+
+
+def tune(key: str, value: int = -1) -> int:
+    """Set a launch-shape knob (mrnnt_tune); returns the previous value (-1 = unknown key)."""
+    return load().mrnnt_tune(key.encode(), int(value))
 
 
 def profile_enable(on: bool = True) -> None:

@@ -240,3 +240,38 @@ def test_config_c2_vs_oracle(op, dev):
     cr, gr = O.oracle_rnnt(acts, labels, T, S, num_threads=16)
     assert_costs(c, cr)
     assert_grads(g, gr)
+
+
+@pytest.mark.parametrize("knobs", [
+    {"softmax_variant": 0, "grad_variant": 0, "dp_variant": 0, "grid_per_cu": 8, "nt_store": 1},
+    {"softmax_variant": 1, "grad_variant": 1, "dp_variant": 1, "grid_per_cu": 0, "nt_store": 0},
+    {"softmax_variant": 1, "grad_variant": 0, "dp_variant": 1, "grid_per_cu": 3, "nt_store": 1},
+    {"softmax_variant": 0, "grad_variant": 0, "dp_variant": 1, "softmax_grid_per_cu": 0, "grad_grid_per_cu": 32},
+    {"softmax_variant": 0, "grad_variant": 1, "dp_variant": 0, "grid_per_cu": 16, "nt_store": 1},
+])
+def test_every_kernel_variant_matches_oracle(op, dev, knobs):
+    """All launch variants selectable through mrnnt_tune compute the same result (alignment included)."""
+    import _mrnnt_lib as L
+    saved = {k: L.tune(k) for k in ("softmax_variant", "grad_variant", "dp_variant", "softmax_grid_per_cu",
+                                    "grad_grid_per_cu", "nt_store")}
+    try:
+        for k, v in knobs.items():
+            assert L.tune(k, v) >= 0
+        rng = np.random.default_rng(77)
+        for V, S_max in ((1024, 40), (260, 300), (64, 12)):
+            acts, labels, T, S = random_problem(rng, 3, (S_max, S_max + 60), S_max, V)
+            c, g = run_gpu(op, dev, acts, labels, T, S)
+            cr, gr = O.oracle_rnnt(acts, labels, T, S)
+            assert_costs(c, cr)
+            assert_grads(g, gr)
+        acts, labels, T, S = random_problem(rng, 3, (20, 60), 10, 128)
+        al = np.zeros((3, int(T.max())), np.int32)
+        for b in range(3):
+            al[b, np.sort(rng.choice(T[b], S[b], replace=False))] = labels[b, : S[b]]
+        c, g = run_gpu(op, dev, acts, labels, T, S, alignment=al, k=2)
+        cr, gr = O.oracle_rnnt(acts, labels, T, S, alignment=al, max_shift=2)
+        assert_costs(c, cr)
+        assert_grads(g, gr)
+    finally:
+        for k, v in saved.items():
+            L.tune(k, v)

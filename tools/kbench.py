@@ -1,0 +1,108 @@
+"""In-process A/B of kernel launch variants (interleaved rounds, per-kernel HIP-event times).
+
+  python tools/kbench.py [--config headline|c2|ragged] [--rounds R] [--variants JSON]
+
+Each variant is a dict of mrnnt_tune knobs; every round runs forward(with beta) + backward once per
+variant, in round-robin order, and records the per-kernel duration from HIP events around each launch.
+Prints one JSON object with the median / min per kernel per variant and the achieved GB/s.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "monotonic-rnnt_amd", "pytorch_binding"))
+sys.path.insert(0, ROOT)
+
+DEFAULT_VARIANTS = [
+    {"softmax_grid_per_cu": 0, "grad_grid_per_cu": 32},
+    {"softmax_grid_per_cu": 0, "grad_grid_per_cu": 24},
+    {"softmax_grid_per_cu": 0, "grad_grid_per_cu": 48},
+    {"softmax_grid_per_cu": 0, "grad_grid_per_cu": 64},
+    {"softmax_grid_per_cu": 64, "grad_grid_per_cu": 32},
+    {"softmax_grid_per_cu": 0, "grad_grid_per_cu": 32, "grad_variant": 1},
+]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="headline")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--variants", default=None)
+    args = ap.parse_args()
+    variants = json.loads(args.variants) if args.variants else DEFAULT_VARIANTS
+
+    import _mrnnt_lib as L
+    from bench import lengths_for
+
+    lib = L.load()
+    DEFAULTS = {k: L.tune(k) for k in ("softmax_variant", "grad_variant", "softmax_grid_per_cu", "grad_grid_per_cu",
+                                       "nt_store", "dp_variant")}
+    dev = torch.device("cuda:0")
+    T, S, V, workload = lengths_for(args.config, 0, 1)
+    B = len(T)
+    rows = int(np.sum(T.astype(np.int64) * (S + 1)))
+    n_band = int(np.sum((S.astype(np.int64) + 1) * (T - S + 1) - 1))
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    acts = torch.empty((rows, V), dtype=torch.float32, device=dev)
+    L.check(lib.mrnnt_synth_acts(ctypes.c_void_p(acts.data_ptr()), 0, rows * V, 0, 1, stream), "synth")
+    grads = torch.empty_like(acts)
+    labels = torch.from_numpy(np.random.default_rng(1).integers(1, V, (B, int(S.max()))).astype(np.int32)).to(dev)
+    T_dev = torch.from_numpy(T).to(dev)
+    S_dev = torch.from_numpy(S).to(dev)
+    costs = torch.empty(B, dtype=torch.float32, device=dev)
+    p = L.MrnntProblem()
+    p.B, p.V, p.blank, p.max_shift = B, V, 0, 0
+    p.T_host, p.S_host = T.ctypes.data, S.ctypes.data
+    p.T_dev, p.S_dev = T_dev.data_ptr(), S_dev.data_ptr()
+    p.acts, p.labels, p.label_stride = acts.data_ptr(), labels.data_ptr(), labels.size(1)
+    p.alignment, p.align_stride, p.align_blank, p.num_rows = None, 0, 0, rows
+    n = ctypes.c_size_t(0)
+    L.check(lib.mrnnt_workspace_size(ctypes.byref(p), ctypes.byref(n)), "ws")
+    ws = torch.empty(n.value, dtype=torch.uint8, device=dev)
+
+    def run_once():
+        L.check(lib.mrnnt_forward(ctypes.byref(p), ctypes.c_void_p(ws.data_ptr()), n.value,
+                                  ctypes.c_void_p(costs.data_ptr()), 1, stream), "fwd")
+        L.check(lib.mrnnt_backward(ctypes.byref(p), ctypes.c_void_p(ws.data_ptr()), None,
+                                   ctypes.c_void_p(grads.data_ptr()), stream), "bwd")
+
+    ref_costs = None
+    times = [dict(log_softmax=[], alpha_beta=[], grad=[]) for _ in variants]
+    for r in range(args.rounds + 1):
+        for i, v in enumerate(variants):
+            for k, val in DEFAULTS.items():
+                L.tune(k, val)
+            for k, val in v.items():
+                assert L.tune(k, val) >= 0, k
+            L.profile_enable(True)
+            run_once()
+            prof = L.profile_read()
+            L.profile_enable(False)
+            c = costs.cpu().numpy()
+            if ref_costs is None:
+                ref_costs = c
+            assert np.allclose(c, ref_costs, rtol=1e-6), "variant changed the costs"
+            if r == 0:
+                continue  # warm-up round
+            for k in times[i]:
+                times[i][k].append(prof[k][0])
+    out = {"workload": workload, "rows": rows, "inband_rows": n_band, "V": V, "variants": []}
+    gb = (n_band + rows) * V * 4 / 1e9
+    sb = n_band * V * 4 / 1e9
+    for v, t in zip(variants, times):
+        med = {k: float(np.median(x)) for k, x in t.items()}
+        out["variants"].append({"knobs": v, "median_ms": med, "min_ms": {k: float(np.min(x)) for k, x in t.items()},
+                                "grad_gbps": round(gb / (med["grad"] * 1e-3), 1),
+                                "softmax_gbps": round(sb / (med["log_softmax"] * 1e-3), 1),
+                                "step_ms": round(sum(med.values()), 3)})
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

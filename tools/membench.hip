@@ -1,0 +1,153 @@
+// membench.hip -- HBM ceilings on this MI355X for the access shapes of the hot path:
+//   read    : float4 loads, reduce to a register (the log-softmax pass)
+//   write   : float4 stores (the zero rows of the gradient)
+//   copy    : float4 load -> store (the gradient pass, 1 read : 1 write)
+//   copy_nt : copy with nontemporal stores
+// Grid-stride over 16-B elements with UNROLL loads in flight per lane; reports GB/s of algorithmic
+// bytes. Build: hipcc --offload-arch=gfx950 -O3 tools/membench.hip -o membench ; run: ./membench [GiB]
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <algorithm>
+#include <cstdlib>
+#include <vector>
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+#define CHECK(x)                                                                        \
+    do {                                                                                \
+        hipError_t e = (x);                                                             \
+        if (e != hipSuccess) {                                                          \
+            std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); \
+            std::exit(1);                                                               \
+        }                                                                               \
+    } while (0)
+
+template <int UNROLL>
+__global__ __launch_bounds__(256) void k_read(const f4 *__restrict__ a, int64_t n, float *__restrict__ out) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    float acc = 0.f;
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + (UNROLL - 1) * stride < n; i += UNROLL * stride) {
+        f4 x[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) x[u] = a[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) acc += x[u].x + x[u].y + x[u].z + x[u].w;
+    }
+    for (; i < n; i += stride) acc += a[i].x;
+    if (acc == 1234.5f) out[0] = acc;
+}
+
+template <int UNROLL>
+__global__ __launch_bounds__(256) void k_write(f4 *__restrict__ b, int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const f4 z = (f4){0.f, 0.f, 0.f, 0.f};
+    for (; i < n; i += stride) __builtin_nontemporal_store(z, &b[i]);
+}
+
+template <int UNROLL, bool NT>
+__global__ __launch_bounds__(256) void k_copy(const f4 *__restrict__ a, f4 *__restrict__ b, int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + (UNROLL - 1) * stride < n; i += UNROLL * stride) {
+        f4 x[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) x[u] = a[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            if constexpr (NT)
+                __builtin_nontemporal_store(x[u], &b[i + u * stride]);
+            else
+                b[i + u * stride] = x[u];
+        }
+    }
+    for (; i < n; i += stride) b[i] = a[i];
+}
+
+// contiguous-chunk variant: each workgroup streams its own contiguous slab (like one lattice column
+// per workgroup), 4 KiB per wave-iteration
+template <bool NT>
+__global__ __launch_bounds__(256) void k_copy_chunk(const f4 *__restrict__ a, f4 *__restrict__ b, int64_t n,
+                                                    int64_t chunk) {
+    for (int64_t c0 = (int64_t)blockIdx.x * chunk; c0 < n; c0 += (int64_t)gridDim.x * chunk) {
+        const int64_t end = c0 + chunk < n ? c0 + chunk : n;
+        for (int64_t i = c0 + threadIdx.x; i < end; i += 256 * 4) {
+            f4 x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i + u * 256 < end) x[u] = a[i + u * 256];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i + u * 256 < end) {
+                    if constexpr (NT)
+                        __builtin_nontemporal_store(x[u], &b[i + u * 256]);
+                    else
+                        b[i + u * 256] = x[u];
+                }
+        }
+    }
+}
+
+__global__ void k_fill(f4 *a, int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        a[i] = (f4){(float)(i & 7), 1.f, 2.f, 3.f};
+}
+
+template <class F>
+static float time_ms(F f, int reps) {
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    f();
+    CHECK(hipDeviceSynchronize());
+    std::vector<float> ts;
+    for (int r = 0; r < reps; ++r) {
+        CHECK(hipEventRecord(e0));
+        f();
+        CHECK(hipEventRecord(e1));
+        CHECK(hipEventSynchronize(e1));
+        float ms;
+        CHECK(hipEventElapsedTime(&ms, e0, e1));
+        ts.push_back(ms);
+    }
+    std::sort(ts.begin(), ts.end());
+    return ts[ts.size() / 2];
+}
+
+int main(int argc, char **argv) {
+    const double gib = argc > 1 ? std::atof(argv[1]) : 16.0;
+    const int64_t n = (int64_t)(gib * (1 << 30)) / 16;
+    int cus = 0;
+    CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    f4 *a, *b;
+    float *out;
+    CHECK(hipMalloc(&a, n * 16));
+    CHECK(hipMalloc(&b, n * 16));
+    CHECK(hipMalloc(&out, 16));
+    k_fill<<<4096, 256>>>(a, n);
+    k_fill<<<4096, 256>>>(b, n);
+    CHECK(hipDeviceSynchronize());
+    const double bytes = (double)n * 16;
+    std::printf("{\"gib\": %.1f, \"cus\": %d, \"results\": [\n", gib, cus);
+    bool first = true;
+    auto rep = [&](const char *name, int wg_per_cu, double mult, float ms) {
+        std::printf("%s {\"kernel\": \"%s\", \"wg_per_cu\": %d, \"ms\": %.3f, \"gbps\": %.1f}", first ? "" : ",\n", name,
+                    wg_per_cu, ms, mult * bytes / (ms * 1e-3) / 1e9);
+        first = false;
+    };
+    for (int w : {4, 8, 16, 32}) {
+        const int grid = cus * w;
+        rep("read_u4", w, 1.0, time_ms([&] { k_read<4><<<grid, 256>>>(a, n, out); }, 5));
+        rep("read_u8", w, 1.0, time_ms([&] { k_read<8><<<grid, 256>>>(a, n, out); }, 5));
+        rep("write_nt", w, 1.0, time_ms([&] { k_write<1><<<grid, 256>>>(b, n); }, 5));
+        rep("copy_u4", w, 2.0, time_ms([&] { k_copy<4, false><<<grid, 256>>>(a, b, n); }, 5));
+        rep("copy_u4_nt", w, 2.0, time_ms([&] { k_copy<4, true><<<grid, 256>>>(a, b, n); }, 5));
+        rep("copy_chunk800k_nt", w, 2.0,
+            time_ms([&] { k_copy_chunk<true><<<grid, 256>>>(a, b, n, 823296 / 16); }, 5));
+    }
+    std::printf("\n]}\n");
+    return 0;
+}
