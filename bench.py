@@ -58,15 +58,25 @@ def main():
     ap.add_argument("--config", default="headline", choices=["headline", "c2", "ragged"])
     ap.add_argument("--cpu-sample", type=int, default=8, help="utterances in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL over xGMI, the real path) or gloo (rehearsal: several ranks may share one GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    dev_index = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
+    gloo = args.dist_backend == "gloo"
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+
+    def coll_tensor(x):  # gloo collectives run on host tensors
+        return x.cpu() if gloo else x
 
     import monotonic_rnnt_op as op
     import _mrnnt_lib as L
@@ -79,7 +89,7 @@ def main():
     # global row offset of this rank's first utterance, so every rank streams different synthetic data
     all_rows = [rows]
     if world > 1:
-        t = torch.tensor([rows], dtype=torch.int64, device=dev)
+        t = coll_tensor(torch.tensor([rows], dtype=torch.int64, device=dev))
         g = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(g, t)
         all_rows = [int(x.item()) for x in g]
@@ -101,7 +111,7 @@ def main():
         loss = costs.sum()
         loss.backward()
         if world > 1:
-            tot = loss.detach().clone()
+            tot = coll_tensor(loss.detach().clone())
             dist.all_reduce(tot)  # the one RCCL exchange of the path: 4 bytes over xGMI
         return loss
 
@@ -123,11 +133,11 @@ def main():
     elapsed = time.perf_counter() - t0
     prof = L.profile_read()
     L.profile_enable(False)
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    el = coll_tensor(torch.tensor([elapsed], dtype=torch.float64, device=dev))
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
-    total_utts = torch.tensor([B], dtype=torch.int64, device=dev)
+    total_utts = coll_tensor(torch.tensor([B], dtype=torch.int64, device=dev))
     if world > 1:
         dist.all_reduce(total_utts)
     total_utts = int(total_utts.item())
@@ -175,7 +185,8 @@ def main():
             "data": "synthetic: counter-hash N(0,1)-like acts (seed 0), labels U[1,V-1] (seed 1+rank); inputs resident in HBM",
             "config": {"workload": workload, "utterances_per_gpu": B, "global_batch": total_utts,
                        "rows_per_gpu": rows, "inband_rows_per_gpu": n_band, "V": V,
-                       "parallelism": f"dp{world} (batch-sharded, one 4-byte RCCL loss all-reduce)"},
+                       "parallelism": f"dp{world} (batch-sharded, one 4-byte "
+                                      f"{'gloo (rehearsal)' if gloo else 'RCCL'} loss all-reduce)"},
             "achieved_hbm_gbps_step": round(step_bytes * total_utts / B * args.steps / elapsed / 1e9, 1),
             "roofline": {"kernel": "grad_vec_kernel (logit gradient)", "bound": "hbm",
                          "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBPS,

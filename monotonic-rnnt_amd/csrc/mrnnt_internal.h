@@ -32,12 +32,12 @@ struct DevProblem {
 
 // Launch-shape knobs (experiment hook: mrnnt_tune in mrnnt_capi.cpp). Defaults are the tuned values.
 struct Tuning {
-    int softmax_variant = 0;  // 0 = row-at-a-time, 1 = software-pipelined (next chunk in flight)
-    int grad_variant = 0;     // 0 = row-at-a-time, 1 = software-pipelined
+    int softmax_variant = 2;  // 0 = row-at-a-time, 1 = software-pipelined, 2 = two rows per wave (V >= 768)
+    int grad_variant = 0;     // 0 = row-at-a-time, 1 = software-pipelined, 2 = two rows per wave (V >= 768)
     int softmax_grid_per_cu = 0;  // workgroups (of 4 waves) per CU; 0 = one workgroup per lattice column
     int grad_grid_per_cu = 32;    // same for the gradient kernel
     int nt_store = 1;         // nontemporal stores of grads
-    int dp_variant = 1;       // 0 = one wave per (utterance, direction), 1 = four waves (DPP + LDS boundary)
+    int dp_variant = 1;       // 0 = one wave/direction (shuffles), 1 = four waves (DPP + LDS), 2 = one wave (DPP)
 };
 Tuning &tuning();
 

@@ -642,19 +642,20 @@ __device__ __forceinline__ double lse2(double x, double y) {
     return (m == NEG_INF_D) ? NEG_INF_D : r;
 }
 
-template <int K, int D>
-__device__ __forceinline__ void alpha_pass4(const DevProblem &p, int b, float *__restrict__ costs, double (*xb)[4]) {
+template <int K, int D, int NW>
+__device__ __forceinline__ void alpha_pass4(const DevProblem &p, int b, float *__restrict__ costs, double (*xb)[8]) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int T = p.T[b], S = p.S[b], W = S + 1;
     const int64_t r0 = p.row_off[b], c0 = p.col_off[b];
     const int s0 = (wave * 64 + lane) * K;
     const bool band = p.min_s != nullptr;
+    static_assert(NW == 1 || NW == 2 || NW == 4 || NW == 8, "cross-wave slots sized for <= 8 waves");
 
     double a[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) a[k] = (s0 + k == 0) ? 0.0 : NEG_INF_D;
-    if (lane == 0) xb[1][wave] = NEG_INF_D;  // alpha(-1, s) for the cross-wave neighbour of step 0
+    if (NW > 1 && lane == 0) xb[1][wave] = NEG_INF_D;  // alpha(-1, s) for the cross-wave neighbour of step 0
 
     double pb[D][K], pe[D][K];
     int mn[D], mx[D];
@@ -681,7 +682,7 @@ __device__ __forceinline__ void alpha_pass4(const DevProblem &p, int b, float *_
             const int lo = max(max(t - (T - 1 - S), mn[d]), 0);
             const int hi = min(min(t + 1, S), mx[d]);
             double carry = dpp_shr1(a[K - 1]);
-            if (lane == 0) carry = (wave == 0) ? NEG_INF_D : xb[(t + 1) & 1][wave - 1];
+            if (lane == 0) carry = (NW == 1 || wave == 0) ? NEG_INF_D : xb[(t + 1) & 1][wave - 1];
             double na[K];
 #pragma unroll
             for (int k = 0; k < K; ++k) {
@@ -696,7 +697,7 @@ __device__ __forceinline__ void alpha_pass4(const DevProblem &p, int b, float *_
                 a[k] = na[k];
                 if (s0 + k < W) out[k] = na[k];
             }
-            if (lane == 63) xb[t & 1][wave] = na[K - 1];
+            if (NW > 1 && lane == 63) xb[t & 1][wave] = na[K - 1];
             const int tn = min(t + D, T - 1);
             const double *rb = p.lpb + r0 + (int64_t)tn * W + s0;
             const double *re = p.lpe + r0 + (int64_t)tn * W + s0 - 1;
@@ -707,7 +708,7 @@ __device__ __forceinline__ void alpha_pass4(const DevProblem &p, int b, float *_
             }
             mn[d] = band ? p.min_s[c0 + tn] : 0;
             mx[d] = band ? p.max_s[c0 + tn] : S;
-            __syncthreads();
+            if (NW > 1) __syncthreads();
         }
     }
 #pragma unroll
@@ -718,8 +719,8 @@ __device__ __forceinline__ void alpha_pass4(const DevProblem &p, int b, float *_
         }
 }
 
-template <int K, int D>
-__device__ __forceinline__ void beta_pass4(const DevProblem &p, int b, double (*xb)[4]) {
+template <int K, int D, int NW>
+__device__ __forceinline__ void beta_pass4(const DevProblem &p, int b, double (*xb)[8]) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int T = p.T[b], S = p.S[b], W = S + 1;
@@ -731,7 +732,7 @@ __device__ __forceinline__ void beta_pass4(const DevProblem &p, int b, double (*
 #pragma unroll
     for (int k = 0; k < K; ++k) bn[k] = (s0 + k == S) ? 0.0 : NEG_INF_D;  // beta(T, s)
     // beta(T, s) of the first cell of every wave, read by the previous wave's lane 63 at step T-1
-    if (lane == 0) xb[(T - 1 + 1) & 1][wave] = bn[0];
+    if (NW > 1 && lane == 0) xb[(T - 1 + 1) & 1][wave] = bn[0];
 
     double pb[D][K], pe[D][K];
     int mn[D], mx[D];
@@ -764,7 +765,7 @@ __device__ __forceinline__ void beta_pass4(const DevProblem &p, int b, double (*
                 hi = min(min(t, S), mx[d]);
             }
             double carry = dpp_shl1(bn[0]);
-            if (lane == 63) carry = (wave == 3) ? NEG_INF_D : xb[(t + 1) & 1][wave + 1];
+            if (lane == 63) carry = (NW == 1 || wave == NW - 1) ? NEG_INF_D : xb[(t + 1) & 1][wave + 1];
             double nb[K];
 #pragma unroll
             for (int k = 0; k < K; ++k) {
@@ -779,7 +780,7 @@ __device__ __forceinline__ void beta_pass4(const DevProblem &p, int b, double (*
                 bn[k] = nb[k];
                 if (s0 + k < W) out[k] = nb[k];
             }
-            if (lane == 0) xb[t & 1][wave] = nb[0];
+            if (NW > 1 && lane == 0) xb[t & 1][wave] = nb[0];
             const int tn = max(t - D, 0);
             const double *rb = p.lpb + r0 + (int64_t)tn * W + s0;
             const double *re = p.lpe + r0 + (int64_t)tn * W + s0;
@@ -790,21 +791,21 @@ __device__ __forceinline__ void beta_pass4(const DevProblem &p, int b, double (*
             }
             mn[d] = (band && tn > 0) ? p.min_s[c0 + tn - 1] : 0;
             mx[d] = (band && tn > 0) ? p.max_s[c0 + tn - 1] : S;
-            __syncthreads();
+            if (NW > 1) __syncthreads();
         }
     }
     if (threadIdx.x == 0) p.llb[b] = bn[0];
 }
 
-template <int K, int D>
-__global__ __launch_bounds__(256) void dp4_kernel(DevProblem p, int with_beta, float *__restrict__ costs) {
-    __shared__ double xb[2][4];
+template <int K, int D, int NW>
+__global__ __launch_bounds__(64 * NW) void dp4_kernel(DevProblem p, int with_beta, float *__restrict__ costs) {
+    __shared__ double xb[2][8];
     const int b = with_beta ? (int)(blockIdx.x >> 1) : (int)blockIdx.x;
     const bool bwd = with_beta && (blockIdx.x & 1);
     if (bwd)
-        beta_pass4<K, D>(p, b, xb);
+        beta_pass4<K, D, NW>(p, b, xb);
     else
-        alpha_pass4<K, D>(p, b, costs, xb);
+        alpha_pass4<K, D, NW>(p, b, costs, xb);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1155,6 +1156,8 @@ hipError_t launch_softmax(const DevProblem &p, int grid, hipStream_t stream) {
             softmax_pipe_kernel<2><<<grid, 256, 0, stream>>>(p);
         else
             softmax_pipe_kernel<1><<<grid, 256, 0, stream>>>(p);
+    } else if (vec_ok(p, nullptr) && tuning().softmax_variant == 2 && p.V / 4 >= 192) {
+        softmax_vec_kernel<4, 2><<<grid, 256, 0, stream>>>(p);
     } else if (vec_ok(p, nullptr)) {
         const int V4 = p.V / 4;
         if (V4 >= 192)
@@ -1177,22 +1180,44 @@ static void dp_launch_k(const DevProblem &p, int with_beta, float *costs, hipStr
     dp_kernel<K, D><<<blocks, 64, 0, stream>>>(p, with_beta, costs);
 }
 
-template <int K>
+template <int K, int NW>
 static void dp4_launch_k(const DevProblem &p, int with_beta, float *costs, hipStream_t stream) {
-    constexpr int D = K <= 2 ? 8 : (K <= 4 ? 4 : 2);
+    constexpr int D = K <= 2 ? 8 : (K <= 4 ? 4 : (K <= 8 ? 2 : 1));
     const int blocks = with_beta ? 2 * p.B : p.B;
-    dp4_kernel<K, D><<<blocks, 256, 0, stream>>>(p, with_beta, costs);
+    dp4_kernel<K, D, NW><<<blocks, 64 * NW, 0, stream>>>(p, with_beta, costs);
 }
 
 hipError_t launch_dp(const DevProblem &p, int S_max, int with_beta, float *costs, hipStream_t stream) {
     const int W = S_max + 1;
-    if (tuning().dp_variant == 1) {
-        if (W <= 256) dp4_launch_k<1>(p, with_beta, costs, stream);
-        else if (W <= 512) dp4_launch_k<2>(p, with_beta, costs, stream);
-        else if (W <= 768) dp4_launch_k<3>(p, with_beta, costs, stream);
-        else if (W <= 1024) dp4_launch_k<4>(p, with_beta, costs, stream);
-        else if (W <= 1536) dp4_launch_k<6>(p, with_beta, costs, stream);
-        else if (W <= kMaxLabelsPlusOne) dp4_launch_k<8>(p, with_beta, costs, stream);
+    if (tuning().dp_variant == 1) {  // NW waves x K cells per lane, sized to S+1
+        if (W <= 64) dp4_launch_k<1, 1>(p, with_beta, costs, stream);
+        else if (W <= 128) dp4_launch_k<1, 2>(p, with_beta, costs, stream);
+        else if (W <= 256) dp4_launch_k<1, 4>(p, with_beta, costs, stream);
+        else if (W <= 512) dp4_launch_k<1, 8>(p, with_beta, costs, stream);
+        else if (W <= 1024) dp4_launch_k<2, 8>(p, with_beta, costs, stream);
+        else if (W <= 1536) dp4_launch_k<3, 8>(p, with_beta, costs, stream);
+        else if (W <= kMaxLabelsPlusOne) dp4_launch_k<4, 8>(p, with_beta, costs, stream);
+        else return hipErrorInvalidValue;
+        return hipGetLastError();
+    }
+    if (tuning().dp_variant == 3) {  // always four waves (round-1 shape), for A/B
+        if (W <= 256) dp4_launch_k<1, 4>(p, with_beta, costs, stream);
+        else if (W <= 512) dp4_launch_k<2, 4>(p, with_beta, costs, stream);
+        else if (W <= 1024) dp4_launch_k<4, 4>(p, with_beta, costs, stream);
+        else if (W <= kMaxLabelsPlusOne) dp4_launch_k<8, 4>(p, with_beta, costs, stream);
+        else return hipErrorInvalidValue;
+        return hipGetLastError();
+    }
+    if (tuning().dp_variant == 2) {  // one wave, K cells per lane, DPP neighbours, no barrier
+        if (W <= 64) dp4_launch_k<1, 1>(p, with_beta, costs, stream);
+        else if (W <= 128) dp4_launch_k<2, 1>(p, with_beta, costs, stream);
+        else if (W <= 192) dp4_launch_k<3, 1>(p, with_beta, costs, stream);
+        else if (W <= 256) dp4_launch_k<4, 1>(p, with_beta, costs, stream);
+        else if (W <= 320) dp4_launch_k<5, 1>(p, with_beta, costs, stream);
+        else if (W <= 384) dp4_launch_k<6, 1>(p, with_beta, costs, stream);
+        else if (W <= 512) dp4_launch_k<8, 1>(p, with_beta, costs, stream);
+        else if (W <= 1024) dp4_launch_k<16, 1>(p, with_beta, costs, stream);
+        else if (W <= kMaxLabelsPlusOne) dp4_launch_k<32, 1>(p, with_beta, costs, stream);
         else return hipErrorInvalidValue;
         return hipGetLastError();
     }
@@ -1228,6 +1253,8 @@ hipError_t launch_grad(const DevProblem &p, const float *scale, float *grads, in
             grad_pipe_launch<true>(p, scale, grads, grid, stream);
         else
             grad_pipe_launch<false>(p, scale, grads, grid, stream);
+    } else if (vec_ok(p, grads) && tuning().grad_variant == 2 && p.V / 4 >= 192) {
+        grad_vec_kernel<4, 2><<<grid, 256, 0, stream>>>(p, scale, grads);
     } else if (vec_ok(p, grads)) {
         const int V4 = p.V / 4;
         if (V4 >= 192)

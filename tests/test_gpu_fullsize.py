@@ -1,0 +1,156 @@
+"""Parity at BASELINE.json's full headline size, (B, T, S, V) = (64, 1000, 200, 1024), through the autograd
+surface on the GPU. The oracle cannot redo 64 utterances in seconds, so this checks
+  * size-independent properties on every row: finite costs; sum_v grad = 0 in every row (the softmax
+    gradient sums to the row occupancy minus the two transition terms, which are equal); exact zeros
+    outside the band; sum over s of the occupancy A(t, s) = 1 in sampled columns, recovered from a
+    non-label, non-blank column of the gradient divided by its softmax probability;
+  * and exact parity (costs 1e-4 relative, grads 1e-4 absolute) on a seeded subset of utterances
+    (first and last), regenerated on the host by the bit-identical twin of the device generator.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+
+B, T, S, V = 64, 1000, 200, 1024
+
+
+@pytest.fixture(scope="module")
+def headline():
+    import _mrnnt_lib as L
+    import monotonic_rnnt_op as op
+
+    dev = torch.device("cuda:0")
+    rows_per = T * (S + 1)
+    rows = B * rows_per
+    acts = torch.empty((rows, V), dtype=torch.float32, device=dev)
+    L.check(L.load().mrnnt_synth_acts(ctypes.c_void_p(acts.data_ptr()), 0, rows * V, 0, 1,
+                                      ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)), "synth")
+    labels_np = np.random.default_rng(1).integers(1, V, (B, S)).astype(np.int32)
+    labels = torch.from_numpy(labels_np).to(dev)
+    Tt = torch.full((B,), T, dtype=torch.int32)
+    St = torch.full((B,), S, dtype=torch.int32)
+    acts.requires_grad_(True)
+    costs = op.monotonic_rnnt_loss(acts, labels, Tt, St, blank_label=0)
+    costs.sum().backward()
+    torch.cuda.synchronize()
+    grads = acts.grad
+    acts.requires_grad_(False)
+    yield dict(acts=acts, grads=grads, costs=costs.detach().cpu().numpy().astype(np.float64), labels=labels_np,
+               rows_per=rows_per)
+    del acts, grads
+    torch.cuda.empty_cache()
+
+
+def test_costs_finite(headline):
+    c = headline["costs"]
+    assert np.all(np.isfinite(c)) and np.all(c > 0)
+
+
+def test_row_sums_zero_and_band_zeros(headline):
+    g = headline["grads"]
+    rs = g.sum(dim=1, dtype=torch.float64)
+    assert rs.abs().max().item() < 1e-4
+    # out-of-band rows are exactly zero: (t, s) with s > t or S - s > T - t
+    t = torch.arange(T, device=g.device).view(T, 1)
+    s = torch.arange(S + 1, device=g.device).view(1, S + 1)
+    oob = ((s > t) | ((S - s) > (T - t))).reshape(-1)
+    gb = g.view(B, T * (S + 1), V)
+    nz = (gb[:, oob, :] != 0).sum().item()
+    assert nz == 0
+    assert torch.isfinite(g).all().item()
+
+
+def test_column_occupancy_sums_to_one(headline):
+    g, acts, labels = headline["grads"], headline["acts"], headline["labels"]
+    rng = np.random.default_rng(11)
+    for b in (0, 17, 63):
+        used = set(labels[b].tolist()) | {0}
+        vstar = next(v for v in range(1, V) if v not in used)
+        for t in rng.choice(T, 4, replace=False):
+            r0 = b * headline["rows_per"] + int(t) * (S + 1)
+            z = acts[r0: r0 + S + 1].double()
+            p = torch.softmax(z, dim=1)[:, vstar]
+            occ = (g[r0: r0 + S + 1, vstar].double() / p).sum().item()
+            assert abs(occ - 1.0) < 1e-4, (b, t, occ)
+
+
+def test_subset_matches_oracle(headline):
+    g, labels = headline["grads"], headline["labels"]
+    rows_per = headline["rows_per"]
+    for b in (0, B - 1):
+        host_acts = O.synth_acts(b * rows_per * V, rows_per * V, seed=0).reshape(rows_per, V)
+        dev_acts = headline["acts"][b * rows_per: (b + 1) * rows_per].cpu().numpy()
+        assert np.array_equal(host_acts, dev_acts)  # device generator == host twin, bit for bit
+        cr, gr = O.oracle_rnnt(host_acts, labels[b: b + 1], [T], [S], precision="f64", num_threads=1)
+        assert abs(headline["costs"][b] - cr[0]) <= 1e-4 * abs(cr[0])
+        gg = g[b * rows_per: (b + 1) * rows_per].cpu().numpy()
+        assert np.abs(gg - gr).max() <= 1e-4
+
+
+def _run(op, acts, labels_np, T, S, dev):
+    labels = torch.from_numpy(labels_np).to(dev)
+    acts.requires_grad_(True)
+    costs = op.monotonic_rnnt_loss(acts, labels, torch.from_numpy(np.asarray(T, np.int32)),
+                                   torch.from_numpy(np.asarray(S, np.int32)), blank_label=0)
+    costs.sum().backward()
+    torch.cuda.synchronize()
+    g = acts.grad
+    acts.requires_grad_(False)
+    acts.grad = None
+    return costs.detach().cpu().numpy().astype(np.float64), g
+
+
+def test_config_c4_ragged_subset():
+    """configs[3] lengths (T~U[200,1600], S~U[20,min(300,T)], V=1024, seed 0): the first 6 utterances of the
+    512-utterance batch, full lengths, against the oracle."""
+    import _mrnnt_lib as L
+    import monotonic_rnnt_op as op
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(0)
+    Tg = rng.integers(200, 1601, 512).astype(np.int32)
+    Sg = np.array([rng.integers(20, min(300, t) + 1) for t in Tg], np.int32)
+    T, S, V = Tg[:6], Sg[:6], 1024
+    rows = int(np.sum(T.astype(np.int64) * (S + 1)))
+    host = O.synth_acts(0, rows * V, seed=5).reshape(rows, V)
+    acts = torch.from_numpy(host).to(dev)
+    labels = np.random.default_rng(2).integers(1, V, (6, int(S.max()))).astype(np.int32)
+    c, g = _run(op, acts, labels, T, S, dev)
+    cr, gr = O.oracle_rnnt(host, labels, T, S, precision="f64", num_threads=6)
+    assert np.max(np.abs(c - cr) / np.abs(cr)) <= 1e-4
+    assert np.abs(g.cpu().numpy() - gr).max() <= 1e-4
+
+
+def test_config_c5_large_vocab():
+    """configs[4] shape family, V = 10000: full (T, S) = (1000, 200) for 2 utterances checked through the
+    size-independent properties, and a (300, 60) utterance pair checked against the oracle."""
+    import monotonic_rnnt_op as op
+    dev = torch.device("cuda:0")
+    V = 10000
+    # properties at full T, S
+    Tn, Sn, Bn = 1000, 200, 2
+    rows = Bn * Tn * (Sn + 1)
+    acts = torch.empty((rows, V), dtype=torch.float32, device=dev)
+    import _mrnnt_lib as L
+    L.check(L.load().mrnnt_synth_acts(ctypes.c_void_p(acts.data_ptr()), 0, rows * V, 7, 1,
+                                      ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)), "synth")
+    labels = np.random.default_rng(3).integers(1, V, (Bn, Sn)).astype(np.int32)
+    c, g = _run(op, acts, labels, [Tn] * Bn, [Sn] * Bn, dev)
+    assert np.all(np.isfinite(c))
+    assert g.sum(dim=1, dtype=torch.float64).abs().max().item() < 1e-4
+    del acts, g
+    torch.cuda.empty_cache()
+    # oracle comparison at a shorter lattice
+    T, S = np.array([300, 240], np.int32), np.array([60, 45], np.int32)
+    rows = int(np.sum(T * (S + 1)))
+    host = O.synth_acts(0, rows * V, seed=9).reshape(rows, V)
+    labels = np.random.default_rng(4).integers(1, V, (2, 60)).astype(np.int32)
+    c, g = _run(op, torch.from_numpy(host).to(dev), labels, T, S, dev)
+    cr, gr = O.oracle_rnnt(host, labels, T, S, precision="f64", num_threads=2)
+    assert np.max(np.abs(c - cr) / np.abs(cr)) <= 1e-4
+    assert np.abs(g.cpu().numpy() - gr).max() <= 1e-4

@@ -247,6 +247,8 @@ def test_config_c2_vs_oracle(op, dev):
     {"softmax_variant": 1, "grad_variant": 1, "dp_variant": 1, "grid_per_cu": 0, "nt_store": 0},
     {"softmax_variant": 1, "grad_variant": 0, "dp_variant": 1, "grid_per_cu": 3, "nt_store": 1},
     {"softmax_variant": 0, "grad_variant": 0, "dp_variant": 1, "softmax_grid_per_cu": 0, "grad_grid_per_cu": 32},
+    {"softmax_variant": 2, "grad_variant": 2, "dp_variant": 2, "softmax_grid_per_cu": 0, "grad_grid_per_cu": 32},
+    {"softmax_variant": 2, "grad_variant": 0, "dp_variant": 3, "softmax_grid_per_cu": 0, "grad_grid_per_cu": 32},
     {"softmax_variant": 0, "grad_variant": 1, "dp_variant": 0, "grid_per_cu": 16, "nt_store": 1},
 ])
 def test_every_kernel_variant_matches_oracle(op, dev, knobs):

@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--config", default="headline")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--variants", default=None)
+    ap.add_argument("--separate-grads", action="store_true", help="allocate grads in its own torch allocation")
     args = ap.parse_args()
     variants = json.loads(args.variants) if args.variants else DEFAULT_VARIANTS
 
@@ -51,7 +52,9 @@ def main():
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     acts = torch.empty((rows, V), dtype=torch.float32, device=dev)
     L.check(lib.mrnnt_synth_acts(ctypes.c_void_p(acts.data_ptr()), 0, rows * V, 0, 1, stream), "synth")
-    grads = torch.empty_like(acts)
+    MAX_OFF_KB = 8192
+    grads_store = torch.empty(rows * V + MAX_OFF_KB * 256, dtype=torch.float32, device=dev)
+    grads_holder = {"t": grads_store[: rows * V].view(rows, V)}
     labels = torch.from_numpy(np.random.default_rng(1).integers(1, V, (B, int(S.max()))).astype(np.int32)).to(dev)
     T_dev = torch.from_numpy(T).to(dev)
     S_dev = torch.from_numpy(S).to(dev)
@@ -70,7 +73,7 @@ def main():
         L.check(lib.mrnnt_forward(ctypes.byref(p), ctypes.c_void_p(ws.data_ptr()), n.value,
                                   ctypes.c_void_p(costs.data_ptr()), 1, stream), "fwd")
         L.check(lib.mrnnt_backward(ctypes.byref(p), ctypes.c_void_p(ws.data_ptr()), None,
-                                   ctypes.c_void_p(grads.data_ptr()), stream), "bwd")
+                                   ctypes.c_void_p(grads_holder["t"].data_ptr()), stream), "bwd")
 
     ref_costs = None
     times = [dict(log_softmax=[], alpha_beta=[], grad=[]) for _ in variants]
@@ -79,7 +82,13 @@ def main():
             for k, val in DEFAULTS.items():
                 L.tune(k, val)
             for k, val in v.items():
+                if k == "grads_offset_kb":
+                    o = int(val) * 256
+                    grads_holder["t"] = grads_store[o: o + rows * V].view(rows, V)
+                    continue
                 assert L.tune(k, val) >= 0, k
+            if "grads_offset_kb" not in v:
+                grads_holder["t"] = grads_store[: rows * V].view(rows, V)
             L.profile_enable(True)
             run_once()
             prof = L.profile_read()
