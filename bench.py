@@ -40,6 +40,16 @@ def lengths_for(config, rank, world):
     if config == "c2":  # configs[1]
         B, T, S, V = 16, 200, 40, 256
         return np.full(B, T, np.int32), np.full(B, S, np.int32), V, "B=16,T=200,S=40,V=256 (configs[1])"
+    if config == "c5":  # configs[4]: V = 10000; 64 utterances = 514.6 GB of acts > 288 GB, so the batch runs as
+        # four 16-utterance chunks (128.6 GB acts + 128.6 GB grads each); one chunk is the measured unit
+        B, T, S, V = 16, 1000, 200, 10000
+        return (np.full(B, T, np.int32), np.full(B, S, np.int32), V,
+                "B=16 chunk of B=64,T=1000,S=200,V=10000 (configs[4], large vocab; batch = 4 chunks)")
+    if config == "ragged64":  # the first 64 utterances of configs[3] (fits one GPU with separate grads)
+        rng = np.random.default_rng(0)
+        Tg = rng.integers(200, 1601, 512).astype(np.int32)
+        Sg = np.array([rng.integers(20, min(300, t) + 1) for t in Tg], np.int32)
+        return Tg[:64], Sg[:64], 1024, "first 64 utterances of configs[3] (ragged T, S), V=1024"
     if config == "ragged":  # configs[3]: B=512 global, T~U[200,1600], S~U[20,min(300,T)], sharded over ranks
         rng = np.random.default_rng(0)
         Tg = rng.integers(200, 1601, 512).astype(np.int32)
@@ -55,7 +65,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="headline", choices=["headline", "c2", "ragged"])
+    ap.add_argument("--config", default="headline", choices=["headline", "c2", "ragged", "ragged64", "c5"])
     ap.add_argument("--cpu-sample", type=int, default=8, help="utterances in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--dist-backend", default="nccl",

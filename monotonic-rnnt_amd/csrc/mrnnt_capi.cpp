@@ -15,11 +15,15 @@
 #include <string>
 #include <vector>
 
+// The library is built with -fvisibility=hidden: only the declarations of the public headers below are
+// exported (the kernels and launchers in mrnnt_internal.h stay internal).
+#pragma GCC visibility push(default)
 #include "gpu_rnnt.h"
 #include "gpu_workspace_manager.h"
 #include "mrnnt.h"
-#include "mrnnt_internal.h"
 #include "rnnt_entrypoint.h"
+#pragma GCC visibility pop
+#include "mrnnt_internal.h"
 
 using namespace mrnnt;
 
@@ -315,6 +319,7 @@ int mrnnt_tune(const char *key, int value) {
     }
     else if (!std::strcmp(key, "nt_store")) slot = &t.nt_store;
     else if (!std::strcmp(key, "dp_variant")) slot = &t.dp_variant;
+    else if (!std::strcmp(key, "nt_load")) slot = &t.nt_load;
     if (!slot) return -1;
     const int prev = *slot;
     if (value >= 0) *slot = value;

@@ -37,6 +37,7 @@ struct Tuning {
     int softmax_grid_per_cu = 0;  // workgroups (of 4 waves) per CU; 0 = one workgroup per lattice column
     int grad_grid_per_cu = 32;    // same for the gradient kernel
     int nt_store = 1;         // nontemporal stores of grads
+    int nt_load = 1;          // nontemporal loads of acts (both streaming kernels)
     int dp_variant = 1;       // 0 = one wave/direction (shuffles), 1 = four waves (DPP + LDS), 2 = one wave (DPP)
 };
 Tuning &tuning();

@@ -59,6 +59,14 @@ __device__ __forceinline__ double lse(double x, double y) {
     return (lo == NEG_INF_D) ? hi : r;
 }
 
+template <bool NTL>
+__device__ __forceinline__ f4 ld4(const f4 *ptr) {
+    if constexpr (NTL)
+        return __builtin_nontemporal_load(ptr);
+    else
+        return *ptr;
+}
+
 __device__ __forceinline__ float pick4(const f4 &x, int c) {
     return c == 0 ? x.x : (c == 1 ? x.y : (c == 2 ? x.z : x.w));
 }
@@ -183,7 +191,7 @@ __device__ __forceinline__ void zero_fill_outside_band(const DevProblem &p, int6
 // U = float4 per lane per chunk (chunk = 256*U floats), R = rows a wave works on at once (R*U <= 4
 // keeps 4 float4 loads per lane in flight for both V = 1024 and V = 256).
 
-template <int U, int R>
+template <int U, int R, bool NTL>
 __global__ __launch_bounds__(256) void softmax_vec_kernel(DevProblem p) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -229,7 +237,7 @@ __global__ __launch_bounds__(256) void softmax_vec_kernel(DevProblem p) {
                     for (int u = 0; u < U; ++u) {
                         const int j4 = base + lane + 64 * u;
                         if (ok[r] && j4 < V4)
-                            x[r][u] = acts4[(rowc + s + r) * (int64_t)V4 + j4];
+                            x[r][u] = ld4<NTL>(&acts4[(rowc + s + r) * (int64_t)V4 + j4]);
                         else
                             x[r][u] = (f4){NEG_INF_F, NEG_INF_F, NEG_INF_F, NEG_INF_F};
                     }
@@ -642,14 +650,14 @@ __device__ __forceinline__ double lse2(double x, double y) {
     return (m == NEG_INF_D) ? NEG_INF_D : r;
 }
 
-template <int K, int D, int NW>
+template <int K, int D, int NW, bool BAND>
 __device__ __forceinline__ void alpha_pass4(const DevProblem &p, int b, float *__restrict__ costs, double (*xb)[8]) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int T = p.T[b], S = p.S[b], W = S + 1;
     const int64_t r0 = p.row_off[b], c0 = p.col_off[b];
     const int s0 = (wave * 64 + lane) * K;
-    const bool band = p.min_s != nullptr;
+    constexpr bool band = BAND;
     static_assert(NW == 1 || NW == 2 || NW == 4 || NW == 8, "cross-wave slots sized for <= 8 waves");
 
     double a[K];
@@ -719,14 +727,14 @@ __device__ __forceinline__ void alpha_pass4(const DevProblem &p, int b, float *_
         }
 }
 
-template <int K, int D, int NW>
+template <int K, int D, int NW, bool BAND>
 __device__ __forceinline__ void beta_pass4(const DevProblem &p, int b, double (*xb)[8]) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int T = p.T[b], S = p.S[b], W = S + 1;
     const int64_t r0 = p.row_off[b], c0 = p.col_off[b];
     const int s0 = (wave * 64 + lane) * K;
-    const bool band = p.min_s != nullptr;
+    constexpr bool band = BAND;
 
     double bn[K];
 #pragma unroll
@@ -797,15 +805,15 @@ __device__ __forceinline__ void beta_pass4(const DevProblem &p, int b, double (*
     if (threadIdx.x == 0) p.llb[b] = bn[0];
 }
 
-template <int K, int D, int NW>
+template <int K, int D, int NW, bool BAND>
 __global__ __launch_bounds__(64 * NW) void dp4_kernel(DevProblem p, int with_beta, float *__restrict__ costs) {
     __shared__ double xb[2][8];
     const int b = with_beta ? (int)(blockIdx.x >> 1) : (int)blockIdx.x;
     const bool bwd = with_beta && (blockIdx.x & 1);
     if (bwd)
-        beta_pass4<K, D, NW>(p, b, xb);
+        beta_pass4<K, D, NW, BAND>(p, b, xb);
     else
-        alpha_pass4<K, D, NW>(p, b, costs, xb);
+        alpha_pass4<K, D, NW, BAND>(p, b, costs, xb);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -839,7 +847,7 @@ __device__ __forceinline__ RowCoef row_coef(const DevProblem &p, int b, int t, i
     return rc;
 }
 
-template <int U, int R>
+template <int U, int R, bool NTL, bool NTS>
 __global__ __launch_bounds__(256) void grad_vec_kernel(DevProblem p, const float *__restrict__ scale,
                                                        float *__restrict__ grads) {
     const int lane = threadIdx.x & 63;
@@ -882,7 +890,7 @@ __global__ __launch_bounds__(256) void grad_vec_kernel(DevProblem p, const float
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
                         const int j4 = base + lane + 64 * u;
-                        if (inb[r] && j4 < V4) x[r][u] = acts4[(rowc + s + r) * (int64_t)V4 + j4];
+                        if (inb[r] && j4 < V4) x[r][u] = ld4<NTL>(&acts4[(rowc + s + r) * (int64_t)V4 + j4]);
                     }
 #pragma unroll
                 for (int r = 0; r < R; ++r)
@@ -913,7 +921,10 @@ __global__ __launch_bounds__(256) void grad_vec_kernel(DevProblem p, const float
                         } else {
                             g = (f4){zf, zf, zf, zf};
                         }
-                        __builtin_nontemporal_store(g, &g4[(rowc + s + r) * (int64_t)V4 + j4]);
+                        if constexpr (NTS)
+                            __builtin_nontemporal_store(g, &g4[(rowc + s + r) * (int64_t)V4 + j4]);
+                        else
+                            g4[(rowc + s + r) * (int64_t)V4 + j4] = g;
                     }
             }
         }
@@ -1147,6 +1158,19 @@ Tuning &tuning() {
     return t;
 }
 
+template <bool NTL>
+static void softmax_vec_launch(const DevProblem &p, int grid, hipStream_t stream) {
+    const int V4 = p.V / 4;
+    if (V4 >= 192 && tuning().softmax_variant == 2)
+        softmax_vec_kernel<4, 2, NTL><<<grid, 256, 0, stream>>>(p);
+    else if (V4 >= 192)
+        softmax_vec_kernel<4, 1, NTL><<<grid, 256, 0, stream>>>(p);
+    else if (V4 >= 96)
+        softmax_vec_kernel<2, 2, NTL><<<grid, 256, 0, stream>>>(p);
+    else
+        softmax_vec_kernel<1, 4, NTL><<<grid, 256, 0, stream>>>(p);
+}
+
 hipError_t launch_softmax(const DevProblem &p, int grid, hipStream_t stream) {
     if (vec_ok(p, nullptr) && tuning().softmax_variant == 1) {
         const int V4 = p.V / 4;
@@ -1156,16 +1180,11 @@ hipError_t launch_softmax(const DevProblem &p, int grid, hipStream_t stream) {
             softmax_pipe_kernel<2><<<grid, 256, 0, stream>>>(p);
         else
             softmax_pipe_kernel<1><<<grid, 256, 0, stream>>>(p);
-    } else if (vec_ok(p, nullptr) && tuning().softmax_variant == 2 && p.V / 4 >= 192) {
-        softmax_vec_kernel<4, 2><<<grid, 256, 0, stream>>>(p);
     } else if (vec_ok(p, nullptr)) {
-        const int V4 = p.V / 4;
-        if (V4 >= 192)
-            softmax_vec_kernel<4, 1><<<grid, 256, 0, stream>>>(p);
-        else if (V4 >= 96)
-            softmax_vec_kernel<2, 2><<<grid, 256, 0, stream>>>(p);
+        if (tuning().nt_load)
+            softmax_vec_launch<true>(p, grid, stream);
         else
-            softmax_vec_kernel<1, 4><<<grid, 256, 0, stream>>>(p);
+            softmax_vec_launch<false>(p, grid, stream);
     } else {
         softmax_scalar_kernel<<<grid, 256, 0, stream>>>(p);
     }
@@ -1184,7 +1203,10 @@ template <int K, int NW>
 static void dp4_launch_k(const DevProblem &p, int with_beta, float *costs, hipStream_t stream) {
     constexpr int D = K <= 2 ? 8 : (K <= 4 ? 4 : (K <= 8 ? 2 : 1));
     const int blocks = with_beta ? 2 * p.B : p.B;
-    dp4_kernel<K, D, NW><<<blocks, 64 * NW, 0, stream>>>(p, with_beta, costs);
+    if (p.min_s)
+        dp4_kernel<K, D, NW, true><<<blocks, 64 * NW, 0, stream>>>(p, with_beta, costs);
+    else
+        dp4_kernel<K, D, NW, false><<<blocks, 64 * NW, 0, stream>>>(p, with_beta, costs);
 }
 
 hipError_t launch_dp(const DevProblem &p, int S_max, int with_beta, float *costs, hipStream_t stream) {
@@ -1247,22 +1269,35 @@ static void grad_pipe_launch(const DevProblem &p, const float *scale, float *gra
         grad_pipe_kernel<1, NT><<<grid, 256, 0, stream>>>(p, scale, grads);
 }
 
+template <bool NTL, bool NTS>
+static void grad_vec_launch(const DevProblem &p, const float *scale, float *grads, int grid, hipStream_t stream) {
+    const int V4 = p.V / 4;
+    if (V4 >= 192 && tuning().grad_variant == 2)
+        grad_vec_kernel<4, 2, NTL, NTS><<<grid, 256, 0, stream>>>(p, scale, grads);
+    else if (V4 >= 192)
+        grad_vec_kernel<4, 1, NTL, NTS><<<grid, 256, 0, stream>>>(p, scale, grads);
+    else if (V4 >= 96)
+        grad_vec_kernel<2, 2, NTL, NTS><<<grid, 256, 0, stream>>>(p, scale, grads);
+    else
+        grad_vec_kernel<1, 4, NTL, NTS><<<grid, 256, 0, stream>>>(p, scale, grads);
+}
+
 hipError_t launch_grad(const DevProblem &p, const float *scale, float *grads, int grid, hipStream_t stream) {
     if (vec_ok(p, grads) && tuning().grad_variant == 1) {
         if (tuning().nt_store)
             grad_pipe_launch<true>(p, scale, grads, grid, stream);
         else
             grad_pipe_launch<false>(p, scale, grads, grid, stream);
-    } else if (vec_ok(p, grads) && tuning().grad_variant == 2 && p.V / 4 >= 192) {
-        grad_vec_kernel<4, 2><<<grid, 256, 0, stream>>>(p, scale, grads);
     } else if (vec_ok(p, grads)) {
-        const int V4 = p.V / 4;
-        if (V4 >= 192)
-            grad_vec_kernel<4, 1><<<grid, 256, 0, stream>>>(p, scale, grads);
-        else if (V4 >= 96)
-            grad_vec_kernel<2, 2><<<grid, 256, 0, stream>>>(p, scale, grads);
+        const bool ntl = tuning().nt_load != 0, nts = tuning().nt_store != 0;
+        if (ntl && nts)
+            grad_vec_launch<true, true>(p, scale, grads, grid, stream);
+        else if (ntl)
+            grad_vec_launch<true, false>(p, scale, grads, grid, stream);
+        else if (nts)
+            grad_vec_launch<false, true>(p, scale, grads, grid, stream);
         else
-            grad_vec_kernel<1, 4><<<grid, 256, 0, stream>>>(p, scale, grads);
+            grad_vec_launch<false, false>(p, scale, grads, grid, stream);
     } else {
         grad_scalar_kernel<<<grid, 256, 0, stream>>>(p, scale, grads);
     }

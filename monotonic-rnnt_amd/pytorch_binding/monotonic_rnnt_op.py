@@ -98,19 +98,21 @@ class _Prepared:
 
 
 def _forward(prep: _Prepared, with_beta: bool):
-    ws = prep.workspace()
-    costs = torch.empty(prep.problem.B, dtype=torch.float32, device=prep.device)
-    _L.check(_L.load().mrnnt_forward(ctypes.byref(prep.problem), _ptr(ws), ws.numel(), _ptr(costs),
-                                     1 if with_beta else 0, prep.stream()), "mrnnt_forward")
+    with torch.cuda.device(prep.device):  # kernels go to this device's current stream
+        ws = prep.workspace()
+        costs = torch.empty(prep.problem.B, dtype=torch.float32, device=prep.device)
+        _L.check(_L.load().mrnnt_forward(ctypes.byref(prep.problem), _ptr(ws), ws.numel(), _ptr(costs),
+                                         1 if with_beta else 0, prep.stream()), "mrnnt_forward")
     return costs, ws
 
 
 def _backward(prep: _Prepared, ws: torch.Tensor, grad_scale: Optional[torch.Tensor]) -> torch.Tensor:
-    grads = torch.empty_like(prep.acts)
-    if grad_scale is not None:
-        grad_scale = grad_scale.detach().to(prep.device, torch.float32).contiguous()
-    _L.check(_L.load().mrnnt_backward(ctypes.byref(prep.problem), _ptr(ws), _ptr(grad_scale), _ptr(grads),
-                                      prep.stream()), "mrnnt_backward")
+    with torch.cuda.device(prep.device):
+        grads = torch.empty_like(prep.acts)
+        if grad_scale is not None:
+            grad_scale = grad_scale.detach().to(prep.device, torch.float32).contiguous()
+        _L.check(_L.load().mrnnt_backward(ctypes.byref(prep.problem), _ptr(ws), _ptr(grad_scale), _ptr(grads),
+                                          prep.stream()), "mrnnt_backward")
     return grads
 
 
@@ -198,8 +200,11 @@ class _Ext:
         if want:
             if not grads.is_cuda or grads.dtype != torch.float32 or not grads.is_contiguous():
                 raise RuntimeError("grads must be a contiguous float32 GPU tensor")
-            _L.check(_L.load().mrnnt_backward(ctypes.byref(prep.problem), _ptr(ws), None, _ptr(grads),
-                                              prep.stream()), "mrnnt_backward")
+            if grads.shape != prep.acts.shape:
+                raise RuntimeError(f"grads must have the shape of acts {tuple(prep.acts.shape)}")
+            with torch.cuda.device(prep.device):
+                _L.check(_L.load().mrnnt_backward(ctypes.byref(prep.problem), _ptr(ws), None, _ptr(grads),
+                                                  prep.stream()), "mrnnt_backward")
         costs.copy_(c)
         return _L.RNNT_STATUS_SUCCESS
 

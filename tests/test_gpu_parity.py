@@ -249,19 +249,20 @@ def test_config_c2_vs_oracle(op, dev):
     {"softmax_variant": 0, "grad_variant": 0, "dp_variant": 1, "softmax_grid_per_cu": 0, "grad_grid_per_cu": 32},
     {"softmax_variant": 2, "grad_variant": 2, "dp_variant": 2, "softmax_grid_per_cu": 0, "grad_grid_per_cu": 32},
     {"softmax_variant": 2, "grad_variant": 0, "dp_variant": 3, "softmax_grid_per_cu": 0, "grad_grid_per_cu": 32},
+    {"softmax_variant": 0, "grad_variant": 2, "dp_variant": 1, "nt_load": 0, "nt_store": 0},
     {"softmax_variant": 0, "grad_variant": 1, "dp_variant": 0, "grid_per_cu": 16, "nt_store": 1},
 ])
 def test_every_kernel_variant_matches_oracle(op, dev, knobs):
     """All launch variants selectable through mrnnt_tune compute the same result (alignment included)."""
     import _mrnnt_lib as L
     saved = {k: L.tune(k) for k in ("softmax_variant", "grad_variant", "dp_variant", "softmax_grid_per_cu",
-                                    "grad_grid_per_cu", "nt_store")}
+                                    "grad_grid_per_cu", "nt_store", "nt_load")}
     try:
         for k, v in knobs.items():
             assert L.tune(k, v) >= 0
         rng = np.random.default_rng(77)
-        for V, S_max in ((1024, 40), (260, 300), (64, 12)):
-            acts, labels, T, S = random_problem(rng, 3, (S_max, S_max + 60), S_max, V)
+        for V, S_max, extra in ((1024, 40, 60), (260, 300, 60), (64, 12, 60), (32, 100, 200), (16, 200, 150)):
+            acts, labels, T, S = random_problem(rng, 3, (S_max, S_max + extra), S_max, V, force={0: (S_max + extra, S_max)})
             c, g = run_gpu(op, dev, acts, labels, T, S)
             cr, gr = O.oracle_rnnt(acts, labels, T, S)
             assert_costs(c, cr)
@@ -277,3 +278,18 @@ def test_every_kernel_variant_matches_oracle(op, dev, knobs):
     finally:
         for k, v in saved.items():
             L.tune(k, v)
+
+
+@pytest.mark.parametrize("S_len,T_len,V", [(1100, 1200, 16), (64, 64, 8), (128, 300, 12), (511, 530, 8)])
+def test_long_label_sequences_vs_oracle(op, dev, S_len, T_len, V):
+    """Label lengths across the recursion's wave/cell sizing boundaries (S+1 = 65, 129, 512, 1101)."""
+    rng = np.random.default_rng(S_len)
+    T = np.array([T_len, max(S_len, T_len - 7)], np.int32)
+    S = np.array([S_len, S_len - 1], np.int32)
+    rows = int(np.sum(T * (S + 1)))
+    acts = rng.standard_normal((rows, V)).astype(np.float32)
+    labels = rng.integers(1, V, (2, S_len)).astype(np.int32)
+    c, g = run_gpu(op, dev, acts, labels, T, S)
+    cr, gr = O.oracle_rnnt(acts, labels, T, S, num_threads=2)
+    assert_costs(c, cr)
+    assert_grads(g, gr)

@@ -40,6 +40,48 @@ __global__ __launch_bounds__(256) void k_read(const f4 *__restrict__ a, int64_t 
 }
 
 template <int UNROLL>
+__global__ __launch_bounds__(256) void k_read_nt(const f4 *__restrict__ a, int64_t n, float *__restrict__ out) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    float acc = 0.f;
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + (UNROLL - 1) * stride < n; i += UNROLL * stride) {
+        f4 x[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) x[u] = __builtin_nontemporal_load(&a[i + u * stride]);
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) acc += x[u].x + x[u].y + x[u].z + x[u].w;
+    }
+    for (; i < n; i += stride) acc += a[i].x;
+    if (acc == 1234.5f) out[0] = acc;
+}
+
+// each workgroup streams a contiguous slab of `chunk` float4s (like one lattice column per workgroup)
+template <int UNROLL>
+__global__ __launch_bounds__(256) void k_read_chunk(const f4 *__restrict__ a, int64_t n, int64_t chunk,
+                                                    float *__restrict__ out) {
+    float acc = 0.f;
+    for (int64_t c0 = (int64_t)blockIdx.x * chunk; c0 < n; c0 += (int64_t)gridDim.x * chunk) {
+        const int64_t end = c0 + chunk < n ? c0 + chunk : n;
+        for (int64_t i = c0 + threadIdx.x; i < end; i += 256 * UNROLL) {
+            f4 x[UNROLL];
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u) x[u] = (i + u * 256 < end) ? a[i + u * 256] : (f4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u) acc += x[u].x + x[u].y + x[u].z + x[u].w;
+        }
+    }
+    if (acc == 1234.5f) out[0] = acc;
+}
+
+template <int UNROLL>
+__global__ __launch_bounds__(256) void k_write_plain(f4 *__restrict__ b, int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const f4 z = (f4){0.f, 0.f, 0.f, 0.f};
+    for (; i < n; i += stride) b[i] = z;
+}
+
+template <int UNROLL>
 __global__ __launch_bounds__(256) void k_write(f4 *__restrict__ b, int64_t n) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -138,15 +180,27 @@ int main(int argc, char **argv) {
                     wg_per_cu, ms, mult * bytes / (ms * 1e-3) / 1e9);
         first = false;
     };
-    for (int w : {4, 8, 16, 32}) {
+    for (int w : {8, 16, 32}) {
         const int grid = cus * w;
-        rep("read_u4", w, 1.0, time_ms([&] { k_read<4><<<grid, 256>>>(a, n, out); }, 5));
         rep("read_u8", w, 1.0, time_ms([&] { k_read<8><<<grid, 256>>>(a, n, out); }, 5));
+        rep("read_u16", w, 1.0, time_ms([&] { k_read<16><<<grid, 256>>>(a, n, out); }, 5));
+        rep("read_nt_u8", w, 1.0, time_ms([&] { k_read_nt<8><<<grid, 256>>>(a, n, out); }, 5));
+        rep("read_chunk64k_u4", w, 1.0, time_ms([&] { k_read_chunk<4><<<grid, 256>>>(a, n, 65536 / 16, out); }, 5));
+        rep("read_chunk800k_u4", w, 1.0, time_ms([&] { k_read_chunk<4><<<grid, 256>>>(a, n, 823296 / 16, out); }, 5));
+        rep("read_chunk800k_u8", w, 1.0, time_ms([&] { k_read_chunk<8><<<grid, 256>>>(a, n, 823296 / 16, out); }, 5));
         rep("write_nt", w, 1.0, time_ms([&] { k_write<1><<<grid, 256>>>(b, n); }, 5));
+        rep("write_plain", w, 1.0, time_ms([&] { k_write_plain<1><<<grid, 256>>>(b, n); }, 5));
         rep("copy_u4", w, 2.0, time_ms([&] { k_copy<4, false><<<grid, 256>>>(a, b, n); }, 5));
         rep("copy_u4_nt", w, 2.0, time_ms([&] { k_copy<4, true><<<grid, 256>>>(a, b, n); }, 5));
         rep("copy_chunk800k_nt", w, 2.0,
             time_ms([&] { k_copy_chunk<true><<<grid, 256>>>(a, b, n, 823296 / 16); }, 5));
+    }
+    {
+        const int64_t chunks = (n + 823296 / 16 - 1) / (823296 / 16);
+        rep("read_chunk800k_onewgper", 0, 1.0,
+            time_ms([&] { k_read_chunk<4><<<(int)chunks, 256>>>(a, n, 823296 / 16, out); }, 5));
+        rep("copy_chunk800k_onewgper_nt", 0, 2.0,
+            time_ms([&] { k_copy_chunk<true><<<(int)chunks, 256>>>(a, b, n, 823296 / 16); }, 5));
     }
     std::printf("\n]}\n");
     return 0;
