@@ -198,7 +198,7 @@ def main():
                        "parallelism": f"dp{world} (batch-sharded, one 4-byte "
                                       f"{'gloo (rehearsal)' if gloo else 'RCCL'} loss all-reduce)"},
             "achieved_hbm_gbps_step": round(step_bytes * total_utts / B * args.steps / elapsed / 1e9, 1),
-            "roofline": {"kernel": "grad_vec_kernel (logit gradient)", "bound": "hbm",
+            "roofline": {"kernel": "grad_kernel (logit gradient)", "bound": "hbm",
                          "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4) if achieved else None,
                          "traffic": traffic, "algorithmic_bytes_per_launch": grad_bytes,

@@ -7,7 +7,11 @@
  * Function can run the loss in forward and the logit gradient (with dL/dcost fused) in backward.
  *
  * Data layout (same contract as the reference, monotonic_rnnt_op.py:133-140):
- *   acts    [N, V] fp32, N = sum_b T_b (S_b+1); utterance b contiguous, then t-major, then s
+ *   acts    [N, V], N = sum_b T_b (S_b+1); utterance b contiguous, then t-major, then s ("packed").
+ *           Extension (acts_layout): padded [B, pad_T, pad_S1, V] with (b, t, s) at row
+ *           (b*pad_T + t)*pad_S1 + s -- the joint network's natural output, no packing copy.
+ *           Element type fp32 (reference), or bf16 / fp16 (acts_dtype); grads use the same type and
+ *           layout. The arithmetic is fp32/fp64 in registers whatever the element type.
  *   labels  [B, label_stride] int32, label of (b, s) at labels[b*label_stride + s]
  *   T, S    [B] int32 input / label lengths (device copies for the kernels, host copies to plan)
  *   alignment (optional) [B, align_stride] int32, frames equal to align_blank are blanks
@@ -26,7 +30,12 @@
 extern "C" {
 #endif
 
-#define MRNNT_VERSION 1
+#define MRNNT_VERSION 2
+
+/* acts / grads element types */
+#define MRNNT_F32 0
+#define MRNNT_BF16 1
+#define MRNNT_F16 2
 
 typedef struct mrnnt_problem {
     int B;                   /* utterances */
@@ -37,13 +46,18 @@ typedef struct mrnnt_problem {
     const int *S_host;       /* host [B] */
     const int *T_dev;        /* device [B] (same values) */
     const int *S_dev;        /* device [B] */
-    const float *acts;       /* device [N, V] */
+    const void *acts;        /* device [N, V] packed, or [B, pad_T, pad_S1, V] padded; acts_dtype elements */
     const int *labels;       /* device [B, label_stride] */
     int64_t label_stride;
     const int *alignment;    /* device [B, align_stride] or NULL */
     int64_t align_stride;
     int align_blank;         /* value marking blank frames in `alignment` */
-    int64_t num_rows;        /* N as the caller sized acts; must equal sum_b T_b (S_b+1) (checked) */
+    int64_t num_rows;        /* rows of acts as the caller sized it (checked; < 0 skips the check): packed
+                                sum_b T_b (S_b+1), padded B*pad_T*pad_S1 */
+    /* --- version 2 --- (zero-initialised = the reference contract: packed fp32) */
+    int acts_dtype;          /* MRNNT_F32 / MRNNT_BF16 / MRNNT_F16 */
+    int64_t pad_T;           /* padded layout: frames per utterance slot (>= max T_b) */
+    int64_t pad_S1;          /* padded layout: label positions per frame (>= max S_b + 1); 0 = packed */
 } mrnnt_problem;
 
 /* Validate lengths (reference semantics: B > 0, V > 0, T_b > 0, S_b >= 0, T_b >= S_b) and return the
@@ -57,14 +71,15 @@ RNNTStatus mrnnt_forward(const mrnnt_problem *p, void *workspace, size_t workspa
                          int with_beta, hipStream_t stream);
 
 /* Backward: grads[r, v] = grad_scale[b(r)] * dcost_b / dacts[r, v] for every row (out-of-band rows
- * are written with zeros; no pre-zeroing needed). grad_scale (device [B]) may be NULL (= 1).
+ * are written with 0 * grad_scale, padding rows of the padded layout with 0; no pre-zeroing needed).
+ * grads has the layout and element type of acts. grad_scale (device fp32 [B]) may be NULL (= 1).
  * Requires a preceding mrnnt_forward(with_beta=1) on the same workspace and inputs. */
-RNNTStatus mrnnt_backward(const mrnnt_problem *p, const void *workspace, const float *grad_scale, float *grads,
+RNNTStatus mrnnt_backward(const mrnnt_problem *p, const void *workspace, const float *grad_scale, void *grads,
                           hipStream_t stream);
 
 /* forward(with_beta = grads != NULL) followed by backward. */
 RNNTStatus mrnnt_cost_and_grad(const mrnnt_problem *p, void *workspace, size_t workspace_bytes, float *costs_dev,
-                               float *grads, const float *grad_scale, hipStream_t stream);
+                               void *grads, const float *grad_scale, hipStream_t stream);
 
 /* Forward log-likelihoods from the workspace (device double [B]), for debugging/inspection:
  * ll_fwd = alpha(T-1, S), ll_bwd = beta(0, 0). Either may be NULL. Asynchronous on `stream`. */
@@ -83,10 +98,11 @@ int mrnnt_version(void);
 void mrnnt_profile_enable(int enable);
 int mrnnt_profile_read(double *total_ms, int64_t *launches, int n);
 
-/* Launch-shape knobs for experiments (defaults are the tuned values): "softmax_variant" (0 row-at-a-time,
- * 1 pipelined), "grad_variant" (0/1), "softmax_grid_per_cu" / "grad_grid_per_cu" (persistent workgroups per
- * CU, 0 = one workgroup per lattice column; "grid_per_cu" sets both), "nt_store" (0/1), "dp_variant"
- * (0 one wave per utterance and direction, 1 four waves).
+/* Launch-shape knobs for experiments (defaults are the tuned values): "softmax_variant" (rows per wave
+ * of the log-softmax kernel: 0 one, 2 two), "grad_variant" (0 one row per wave, 2 two rows, 3 row-stride
+ * sweep for the packed layout), "softmax_grid_per_cu" / "grad_grid_per_cu" (persistent workgroups per
+ * CU, 0 = one workgroup per lattice column; "grid_per_cu" sets both), "nt_store" / "nt_load" (0/1:
+ * nontemporal grads stores / acts loads).
  * Sets `key` to `value` (value < 0: query only) and returns the previous value, or -1 for an unknown key.
  * Process-global; not thread-safe against concurrent launches. */
 int mrnnt_tune(const char *key, int value);

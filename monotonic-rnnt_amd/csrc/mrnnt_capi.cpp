@@ -46,6 +46,8 @@ size_t align_up(size_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
 struct Plan {
     int B = 0, V = 0, S_max = 0, T_max = 0;
     int64_t N = 0, cols = 0;
+    int elem = ELEM_F32;
+    int64_t pad_T = 0, pad_S1 = 0;
     bool align = false;
     size_t off_row, off_col, off_mtmp, off_min, off_max, off_den, off_lpb, off_lpe, off_alpha, off_beta, off_ll,
         off_llb, total;
@@ -75,9 +77,23 @@ RNNTStatus make_plan(const mrnnt_problem *p, Plan *pl) {
     if (q.S_max + 1 > kMaxLabelsPlusOne)
         return fail(RNNT_STATUS_INVALID_VALUE, "max label length " + std::to_string(q.S_max) + " exceeds " +
                                                    std::to_string(kMaxLabelsPlusOne - 1));
-    if (p->num_rows >= 0 && p->num_rows != q.N)
-        return fail(RNNT_STATUS_INVALID_VALUE, "acts has " + std::to_string(p->num_rows) + " rows but sum_b T_b(S_b+1) = " +
-                                                   std::to_string(q.N));
+    if (p->acts_dtype != ELEM_F32 && p->acts_dtype != ELEM_BF16 && p->acts_dtype != ELEM_F16)
+        return fail(RNNT_STATUS_INVALID_VALUE, "unknown acts_dtype " + std::to_string(p->acts_dtype));
+    q.elem = p->acts_dtype;
+    q.pad_T = p->pad_T;
+    q.pad_S1 = p->pad_S1;
+    int64_t acts_rows = q.N;
+    if (q.pad_S1 != 0) {
+        if (q.pad_S1 < (int64_t)q.S_max + 1 || q.pad_T < q.T_max)
+            return fail(RNNT_STATUS_INVALID_VALUE, "padded layout [B, " + std::to_string(q.pad_T) + ", " +
+                                                       std::to_string(q.pad_S1) + ", V] too small for max T " +
+                                                       std::to_string(q.T_max) + ", max S " + std::to_string(q.S_max));
+        acts_rows = (int64_t)q.B * q.pad_T * q.pad_S1;
+    }
+    if (p->num_rows >= 0 && p->num_rows != acts_rows)
+        return fail(RNNT_STATUS_INVALID_VALUE, "acts has " + std::to_string(p->num_rows) + " rows but the " +
+                                                   (q.pad_S1 ? "padded layout needs " : "lattice needs sum_b T_b(S_b+1) = ") +
+                                                   std::to_string(acts_rows));
     q.align = p->alignment != nullptr;
     size_t o = 0;
     auto take = [&](size_t bytes) {
@@ -118,6 +134,9 @@ DevProblem make_dev(const mrnnt_problem *p, const Plan &pl, const void *ws) {
     d.V = pl.V;
     d.blank = p->blank;
     d.num_cols = pl.cols;
+    d.num_rows = pl.N;
+    d.pad_T = pl.pad_T;
+    d.pad_S1 = pl.pad_S1;
     d.den = reinterpret_cast<float *>(w + pl.off_den);
     d.lpb = reinterpret_cast<double *>(w + pl.off_lpb) + kLpPad;
     d.lpe = reinterpret_cast<double *>(w + pl.off_lpe) + kLpPad;
@@ -225,14 +244,14 @@ RNNTStatus mrnnt_forward(const mrnnt_problem *p, void *ws, size_t ws_bytes, floa
         if (e != hipSuccess) return fail_hip(e, "alignment band kernels");
     }
     const int grid = streaming_grid(pl.cols, tuning().softmax_grid_per_cu);
-    e = timed(K_SOFTMAX, stream, [&] { return launch_softmax(d, grid, stream); });
+    e = timed(K_SOFTMAX, stream, [&] { return launch_softmax(d, pl.elem, grid, stream); });
     if (e != hipSuccess) return fail_hip(e, "log-softmax kernel");
     e = timed(K_DP, stream, [&] { return launch_dp(d, pl.S_max, with_beta ? 1 : 0, costs_dev, stream); });
     if (e != hipSuccess) return fail_hip(e, "alpha/beta kernel");
     return RNNT_STATUS_SUCCESS;
 }
 
-RNNTStatus mrnnt_backward(const mrnnt_problem *p, const void *ws, const float *grad_scale, float *grads,
+RNNTStatus mrnnt_backward(const mrnnt_problem *p, const void *ws, const float *grad_scale, void *grads,
                           hipStream_t stream) {
     Plan pl;
     RNNTStatus st = make_plan(p, &pl);
@@ -241,13 +260,20 @@ RNNTStatus mrnnt_backward(const mrnnt_problem *p, const void *ws, const float *g
     if (!ws) return fail(RNNT_STATUS_INVALID_VALUE, "workspace is null");
     if (!grads) return fail(RNNT_STATUS_INVALID_VALUE, "grads is null");
     DevProblem d = make_dev(p, pl, ws);
-    const int grid = streaming_grid(pl.cols, tuning().grad_grid_per_cu);
-    const hipError_t e = timed(K_GRAD, stream, [&] { return launch_grad(d, grad_scale, grads, grid, stream); });
+    // grad_variant 3 sweeps rows (packed layout only), the others walk lattice columns
+    const int grid = (tuning().grad_variant == 3 && pl.pad_S1 == 0)
+                         ? streaming_grid(pl.N, std::max(1, tuning().grad_grid_per_cu))
+                         : streaming_grid(pl.cols, tuning().grad_grid_per_cu);
+    hipError_t e = timed(K_GRAD, stream, [&] { return launch_grad(d, pl.elem, grad_scale, grads, grid, stream); });
     if (e != hipSuccess) return fail_hip(e, "gradient kernel");
+    if (pl.pad_S1 != 0) {
+        e = launch_pad_zero(d, pl.elem, grads, stream);
+        if (e != hipSuccess) return fail_hip(e, "padding-rows zero kernel");
+    }
     return RNNT_STATUS_SUCCESS;
 }
 
-RNNTStatus mrnnt_cost_and_grad(const mrnnt_problem *p, void *ws, size_t ws_bytes, float *costs_dev, float *grads,
+RNNTStatus mrnnt_cost_and_grad(const mrnnt_problem *p, void *ws, size_t ws_bytes, float *costs_dev, void *grads,
                                const float *grad_scale, hipStream_t stream) {
     RNNTStatus st = mrnnt_forward(p, ws, ws_bytes, costs_dev, grads != nullptr, stream);
     if (st != RNNT_STATUS_SUCCESS || grads == nullptr) return st;
@@ -318,7 +344,6 @@ int mrnnt_tune(const char *key, int value) {
         return prev;
     }
     else if (!std::strcmp(key, "nt_store")) slot = &t.nt_store;
-    else if (!std::strcmp(key, "dp_variant")) slot = &t.dp_variant;
     else if (!std::strcmp(key, "nt_load")) slot = &t.nt_load;
     if (!slot) return -1;
     const int prev = *slot;

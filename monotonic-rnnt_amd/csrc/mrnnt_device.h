@@ -1,0 +1,173 @@
+// mrnnt_device.h -- device-side helpers shared by the kernels of libmonotonic_rnnt_amd.so
+// (gfx950 / CDNA4, wave64): constants, fast transcendentals, the fp64 log-sum-exp, wave reductions,
+// utterance cursors, the element-type traits of the acts/grads I/O, and acts-layout addressing.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mrnnt_internal.h"
+
+namespace mrnnt {
+
+#define NEG_INF_F (-__builtin_huge_valf())
+#define NEG_INF_D (-__builtin_huge_val())
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr double kLog2eD = 1.4426950408889634073599;
+constexpr float kLn2 = 0.69314718055994531f;
+
+// native 16-byte vectors (dwordx4 loads/stores; the nontemporal builtins want ext_vector_type)
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }  // v_exp_f32
+__device__ __forceinline__ float fast_log2(float x) { return __builtin_amdgcn_logf(x); }   // v_log_f32
+
+// log(e^x + e^y) with fp64 state (rnnt_helper.h:16-30 semantics): m + log1p(exp(-|x - y|)). The bounded
+// correction (in [0, ln 2]) uses the fp32 hardware exp2/log2 plus the classic log1p rounding correction
+// (~1e-7 absolute per step). One -inf input gives d = -inf, e = 0, r = m exactly; both -inf is the only
+// NaN case and is patched to -inf.
+__device__ __forceinline__ double lse2(double x, double y) {
+    const double m = fmax(x, y);
+    const float d = (float)(-fabs(x - y));
+    const float e = fast_exp2(d * kLog2e);
+    const float u = 1.0f + e;
+    const float corr = ((u - 1.0f) - e) * __builtin_amdgcn_rcpf(u);
+    const float c = fast_log2(u) * kLn2 - corr;
+    const double r = m + (double)c;
+    return (m == NEG_INF_D) ? NEG_INF_D : r;
+}
+
+// wave64 butterfly reduction of an online-softmax (max, sum-exp) pair
+__device__ __forceinline__ void wave_reduce_max_sum(float &m, float &s) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const float m2 = __shfl_xor(m, off);
+        const float s2 = __shfl_xor(s, off);
+        const float mn = fmaxf(m, m2);
+        const float mr = (mn == NEG_INF_F) ? 0.0f : mn;
+        s = s * fast_exp2((m - mr) * kLog2e) + s2 * fast_exp2((m2 - mr) * kLog2e);
+        m = mn;
+    }
+}
+
+// Monotone utterance cursor over a prefix-offset array (col_off or row_off), for a workgroup/wave that
+// walks indices in increasing order: one binary search at start, then amortised O(1) advances.
+struct Cursor {
+    int b;
+    __device__ __forceinline__ void init(const int64_t *off, int B, int64_t i) {
+        int lo = 0, hi = B - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (off[mid] <= i) lo = mid; else hi = mid - 1;
+        }
+        b = lo;
+    }
+    __device__ __forceinline__ void advance(const int64_t *off, int64_t i) {
+        while (off[b + 1] <= i) ++b;
+    }
+};
+
+// First acts/grads row of lattice column (b, t): packed layout (reference contract) = the internal
+// row rowc; padded [B, pad_T, pad_S1, V] layout = (b * pad_T + t) * pad_S1.
+__device__ __forceinline__ int64_t acts_col_base(const DevProblem &p, int b, int t, int64_t rowc) {
+    return p.pad_S1 ? ((int64_t)b * p.pad_T + t) * p.pad_S1 : rowc;
+}
+
+// ---- element-type traits of the acts / grads I/O (math is fp32 in registers) ----------------------
+
+struct IoF32 {
+    typedef float S;
+    static constexpr int E = 4;  // elements per 16-byte vector
+    typedef f4 V;
+    __device__ static __forceinline__ void unpack(const V &v, float (&x)[E]) {
+        x[0] = v.x;
+        x[1] = v.y;
+        x[2] = v.z;
+        x[3] = v.w;
+    }
+    __device__ static __forceinline__ V pack(const float (&x)[E]) { return (V){x[0], x[1], x[2], x[3]}; }
+    __device__ static __forceinline__ float to_f(S s) { return s; }
+    __device__ static __forceinline__ S from_f(float f) { return f; }
+};
+
+struct IoBF16 {
+    typedef unsigned short S;  // bf16 bits
+    static constexpr int E = 8;
+    typedef u4 V;
+    __device__ static __forceinline__ void unpack(const V &v, float (&x)[E]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            x[2 * i] = __uint_as_float(v[i] << 16);
+            x[2 * i + 1] = __uint_as_float(v[i] & 0xffff0000u);
+        }
+    }
+    __device__ static __forceinline__ unsigned pack2(float a, float b) {  // v_cvt_pk_bf16_f32, RNE
+        const unsigned short lo = __builtin_bit_cast(unsigned short, (__bf16)a);
+        const unsigned short hi = __builtin_bit_cast(unsigned short, (__bf16)b);
+        return (unsigned)lo | ((unsigned)hi << 16);
+    }
+    __device__ static __forceinline__ V pack(const float (&x)[E]) {
+        return (V){pack2(x[0], x[1]), pack2(x[2], x[3]), pack2(x[4], x[5]), pack2(x[6], x[7])};
+    }
+    __device__ static __forceinline__ float to_f(S s) { return __uint_as_float((unsigned)s << 16); }
+    __device__ static __forceinline__ S from_f(float f) { return __builtin_bit_cast(unsigned short, (__bf16)f); }
+};
+
+struct IoF16 {
+    typedef unsigned short S;  // binary16 bits
+    static constexpr int E = 8;
+    typedef u4 V;
+    __device__ static __forceinline__ float h2f(unsigned short h) { return (float)__builtin_bit_cast(_Float16, h); }
+    __device__ static __forceinline__ void unpack(const V &v, float (&x)[E]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            x[2 * i] = h2f((unsigned short)(v[i] & 0xffffu));
+            x[2 * i + 1] = h2f((unsigned short)(v[i] >> 16));
+        }
+    }
+    __device__ static __forceinline__ unsigned pack2(float a, float b) {
+        const unsigned short lo = __builtin_bit_cast(unsigned short, (_Float16)a);
+        const unsigned short hi = __builtin_bit_cast(unsigned short, (_Float16)b);
+        return (unsigned)lo | ((unsigned)hi << 16);
+    }
+    __device__ static __forceinline__ V pack(const float (&x)[E]) {
+        return (V){pack2(x[0], x[1]), pack2(x[2], x[3]), pack2(x[4], x[5]), pack2(x[6], x[7])};
+    }
+    __device__ static __forceinline__ float to_f(S s) { return h2f(s); }
+    __device__ static __forceinline__ S from_f(float f) { return __builtin_bit_cast(unsigned short, (_Float16)f); }
+};
+
+template <bool NT, class V>
+__device__ __forceinline__ V vload(const V *ptr) {
+    if constexpr (NT)
+        return __builtin_nontemporal_load(ptr);
+    else
+        return *ptr;
+}
+
+template <bool NT, class V>
+__device__ __forceinline__ void vstore(V *ptr, const V &v) {
+    if constexpr (NT)
+        __builtin_nontemporal_store(v, ptr);
+    else
+        *ptr = v;
+}
+
+template <class IO>
+__device__ __forceinline__ typename IO::V splat(float f) {
+    float x[IO::E];
+#pragma unroll
+    for (int i = 0; i < IO::E; ++i) x[i] = f;
+    return IO::pack(x);
+}
+
+template <int E>
+__device__ __forceinline__ float pick(const float (&x)[E], int c) {
+    float r = x[0];
+#pragma unroll
+    for (int i = 1; i < E; ++i) r = (c == i) ? x[i] : r;
+    return r;
+}
+
+}  // namespace mrnnt

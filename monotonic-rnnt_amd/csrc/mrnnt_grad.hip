@@ -1,0 +1,311 @@
+// mrnnt_grad.hip -- logit gradient (replaces compute_grad_kernel, gpu_rnnt_kernel.h:239-288,
+// and the CPU loop cpu_rnnt.h:216-236), with the upstream gradient (grad_scale[b]) fused:
+//   g[v] = exp(z[v] + den + alpha(t-1,s) + beta(t,s) - ll)
+//        - [v == blank]                     exp(lpb + alpha(t-1,s) + beta(t+1,s)   - ll)
+//        - [v != blank, s < S, v == label]  exp(lpe + alpha(t-1,s) + beta(t+1,s+1) - ll)
+// times grad_scale[b]. Per row the three coefficients are formed in fp64 from the recursion state; per
+// element it is one fma + one v_exp_f32 (+ a select for the <= 2 special columns) in fp32 registers,
+// then one conversion to the output element type. Out-of-band lattice rows store 0 * grad_scale (the
+// reference's backward multiplies its zero rows by grad_output); padding rows of the padded layout
+// store 0 (launch_pad_zero).
+#include "mrnnt_device.h"
+
+namespace mrnnt {
+
+struct RowCoef {
+    float c2;  // (den + alpha(t-1,s) + beta(t,s) - ll) * log2(e)
+    float cb;  // blank correction
+    float ce;  // label correction
+    int lab;   // label(s) (-1 for s == S or label == blank)
+};
+
+__device__ __forceinline__ RowCoef row_coef(const DevProblem &p, int t, int T, int S, int s, int64_t row, double ll,
+                                            const int *__restrict__ lab_b) {
+    const int W = S + 1;
+    const double am = (t == 0) ? (s == 0 ? 0.0 : NEG_INF_D) : p.alpha[row - W];
+    const double b0 = p.beta[row];
+    const double b1 = (t == T - 1) ? (s == S ? 0.0 : NEG_INF_D) : p.beta[row + W];
+    const double b2 = (s == S) ? NEG_INF_D : ((t == T - 1) ? (s + 1 == S ? 0.0 : NEG_INF_D) : p.beta[row + W + 1]);
+    const double base = am - ll;
+    RowCoef rc;
+    rc.c2 = (float)(((double)p.den[row] + base + b0) * kLog2eD);
+    rc.cb = (float)exp(p.lpb[row] + base + b1);
+    rc.ce = (s < S) ? (float)exp(p.lpe[row] + base + b2) : 0.0f;
+    const int lab = (s < S) ? lab_b[s] : -1;
+    rc.lab = (lab == p.blank) ? -1 : lab;
+    return rc;
+}
+
+template <class IO>
+__device__ __forceinline__ typename IO::V grad_vec(const typename IO::V &xv, const RowCoef &rc, int j, int blank,
+                                                   float sc) {
+    constexpr int E = IO::E;
+    float x[E];
+    IO::unpack(xv, x);
+    const int v0 = j * E;
+    const int db = blank - v0;
+    const int de = rc.lab >= 0 ? rc.lab - v0 : -1;
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+        float g = fast_exp2(fmaf(x[i], kLog2e, rc.c2));
+        g -= (db == i ? rc.cb : 0.0f) + (de == i ? rc.ce : 0.0f);
+        x[i] = g * sc;
+    }
+    return IO::pack(x);
+}
+
+// Column-walking kernel (grad_variant 0 / 2): workgroups walk lattice columns, the four waves take rows
+// s (R at a time), lanes take 16-byte vectors of the row, U per lane per chunk.
+template <class IO, int U, int R, bool NTL, bool NTS>
+__global__ __launch_bounds__(256) void grad_kernel(DevProblem p, const float *__restrict__ scale,
+                                                       void *__restrict__ grads) {
+    typedef typename IO::V Vec;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int VL = p.V / IO::E;
+    const int blank = p.blank;
+    const Vec *__restrict__ av = reinterpret_cast<const Vec *>(p.acts);
+    Vec *__restrict__ gv = reinterpret_cast<Vec *>(grads);
+
+    Cursor cur;
+    cur.init(p.col_off, p.B, blockIdx.x);
+    for (int64_t c = blockIdx.x; c < p.num_cols; c += gridDim.x) {
+        cur.advance(p.col_off, c);
+        const int b = cur.b;
+        const int T = p.T[b], S = p.S[b];
+        const int t = (int)(c - p.col_off[b]);
+        const int64_t rowc = p.row_off[b] + (int64_t)t * (S + 1);
+        const int64_t arow = acts_col_base(p, b, t, rowc);
+        const int lo = max(0, t - (T - S));
+        const int hi = min(t, S);
+        const double ll = p.ll[b];
+        const float sc = scale ? scale[b] : 1.0f;
+        const Vec zv = splat<IO>(0.0f * sc);
+        const int *__restrict__ lab_b = p.labels + (int64_t)b * p.label_stride;
+
+        for (int s = wave * R; s <= S; s += 4 * R) {
+            RowCoef rc[R];
+            bool ok[R], inb[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int sr = s + r;
+                ok[r] = sr <= S;
+                inb[r] = ok[r] && sr >= lo && sr <= hi;
+                if (inb[r]) rc[r] = row_coef(p, t, T, S, sr, rowc + sr, ll, lab_b);
+                else rc[r] = RowCoef{0.0f, 0.0f, 0.0f, -1};
+            }
+            for (int base = 0; base < VL; base += 64 * U) {
+                Vec x[R][U];
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const int j = base + lane + 64 * u;
+                        if (inb[r] && j < VL) x[r][u] = vload<NTL>(&av[(arow + s + r) * (int64_t)VL + j]);
+                    }
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const int j = base + lane + 64 * u;
+                        if (!ok[r] || j >= VL) continue;
+                        const Vec g = inb[r] ? grad_vec<IO>(x[r][u], rc[r], j, blank, sc) : zv;
+                        vstore<NTS>(&gv[(arow + s + r) * (int64_t)VL + j], g);
+                    }
+            }
+        }
+    }
+}
+
+// Row-stride kernel (grad_variant 3, packed layout only): every wave of the grid sweeps lattice rows in
+// memory order (wave w takes rows w, w + nwaves, ...), so the grid streams one contiguous window of acts
+// and grads like a grid-stride copy; (b, t, s) of a row come from a per-wave monotone cursor over row_off
+// and one 32-bit division.
+template <class IO, int U, bool NTL, bool NTS>
+__global__ __launch_bounds__(256) void grad_rows_kernel(DevProblem p, const float *__restrict__ scale,
+                                                            void *__restrict__ grads) {
+    typedef typename IO::V Vec;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t gw = (int64_t)blockIdx.x * 4 + wave;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    const int VL = p.V / IO::E;
+    const int blank = p.blank;
+    const Vec *__restrict__ av = reinterpret_cast<const Vec *>(p.acts);
+    Vec *__restrict__ gv = reinterpret_cast<Vec *>(grads);
+
+    Cursor cur;
+    cur.init(p.row_off, p.B, gw);
+    for (int64_t row = gw; row < p.num_rows; row += nw) {
+        cur.advance(p.row_off, row);
+        const int b = cur.b;
+        const int T = p.T[b], S = p.S[b];
+        const unsigned loc = (unsigned)(row - p.row_off[b]);
+        const int t = (int)(loc / (unsigned)(S + 1));
+        const int s = (int)(loc - (unsigned)t * (unsigned)(S + 1));
+        const bool inb = s <= t && (S - s) <= (T - t);
+        const float sc = scale ? scale[b] : 1.0f;
+        Vec *__restrict__ out = gv + row * (int64_t)VL;
+        if (!inb) {
+            const Vec zv = splat<IO>(0.0f * sc);
+            for (int j = lane; j < VL; j += 64) vstore<NTS>(out + j, zv);
+            continue;
+        }
+        const RowCoef rc = row_coef(p, t, T, S, s, row, p.ll[b], p.labels + (int64_t)b * p.label_stride);
+        for (int base = 0; base < VL; base += 64 * U) {
+            Vec x[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int j = base + lane + 64 * u;
+                if (j < VL) x[u] = vload<NTL>(&av[row * (int64_t)VL + j]);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int j = base + lane + 64 * u;
+                if (j < VL) vstore<NTS>(out + j, grad_vec<IO>(x[u], rc, j, blank, sc));
+            }
+        }
+    }
+}
+
+// Scalar path (any V, any alignment): one row per wave, lanes stride over v.
+template <class IO>
+__global__ __launch_bounds__(256) void grad_scalar_kernel(DevProblem p, const float *__restrict__ scale,
+                                                          void *__restrict__ grads) {
+    typedef typename IO::S Sc;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int V = p.V;
+    const int blank = p.blank;
+    const Sc *__restrict__ acts = reinterpret_cast<const Sc *>(p.acts);
+    Sc *__restrict__ gs = reinterpret_cast<Sc *>(grads);
+    Cursor cur;
+    cur.init(p.col_off, p.B, blockIdx.x);
+    for (int64_t c = blockIdx.x; c < p.num_cols; c += gridDim.x) {
+        cur.advance(p.col_off, c);
+        const int b = cur.b;
+        const int T = p.T[b], S = p.S[b];
+        const int t = (int)(c - p.col_off[b]);
+        const int64_t rowc = p.row_off[b] + (int64_t)t * (S + 1);
+        const int64_t arow = acts_col_base(p, b, t, rowc);
+        const int lo = max(0, t - (T - S));
+        const int hi = min(t, S);
+        const double ll = p.ll[b];
+        const float sc = scale ? scale[b] : 1.0f;
+        const Sc zs = IO::from_f(0.0f * sc);
+        const int *__restrict__ lab_b = p.labels + (int64_t)b * p.label_stride;
+        for (int s = wave; s <= S; s += 4) {
+            Sc *__restrict__ g = gs + (arow + s) * (int64_t)V;
+            if (s < lo || s > hi) {
+                for (int v = lane; v < V; v += 64) g[v] = zs;
+                continue;
+            }
+            const RowCoef rc = row_coef(p, t, T, S, s, rowc + s, ll, lab_b);
+            const Sc *__restrict__ z = acts + (arow + s) * (int64_t)V;
+            for (int v = lane; v < V; v += 64) {
+                float gv = fast_exp2(fmaf(IO::to_f(z[v]), kLog2e, rc.c2));
+                if (v == blank) gv -= rc.cb;
+                else if (v == rc.lab) gv -= rc.ce;
+                g[v] = IO::from_f(gv * sc);
+            }
+        }
+    }
+}
+
+// Padded layout: rows (b, t, s) with t >= T_b or s > S_b are not lattice rows; their gradient is 0.
+// One wave per padded row, grid-stride; lattice rows are skipped (written by the gradient kernel).
+template <class IO>
+__global__ __launch_bounds__(256) void pad_zero_kernel(DevProblem p, void *__restrict__ grads, int vec) {
+    typedef typename IO::S Sc;
+    typedef typename IO::V Vec;
+    const int lane = threadIdx.x & 63;
+    const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    const int64_t rows = (int64_t)p.B * p.pad_T * p.pad_S1;
+    const int V = p.V;
+    for (int64_t row = gw; row < rows; row += nw) {
+        const int64_t bt = row / p.pad_S1;
+        const int s = (int)(row - bt * p.pad_S1);
+        const int b = (int)(bt / p.pad_T);
+        const int t = (int)(bt - (int64_t)b * p.pad_T);
+        if (t < p.T[b] && s <= p.S[b]) continue;
+        if (vec) {
+            const int VL = V / IO::E;
+            Vec *__restrict__ g = reinterpret_cast<Vec *>(grads) + row * (int64_t)VL;
+            const Vec zv = splat<IO>(0.0f);
+            for (int j = lane; j < VL; j += 64) vstore<true>(g + j, zv);
+        } else {
+            Sc *__restrict__ g = reinterpret_cast<Sc *>(grads) + row * (int64_t)V;
+            const Sc zs = IO::from_f(0.0f);
+            for (int v = lane; v < V; v += 64) g[v] = zs;
+        }
+    }
+}
+
+template <class IO>
+static bool vec_ok(const DevProblem &p, const void *grads) {
+    return (p.V % IO::E) == 0 && (reinterpret_cast<uintptr_t>(p.acts) % 16) == 0 &&
+           (reinterpret_cast<uintptr_t>(grads) % 16) == 0;
+}
+
+template <class IO, bool NTL, bool NTS>
+static void launch_vec(const DevProblem &p, const float *scale, void *grads, int grid, hipStream_t stream) {
+    const int VL = p.V / IO::E;
+    const int variant = tuning().grad_variant;
+    if (variant == 3 && p.pad_S1 == 0 && VL >= 192)
+        grad_rows_kernel<IO, 4, NTL, NTS><<<grid, 256, 0, stream>>>(p, scale, grads);
+    else if (VL >= 192 && variant == 2)
+        grad_kernel<IO, 4, 2, NTL, NTS><<<grid, 256, 0, stream>>>(p, scale, grads);
+    else if (VL >= 192)
+        grad_kernel<IO, 4, 1, NTL, NTS><<<grid, 256, 0, stream>>>(p, scale, grads);
+    else if (VL >= 96)
+        grad_kernel<IO, 2, 2, NTL, NTS><<<grid, 256, 0, stream>>>(p, scale, grads);
+    else
+        grad_kernel<IO, 1, 4, NTL, NTS><<<grid, 256, 0, stream>>>(p, scale, grads);
+}
+
+template <class IO>
+static void launch_io(const DevProblem &p, const float *scale, void *grads, int grid, hipStream_t stream) {
+    if (!vec_ok<IO>(p, grads)) {
+        grad_scalar_kernel<IO><<<grid, 256, 0, stream>>>(p, scale, grads);
+        return;
+    }
+    const bool ntl = tuning().nt_load != 0, nts = tuning().nt_store != 0;
+    if (ntl && nts) launch_vec<IO, true, true>(p, scale, grads, grid, stream);
+    else if (ntl) launch_vec<IO, true, false>(p, scale, grads, grid, stream);
+    else if (nts) launch_vec<IO, false, true>(p, scale, grads, grid, stream);
+    else launch_vec<IO, false, false>(p, scale, grads, grid, stream);
+}
+
+hipError_t launch_grad(const DevProblem &p, int elem, const float *scale, void *grads, int grid, hipStream_t stream) {
+    switch (elem) {
+        case ELEM_F32: launch_io<IoF32>(p, scale, grads, grid, stream); break;
+        case ELEM_BF16: launch_io<IoBF16>(p, scale, grads, grid, stream); break;
+        case ELEM_F16: launch_io<IoF16>(p, scale, grads, grid, stream); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_pad_zero(const DevProblem &p, int elem, void *grads, hipStream_t stream) {
+    if (p.pad_S1 == 0) return hipSuccess;
+    const int64_t rows = (int64_t)p.B * p.pad_T * p.pad_S1;
+    if (rows == 0) return hipSuccess;
+    int64_t blocks = (rows + 3) / 4;
+    if (blocks > 8192) blocks = 8192;
+    switch (elem) {
+        case ELEM_F32:
+            pad_zero_kernel<IoF32><<<(int)blocks, 256, 0, stream>>>(p, grads, (int)vec_ok<IoF32>(p, grads));
+            break;
+        case ELEM_BF16:
+            pad_zero_kernel<IoBF16><<<(int)blocks, 256, 0, stream>>>(p, grads, (int)vec_ok<IoBF16>(p, grads));
+            break;
+        case ELEM_F16:
+            pad_zero_kernel<IoF16><<<(int)blocks, 256, 0, stream>>>(p, grads, (int)vec_ok<IoF16>(p, grads));
+            break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace mrnnt

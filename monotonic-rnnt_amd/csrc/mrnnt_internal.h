@@ -1,5 +1,5 @@
-// mrnnt_internal.h -- device problem descriptor and kernel launchers shared by the host code
-// (mrnnt_capi.cpp) and the kernels (mrnnt_kernels.hip). Not installed; not part of the ABI.
+// mrnnt_internal.h -- device problem descriptor, launch knobs and kernel launchers shared by the host
+// code (mrnnt_capi.cpp) and the kernels (mrnnt_*.hip). Not installed; not part of the ABI.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -7,10 +7,15 @@
 
 namespace mrnnt {
 
+// Element type of acts and grads (the math is fp32/fp64 inside the kernels).
+enum ElemType { ELEM_F32 = 0, ELEM_BF16 = 1, ELEM_F16 = 2 };
+
 // Everything a kernel needs, passed by value as a kernel argument.
-// Row r = (b, t, s) lives at row_off[b] + t*(S_b+1) + s; column (b, t) at col_off[b] + t.
+// Internal per-row arrays use the packed lattice row r = row_off[b] + t*(S_b+1) + s (column (b, t) at
+// col_off[b] + t). acts/grads rows use the caller's layout: packed (the same r) or padded
+// [B, pad_T, pad_S1, V] with row (b*pad_T + t)*pad_S1 + s.
 struct DevProblem {
-    const float *acts;          // [N, V]
+    const void *acts;           // [rows, V] of elem type
     const int *labels;          // [B, label_stride]
     int64_t label_stride;
     const int *T;               // [B]
@@ -21,6 +26,8 @@ struct DevProblem {
     const int *max_s;           // [cols]
     int B, V, blank;
     int64_t num_cols;           // sum_b T_b
+    int64_t num_rows;           // N = sum_b T_b (S_b + 1)
+    int64_t pad_T, pad_S1;      // padded acts layout (pad_S1 == 0: packed)
     float *den;                 // [N]  log-softmax denominator  -max - log sum exp(z - max)
     double *lpb;                // [N]  z[r, blank] + den[r]
     double *lpe;                // [N]  z[r, label(s)] + den[r]   (s < S)
@@ -32,13 +39,12 @@ struct DevProblem {
 
 // Launch-shape knobs (experiment hook: mrnnt_tune in mrnnt_capi.cpp). Defaults are the tuned values.
 struct Tuning {
-    int softmax_variant = 2;  // 0 = row-at-a-time, 1 = software-pipelined, 2 = two rows per wave (V >= 768)
-    int grad_variant = 0;     // 0 = row-at-a-time, 1 = software-pipelined, 2 = two rows per wave (V >= 768)
+    int softmax_variant = 2;      // rows per wave of the log-softmax kernel: 0 -> 1 row, 2 -> 2 rows (large V)
+    int grad_variant = 0;         // 0 -> 1 row per wave, 2 -> 2 rows per wave, 3 -> row-stride sweep (packed)
     int softmax_grid_per_cu = 0;  // workgroups (of 4 waves) per CU; 0 = one workgroup per lattice column
     int grad_grid_per_cu = 32;    // same for the gradient kernel
-    int nt_store = 1;         // nontemporal stores of grads
-    int nt_load = 1;          // nontemporal loads of acts (both streaming kernels)
-    int dp_variant = 1;       // 0 = one wave/direction (shuffles), 1 = four waves (DPP + LDS), 2 = one wave (DPP)
+    int nt_store = 1;             // nontemporal stores of grads
+    int nt_load = 1;              // nontemporal loads of acts (both streaming kernels)
 };
 Tuning &tuning();
 
@@ -48,14 +54,16 @@ enum KernelId { K_BAND = 0, K_SOFTMAX = 1, K_DP = 2, K_GRAD = 3, K_SETUP = 4, K_
 hipError_t launch_setup(const int *T, const int *S, int B, int64_t *row_off, int64_t *col_off, hipStream_t stream);
 hipError_t launch_align(const DevProblem &p, const int *alignment, int64_t align_stride, int align_blank,
                         int max_shift, int *mtmp, int *min_s, int *max_s, hipStream_t stream);
-hipError_t launch_softmax(const DevProblem &p, int grid, hipStream_t stream);
+hipError_t launch_softmax(const DevProblem &p, int elem, int grid, hipStream_t stream);
 hipError_t launch_dp(const DevProblem &p, int S_max, int with_beta, float *costs, hipStream_t stream);
-hipError_t launch_grad(const DevProblem &p, const float *scale, float *grads, int grid, hipStream_t stream);
+hipError_t launch_grad(const DevProblem &p, int elem, const float *scale, void *grads, int grid, hipStream_t stream);
+hipError_t launch_pad_zero(const DevProblem &p, int elem, void *grads, hipStream_t stream);
 hipError_t launch_synth(float *out, int64_t begin, int64_t count, uint64_t seed, int normal, hipStream_t stream);
 
-// Largest S+1 the DP kernel instantiations cover (64 lanes x 32 cells per lane).
-constexpr int kMaxLabelsPlusOne = 64 * 32;
-// Padding (elements) around the lp arrays so the DP's whole-wave row loads never leave the allocation.
-constexpr int64_t kLpPad = 64 * 32 + 64;
+// Largest S+1 the recursion instantiations cover (8 waves x 64 lanes x 4 cells per lane).
+constexpr int kMaxLabelsPlusOne = 2048;
+// Padding (elements) around the lp arrays so the recursion's whole-workgroup row loads never leave the
+// allocation (>= the largest lanes x cells block).
+constexpr int64_t kLpPad = 2048 + 64;
 
 }  // namespace mrnnt

@@ -1,0 +1,207 @@
+// mrnnt_softmax.hip -- log-softmax row reduce (replaces reference reduce.h:79-154 and the
+// strided acts gathers of gpu_rnnt_kernel.h:80-84).
+//
+// One pass over the in-band rows of acts. Work decomposition: workgroups walk lattice columns (b, t)
+// (one workgroup per column by default, or a persistent grid with a monotone utterance cursor); inside a
+// column the four waves take rows s. Per row each lane keeps an online (max, sum-exp) over its 16-byte
+// vector loads, one wave64 butterfly merges the pairs, den = -max - log(sum) is formed in fp64, and the
+// blank / label logits are captured from registers on the way, so the kernel also emits
+//   lpb[r] = z[r, blank] + den[r],   lpe[r] = z[r, label(s)] + den[r]
+// -- the only two log-probs the recursion reads. Rows outside the band are never read; their lp entries
+// are zero-filled (finite) so the recursion needs no guards.
+#include "mrnnt_device.h"
+
+namespace mrnnt {
+
+__device__ __forceinline__ void zero_fill_outside_band(const DevProblem &p, int64_t rowc, int S, int lo, int hi) {
+    for (int s = threadIdx.x; s <= S; s += blockDim.x)
+        if (s < lo || s > hi) {
+            p.lpb[rowc + s] = 0.0;
+            p.lpe[rowc + s] = 0.0;
+        }
+}
+
+__device__ __forceinline__ void write_row(const DevProblem &p, int64_t row, float m, float sum, float zb, float ze) {
+    const double den = -(double)m - log((double)sum);
+    p.den[row] = (float)den;
+    p.lpb[row] = (double)zb + den;
+    p.lpe[row] = (double)ze + den;
+}
+
+// Vector path: V % E == 0, 16-byte aligned rows. U = vector loads per lane per chunk (a chunk covers
+// 64*U*E elements), R = rows a wave reduces at once (U*R vector loads in flight per lane).
+template <class IO, int U, int R, bool NTL>
+__global__ __launch_bounds__(256) void softmax_kernel(DevProblem p) {
+    constexpr int E = IO::E;
+    typedef typename IO::V Vec;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int VL = p.V / E;  // vector loads per row
+    const Vec *__restrict__ av = reinterpret_cast<const Vec *>(p.acts);
+    const int blank = p.blank;
+    const int bj = blank / E, bc = blank % E, blane = bj & 63;
+    const Vec ninf = splat<IO>(NEG_INF_F);
+
+    Cursor cur;
+    cur.init(p.col_off, p.B, blockIdx.x);
+    for (int64_t c = blockIdx.x; c < p.num_cols; c += gridDim.x) {
+        cur.advance(p.col_off, c);
+        const int b = cur.b;
+        const int T = p.T[b], S = p.S[b];
+        const int t = (int)(c - p.col_off[b]);
+        const int64_t rowc = p.row_off[b] + (int64_t)t * (S + 1);
+        const int64_t arow = acts_col_base(p, b, t, rowc);
+        const int lo = max(0, t - (T - S));
+        const int hi = min(t, S);
+        const int *__restrict__ lab_b = p.labels + (int64_t)b * p.label_stride;
+        zero_fill_outside_band(p, rowc, S, lo, hi);
+
+        for (int s = lo + wave * R; s <= hi; s += 4 * R) {
+            float m[R], sum[R], zb[R], ze[R];
+            int lab[R];
+            bool ok[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int sr = s + r;
+                ok[r] = sr <= hi;
+                lab[r] = (ok[r] && sr < S) ? lab_b[sr] : -1;
+                m[r] = NEG_INF_F;
+                sum[r] = 0.0f;
+                zb[r] = 0.0f;
+                ze[r] = 0.0f;
+            }
+            for (int base = 0; base < VL; base += 64 * U) {
+                Vec x[R][U];
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const int j = base + lane + 64 * u;
+                        if (ok[r] && j < VL)
+                            x[r][u] = vload<NTL>(&av[(arow + s + r) * (int64_t)VL + j]);
+                        else
+                            x[r][u] = ninf;
+                    }
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    float xf[U][E];
+                    float cm = NEG_INF_F;
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const int j = base + lane + 64 * u;
+                        IO::unpack(x[r][u], xf[u]);
+#pragma unroll
+                        for (int i = 0; i < E; ++i) cm = fmaxf(cm, xf[u][i]);
+                        if (j == bj) zb[r] = pick<E>(xf[u], bc);
+                        if (lab[r] >= 0 && j == lab[r] / E) ze[r] = pick<E>(xf[u], lab[r] % E);
+                    }
+                    const float mn = fmaxf(m[r], cm);
+                    const float mr = (mn == NEG_INF_F) ? 0.0f : mn;
+                    float acc = sum[r] * fast_exp2((m[r] - mr) * kLog2e);
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+#pragma unroll
+                        for (int i = 0; i < E; ++i) acc += fast_exp2((xf[u][i] - mr) * kLog2e);
+                    sum[r] = acc;
+                    m[r] = mn;
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r) wave_reduce_max_sum(m[r], sum[r]);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                if (!ok[r]) continue;
+                const float zbv = __shfl(zb[r], blane);
+                const float zev = lab[r] >= 0 ? __shfl(ze[r], (lab[r] / E) & 63) : 0.0f;
+                if (lane == 0) write_row(p, rowc + s + r, m[r], sum[r], zbv, zev);
+            }
+        }
+    }
+}
+
+// Scalar path (any V, any alignment, any element type): one row per wave, lanes stride over v.
+template <class IO>
+__global__ __launch_bounds__(256) void softmax_scalar_kernel(DevProblem p) {
+    typedef typename IO::S Sc;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int V = p.V;
+    const int blank = p.blank;
+    const Sc *__restrict__ acts = reinterpret_cast<const Sc *>(p.acts);
+    Cursor cur;
+    cur.init(p.col_off, p.B, blockIdx.x);
+    for (int64_t c = blockIdx.x; c < p.num_cols; c += gridDim.x) {
+        cur.advance(p.col_off, c);
+        const int b = cur.b;
+        const int T = p.T[b], S = p.S[b];
+        const int t = (int)(c - p.col_off[b]);
+        const int64_t rowc = p.row_off[b] + (int64_t)t * (S + 1);
+        const int64_t arow = acts_col_base(p, b, t, rowc);
+        const int lo = max(0, t - (T - S));
+        const int hi = min(t, S);
+        const int *__restrict__ lab_b = p.labels + (int64_t)b * p.label_stride;
+        zero_fill_outside_band(p, rowc, S, lo, hi);
+        for (int s = lo + wave; s <= hi; s += 4) {
+            const int lab = s < S ? lab_b[s] : -1;
+            const Sc *__restrict__ z = acts + (arow + s) * (int64_t)V;
+            float m = NEG_INF_F, sum = 0.0f, zb = 0.0f, ze = 0.0f;
+            for (int v0 = 0; v0 < V; v0 += 256) {
+                float x[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int v = v0 + lane + 64 * u;
+                    x[u] = v < V ? IO::to_f(z[v]) : NEG_INF_F;
+                    if (v == blank) zb = x[u];
+                    if (v == lab) ze = x[u];
+                }
+                const float mn = fmaxf(m, fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])));
+                const float mr = (mn == NEG_INF_F) ? 0.0f : mn;
+                float acc = sum * fast_exp2((m - mr) * kLog2e);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) acc += fast_exp2((x[u] - mr) * kLog2e);
+                sum = acc;
+                m = mn;
+            }
+            wave_reduce_max_sum(m, sum);
+            const float zbv = __shfl(zb, blank & 63);
+            const float zev = lab >= 0 ? __shfl(ze, lab & 63) : 0.0f;
+            if (lane == 0) write_row(p, rowc + s, m, sum, zbv, zev);
+        }
+    }
+}
+
+template <class IO, bool NTL>
+static void launch_vec(const DevProblem &p, int grid, hipStream_t stream) {
+    const int VL = p.V / IO::E;
+    if (VL >= 192 && tuning().softmax_variant == 2)
+        softmax_kernel<IO, 4, 2, NTL><<<grid, 256, 0, stream>>>(p);
+    else if (VL >= 192)
+        softmax_kernel<IO, 4, 1, NTL><<<grid, 256, 0, stream>>>(p);
+    else if (VL >= 96)
+        softmax_kernel<IO, 2, 2, NTL><<<grid, 256, 0, stream>>>(p);
+    else
+        softmax_kernel<IO, 1, 4, NTL><<<grid, 256, 0, stream>>>(p);
+}
+
+template <class IO>
+static void launch_io(const DevProblem &p, int grid, hipStream_t stream) {
+    const bool vec = (p.V % IO::E) == 0 && (reinterpret_cast<uintptr_t>(p.acts) % 16) == 0;
+    if (!vec)
+        softmax_scalar_kernel<IO><<<grid, 256, 0, stream>>>(p);
+    else if (tuning().nt_load)
+        launch_vec<IO, true>(p, grid, stream);
+    else
+        launch_vec<IO, false>(p, grid, stream);
+}
+
+hipError_t launch_softmax(const DevProblem &p, int elem, int grid, hipStream_t stream) {
+    switch (elem) {
+        case ELEM_F32: launch_io<IoF32>(p, grid, stream); break;
+        case ELEM_BF16: launch_io<IoBF16>(p, grid, stream); break;
+        case ELEM_F16: launch_io<IoF16>(p, grid, stream); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace mrnnt

@@ -20,6 +20,11 @@ RNNT_STATUS_UNKNOWN_ERROR = 4
 STATUS_NAMES = {0: "no error", 1: "device memcpy or memset failed", 2: "invalid value", 3: "execution failed",
                 4: "unknown error"}
 
+# acts / grads element types (MRNNT_F32 / MRNNT_BF16 / MRNNT_F16 in include/mrnnt.h)
+MRNNT_F32 = 0
+MRNNT_BF16 = 1
+MRNNT_F16 = 2
+
 # kernel-family order of mrnnt_profile_read
 KERNELS = ("band", "log_softmax", "alpha_beta", "grad", "setup")
 
@@ -41,6 +46,10 @@ class MrnntProblem(ctypes.Structure):
         ("align_stride", ctypes.c_int64),
         ("align_blank", ctypes.c_int),
         ("num_rows", ctypes.c_int64),
+        # version 2 (zero = the reference contract: packed fp32 acts)
+        ("acts_dtype", ctypes.c_int),
+        ("pad_T", ctypes.c_int64),
+        ("pad_S1", ctypes.c_int64),
     ]
 
 
@@ -84,6 +93,9 @@ def load() -> ctypes.CDLL:
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        if lib.mrnnt_version() < 2:
+            raise ImportError(f"{LIB_PATH} is a stale build (ABI version {lib.mrnnt_version()} < 2); "
+                              "rebuild with `make -C monotonic-rnnt_amd`")
         _lib = lib
         return lib
 

@@ -19,6 +19,9 @@ Behavioural differences from the reference, all deliberate:
   * costs are computed on the device (the reference computes into a host tensor and copies, :37, :90);
   * labels / alignment use their true row strides (the reference assumes max(S) / max(T));
   * MonotonicRNNTLoss.forward uses self.blank_label (the reference reads a missing self.blank, :214).
+
+Extensions beyond the reference: bf16/fp16 acts (costs stay fp32) and the padded
+[B, pad_T, pad_S1, V] acts layout, both read in place by the same kernels.
 """
 from __future__ import annotations
 
@@ -36,6 +39,10 @@ except ImportError:  # imported with pytorch_binding/ on sys.path, like the refe
 _L.load()  # fail loudly at import if the HIP library is missing
 
 
+# acts element types the kernels read (the arithmetic is fp32/fp64 in registers whatever the type)
+_ELEM = {torch.float32: _L.MRNNT_F32, torch.bfloat16: _L.MRNNT_BF16, torch.float16: _L.MRNNT_F16}
+
+
 def _ptr(t: Optional[torch.Tensor]):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
@@ -47,10 +54,12 @@ class _Prepared:
         if not acts.is_cuda:
             raise RuntimeError("monotonic_rnnt (MI355X build): acts must be a GPU tensor; "
                                "this build has no CPU implementation")
-        if acts.dtype != torch.float32:
-            raise RuntimeError("monotonic_rnnt: acts must be float32 (reference monotonic_rnnt.cu:19,84)")
-        if acts.dim() != 2:
-            raise RuntimeError("monotonic_rnnt: acts must be packed 2-D [sum_b T_b (S_b+1), V]")
+        if acts.dtype not in _ELEM:
+            raise RuntimeError("monotonic_rnnt: acts must be float32 (reference monotonic_rnnt.cu:19,84), "
+                               f"or bfloat16 / float16 (extension); got {acts.dtype}")
+        if acts.dim() not in (2, 4):
+            raise RuntimeError("monotonic_rnnt: acts must be packed 2-D [sum_b T_b (S_b+1), V] "
+                               "or padded 4-D [B, max_T, max_S+1, V]")
         dev = acts.device
         self.acts = acts.contiguous()
         B = labels.size(0)
@@ -71,7 +80,7 @@ class _Prepared:
             self.alignment = (al.view(B, -1) if al.dim() == 1 else al).contiguous()
         p = _L.MrnntProblem()
         p.B = B
-        p.V = self.acts.size(1)
+        p.V = self.acts.size(-1)
         p.blank = int(blank_label)
         p.max_shift = int(max_shift)
         p.T_host = self.T_host.ctypes.data
@@ -84,7 +93,14 @@ class _Prepared:
         p.alignment = self.alignment.data_ptr() if self.alignment is not None else None
         p.align_stride = self.alignment.size(1) if self.alignment is not None else 0
         p.align_blank = int(blank_label)  # the reference parses the alignment with the same blank (monotonic_rnnt.cu:144)
-        p.num_rows = self.acts.size(0)
+        p.acts_dtype = _ELEM[self.acts.dtype]
+        if self.acts.dim() == 4:
+            if self.acts.size(0) != B:
+                raise RuntimeError(f"monotonic_rnnt: padded acts has {self.acts.size(0)} utterances, labels {B}")
+            p.pad_T, p.pad_S1 = self.acts.size(1), self.acts.size(2)
+            p.num_rows = B * p.pad_T * p.pad_S1
+        else:
+            p.num_rows = self.acts.size(0)
         self.problem = p
         self.device = dev
 
@@ -152,6 +168,9 @@ def monotonic_rnnt_loss(acts: torch.Tensor, labels: torch.Tensor, input_lengths:
     Args (reference monotonic_rnnt_op.py:130-160):
         acts:           packed 2-D float32 GPU tensor of logits, (sum_b T_b*(S_b+1), V), utterance b
                         contiguous, then t-major, then s. Softmax is applied internally.
+                        Extensions: bfloat16 / float16 elements (fp32 math; grads in the same type), and
+                        the padded 4-D joint-network layout [B, pad_T >= max T, pad_S1 >= max S + 1, V]
+                        read in place (no packing copy; grads of padding rows are 0).
         labels:         2-D int tensor [B, max_b S_b] of padded label sequences.
         input_lengths:  1-D int tensor [B] of T_b.
         label_lengths:  1-D int tensor [B] of S_b.
@@ -198,8 +217,8 @@ class _Ext:
         want = grads is not None and grads.numel() > 0
         c, ws = _forward(prep, with_beta=want)
         if want:
-            if not grads.is_cuda or grads.dtype != torch.float32 or not grads.is_contiguous():
-                raise RuntimeError("grads must be a contiguous float32 GPU tensor")
+            if not grads.is_cuda or grads.dtype != prep.acts.dtype or not grads.is_contiguous():
+                raise RuntimeError(f"grads must be a contiguous {prep.acts.dtype} GPU tensor")
             if grads.shape != prep.acts.shape:
                 raise RuntimeError(f"grads must have the shape of acts {tuple(prep.acts.shape)}")
             with torch.cuda.device(prep.device):

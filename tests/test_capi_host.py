@@ -118,3 +118,41 @@ def test_torch_op_rejects_cpu_tensors():
         op.monotonic_rnnt_loss(acts, torch.tensor([[1, 2]], dtype=torch.int32), torch.tensor([4]), torch.tensor([2]))
     with pytest.raises(RuntimeError):
         op.monotonic_rnnt_cpp.cpu_monotonic_rnnt(acts, None, None, None, None, None, 0, 0)
+
+
+def test_ctypes_problem_struct_matches_c_layout():
+    """The ctypes mirror of mrnnt_problem has the C header's size and field offsets (checked with gcc)."""
+    import _mrnnt_lib as L
+    fields = [f for f, _ in L.MrnntProblem._fields_]
+    body = "".join(f'printf("%zu\\n", offsetof(mrnnt_problem, {f}));' for f in fields)
+    src = ('#include <stddef.h>\n#include <stdio.h>\n#include "mrnnt.h"\n'
+           f'int main(void){{ printf("%zu\\n", sizeof(mrnnt_problem)); {body} return 0; }}\n')
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        exe = os.path.join(d, "layout")
+        r = subprocess.run(["gcc", "-std=c11", "-I", INC, "-x", "c", "-", "-o", exe], input=src,
+                           capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr
+        vals = [int(x) for x in subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()]
+    assert vals[0] == ctypes.sizeof(L.MrnntProblem)
+    assert vals[1:] == [getattr(L.MrnntProblem, f).offset for f in fields]
+
+
+def test_padded_layout_and_dtype_validation(lib):
+    import _mrnnt_lib as L
+    n = ctypes.c_size_t(0)
+    p, keep = _problem([4, 7], [2, 5])
+    p.pad_T, p.pad_S1 = 7, 6
+    p.num_rows = 2 * 7 * 6
+    assert lib.mrnnt_workspace_size(ctypes.byref(p), ctypes.byref(n)) == L.RNNT_STATUS_SUCCESS
+    p.pad_S1 = 5  # < max S + 1
+    p.num_rows = 2 * 7 * 5
+    assert lib.mrnnt_workspace_size(ctypes.byref(p), ctypes.byref(n)) == L.RNNT_STATUS_INVALID_VALUE
+    assert b"padded layout" in lib.mrnnt_last_error()
+    p.pad_T, p.pad_S1, p.num_rows = 7, 6, 2 * 7 * 6 - 1  # wrong row count for the padded layout
+    assert lib.mrnnt_workspace_size(ctypes.byref(p), ctypes.byref(n)) == L.RNNT_STATUS_INVALID_VALUE
+    p.num_rows = 2 * 7 * 6
+    for dt, ok in ((L.MRNNT_F32, True), (L.MRNNT_BF16, True), (L.MRNNT_F16, True), (3, False), (-1, False)):
+        p.acts_dtype = dt
+        st = lib.mrnnt_workspace_size(ctypes.byref(p), ctypes.byref(n))
+        assert (st == L.RNNT_STATUS_SUCCESS) == ok, dt

@@ -243,19 +243,19 @@ def test_config_c2_vs_oracle(op, dev):
 
 
 @pytest.mark.parametrize("knobs", [
-    {"softmax_variant": 0, "grad_variant": 0, "dp_variant": 0, "grid_per_cu": 8, "nt_store": 1},
-    {"softmax_variant": 1, "grad_variant": 1, "dp_variant": 1, "grid_per_cu": 0, "nt_store": 0},
-    {"softmax_variant": 1, "grad_variant": 0, "dp_variant": 1, "grid_per_cu": 3, "nt_store": 1},
-    {"softmax_variant": 0, "grad_variant": 0, "dp_variant": 1, "softmax_grid_per_cu": 0, "grad_grid_per_cu": 32},
-    {"softmax_variant": 2, "grad_variant": 2, "dp_variant": 2, "softmax_grid_per_cu": 0, "grad_grid_per_cu": 32},
-    {"softmax_variant": 2, "grad_variant": 0, "dp_variant": 3, "softmax_grid_per_cu": 0, "grad_grid_per_cu": 32},
-    {"softmax_variant": 0, "grad_variant": 2, "dp_variant": 1, "nt_load": 0, "nt_store": 0},
-    {"softmax_variant": 0, "grad_variant": 1, "dp_variant": 0, "grid_per_cu": 16, "nt_store": 1},
+    {"softmax_variant": 0, "grad_variant": 0, "grid_per_cu": 8, "nt_store": 1},
+    {"softmax_variant": 2, "grad_variant": 2, "grid_per_cu": 0, "nt_store": 0},
+    {"softmax_variant": 0, "grad_variant": 0, "grid_per_cu": 3, "nt_store": 1},
+    {"softmax_variant": 0, "grad_variant": 0, "softmax_grid_per_cu": 0, "grad_grid_per_cu": 32},
+    {"softmax_variant": 2, "grad_variant": 2, "softmax_grid_per_cu": 0, "grad_grid_per_cu": 32},
+    {"softmax_variant": 0, "grad_variant": 2, "nt_load": 0, "nt_store": 0},
+    {"softmax_variant": 2, "grad_variant": 3, "softmax_grid_per_cu": 5, "grad_grid_per_cu": 7},
+    {"softmax_variant": 0, "grad_variant": 3, "grid_per_cu": 16, "nt_store": 1, "nt_load": 0},
 ])
 def test_every_kernel_variant_matches_oracle(op, dev, knobs):
     """All launch variants selectable through mrnnt_tune compute the same result (alignment included)."""
     import _mrnnt_lib as L
-    saved = {k: L.tune(k) for k in ("softmax_variant", "grad_variant", "dp_variant", "softmax_grid_per_cu",
+    saved = {k: L.tune(k) for k in ("softmax_variant", "grad_variant", "softmax_grid_per_cu",
                                     "grad_grid_per_cu", "nt_store", "nt_load")}
     try:
         for k, v in knobs.items():
@@ -293,3 +293,92 @@ def test_long_label_sequences_vs_oracle(op, dev, S_len, T_len, V):
     cr, gr = O.oracle_rnnt(acts, labels, T, S, num_threads=2)
     assert_costs(c, cr)
     assert_grads(g, gr)
+
+
+# ---------------------------------------------------------------------------------------------
+# extensions: padded [B, pad_T, pad_S1, V] acts read in place; bf16 / fp16 acts
+
+def pack_to_padded(acts, T, S, pad_T, pad_S1, fill=np.nan):
+    """Scatter packed rows into the padded joint-network layout; padding rows hold `fill`."""
+    B, V = len(T), acts.shape[1]
+    out = np.full((B, pad_T, pad_S1, V), fill, np.float32)
+    r = 0
+    for b in range(B):
+        n = int(T[b]) * (int(S[b]) + 1)
+        out[b, : T[b], : S[b] + 1] = acts[r:r + n].reshape(T[b], S[b] + 1, V)
+        r += n
+    return out
+
+
+def padded_to_packed(x, T, S):
+    return np.concatenate([x[b, : T[b], : S[b] + 1].reshape(-1, x.shape[-1]) for b in range(len(T))])
+
+
+@pytest.mark.parametrize("V", [7, 64, 1024])
+def test_padded_layout_bit_identical_to_packed(op, dev, V):
+    """The padded layout reads the same logits in place: costs and lattice grads are bit-identical to the
+    packed run, padding rows of grads are exactly 0 (NaN-filled padding of acts is never read)."""
+    rng = np.random.default_rng(300 + V)
+    acts, labels, T, S = random_problem(rng, 4, (1, 30), 9, V, force={0: (30, 9), 1: (1, 0)})
+    pad_T, pad_S1 = int(T.max()) + 2, int(S.max()) + 3
+    scale = np.array([1.0, -2.0, 0.5, 3.0], np.float32)
+    c, g = run_gpu(op, dev, acts, labels, T, S, scale=scale)
+    xp = torch.from_numpy(pack_to_padded(acts, T, S, pad_T, pad_S1)).to(dev).requires_grad_(True)
+    cp = op.monotonic_rnnt_loss(xp, torch.from_numpy(labels).to(dev), torch.from_numpy(T), torch.from_numpy(S))
+    (cp * torch.from_numpy(scale).to(dev)).sum().backward()
+    gp = xp.grad.cpu().numpy()
+    assert np.array_equal(cp.detach().cpu().numpy().astype(np.float64), c)
+    assert np.array_equal(padded_to_packed(gp, T, S), g)
+    mask = np.ones(gp.shape[:3], bool)
+    for b in range(4):
+        mask[b, : T[b], : S[b] + 1] = False
+    assert np.all(gp[mask] == 0.0)
+    # the reference-named extension function takes the padded layout too
+    costs = torch.zeros(4)
+    grads = torch.empty_like(xp)
+    assert op.monotonic_rnnt_cpp.gpu_monotonic_rnnt(xp.detach(), torch.from_numpy(labels).to(dev),
+                                                    torch.from_numpy(T), torch.from_numpy(S), costs, grads, 0) == 0
+    assert np.array_equal(costs.numpy().astype(np.float64), c)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("V", [15, 256, 1000, 1024])
+def test_reduced_precision_acts_vs_oracle(op, dev, dtype, V):
+    """bf16 / fp16 acts, fp32/fp64 math: parity against the double oracle on the upcast inputs.
+    Tolerance: costs as fp32 (1e-4 relative); grads 1e-4 absolute + one rounding of the output type
+    (2^-8 relative for bf16, 2^-11 for fp16), since grads are stored in the acts element type."""
+    rng = np.random.default_rng(400 + V)
+    acts, labels, T, S = random_problem(rng, 4, (1, 40), 12, V, force={0: (40, 12)})
+    a = torch.from_numpy(acts).to(dev).to(dtype).requires_grad_(True)
+    up = a.detach().float().cpu().numpy()  # the exact values the kernels read
+    scale = np.array([1.0, 0.5, -1.0, 2.0], np.float32)
+    costs = op.monotonic_rnnt_loss(a, torch.from_numpy(labels).to(dev), torch.from_numpy(T), torch.from_numpy(S))
+    assert costs.dtype == torch.float32
+    (costs * torch.from_numpy(scale).to(dev)).sum().backward()
+    assert a.grad.dtype == dtype
+    g = a.grad.float().cpu().numpy()
+    cr, gr = O.oracle_rnnt(up, labels, T, S)
+    gr = gr * np.repeat(scale.astype(np.float64), T * (S + 1))[:, None]
+    assert_costs(costs.detach().cpu().numpy().astype(np.float64), cr)
+    rel = 2.0 ** -8 if dtype == torch.bfloat16 else 2.0 ** -11
+    err = np.abs(g - gr) - rel * np.abs(gr)
+    assert err.max() <= GRAD_TOL, err.max()
+
+
+def test_reduced_precision_padded_and_aligned(op, dev):
+    """bf16 + padded layout + alignment band together, against the oracle on the upcast packed inputs."""
+    rng = np.random.default_rng(555)
+    acts, labels, T, S = random_problem(rng, 3, (20, 60), 10, 128)
+    al = np.zeros((3, int(T.max())), np.int32)
+    for b in range(3):
+        al[b, np.sort(rng.choice(T[b], S[b], replace=False))] = labels[b, : S[b]]
+    pad = pack_to_padded(acts, T, S, int(T.max()), int(S.max()) + 1, fill=0.0)
+    x = torch.from_numpy(pad).to(dev).to(torch.bfloat16).requires_grad_(True)
+    up = padded_to_packed(x.detach().float().cpu().numpy(), T, S)
+    costs = op.monotonic_rnnt_loss(x, torch.from_numpy(labels).to(dev), torch.from_numpy(T), torch.from_numpy(S),
+                                   torch.from_numpy(al).to(dev), 2)
+    costs.sum().backward()
+    g = padded_to_packed(x.grad.float().cpu().numpy(), T, S)
+    cr, gr = O.oracle_rnnt(up, labels, T, S, alignment=al, max_shift=2)
+    assert_costs(costs.detach().cpu().numpy().astype(np.float64), cr)
+    assert (np.abs(g - gr) - 2.0 ** -8 * np.abs(gr)).max() <= GRAD_TOL

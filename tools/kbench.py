@@ -43,7 +43,7 @@ def main():
 
     lib = L.load()
     DEFAULTS = {k: L.tune(k) for k in ("softmax_variant", "grad_variant", "softmax_grid_per_cu", "grad_grid_per_cu",
-                                       "nt_store", "nt_load", "dp_variant")}
+                                       "nt_store", "nt_load")}
     dev = torch.device("cuda:0")
     T, S, V, workload = lengths_for(args.config, 0, 1)
     B = len(T)
