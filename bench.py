@@ -8,8 +8,10 @@ the single RCCL all-reduce of the summed loss. Inputs are synthetic and resident
 Scaling is weak: every rank owns its own B utterances (batch sharding, no data-path collective).
 
 Rank 0 prints ONE JSON line with the contract fields plus:
-  roofline     : the gradient kernel (dominant), algorithmic bytes (N_v + N) * V * 4 per launch divided by its
-                 average duration from HIP events recorded around each launch on its stream in the timed region
+  roofline     : the gradient kernel (dominant), algorithmic bytes (N_live + N) * V * 4 per launch (N_live = in-band
+                 rows whose fp32 gradient is not exactly zero, the rows it reads) divided by its average duration
+                 from HIP events recorded around each launch on its stream in the timed region; the SURVEY §8d
+                 formula (N_v + N) * V * 4 is reported beside it as formula_bytes_per_launch / formula_gbps
   cpu_baseline : the reference's own CpuRNNTComputer<float> (oracle/_ref) -- or the oracle port when the reference
                  build is absent -- timed on a bounded sample of the same workload on the host cores
   kernels      : per-kernel average ms and achieved GB/s
@@ -68,6 +70,8 @@ def main():
     ap.add_argument("--config", default="headline", choices=["headline", "c2", "ragged", "ragged64", "c5"])
     ap.add_argument("--cpu-sample", type=int, default=8, help="utterances in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
+                    help="launch knob for experiments (mrnnt_tune); the defaults are the tuned values")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI, the real path) or gloo (rehearsal: several ranks may share one GPU)")
     args = ap.parse_args()
@@ -92,6 +96,10 @@ def main():
     import _mrnnt_lib as L
 
     lib = L.load()
+    for kv in args.tune:
+        k, v = kv.split("=")
+        if L.tune(k, int(v)) < 0:
+            raise SystemExit(f"unknown knob {k}")
     T, S, V, workload = lengths_for(args.config, rank, world)
     B = len(T)
     rows = int(np.sum(T.astype(np.int64) * (S + 1)))
@@ -152,9 +160,13 @@ def main():
         dist.all_reduce(total_utts)
     total_utts = int(total_utts.item())
 
-    grad_bytes = (n_band + rows) * V * 4  # algorithmic: read in-band acts rows once, write every grads row once
+    # live rows: in-band rows whose gradient is not exactly zero in fp32 -- the only acts rows the gradient
+    # kernel reads (occupancy skip); counted once after the timed region
+    live = live_rows(op, L, acts, labels, T_t, S_t, dev)
+    grad_bytes = (live + rows) * V * 4  # algorithmic: read live acts rows once, write every grads row once
+    formula_grad_bytes = (n_band + rows) * V * 4  # SURVEY.md §8d formula: every in-band row read
     softmax_bytes = n_band * V * 4
-    step_bytes = (2 * n_band + rows) * V * 4
+    step_bytes = (n_band + live + rows) * V * 4
 
     def avg_ms(name):
         ms, n = prof[name]
@@ -170,7 +182,9 @@ def main():
     if os.path.exists(pmc_path):
         try:
             pm = json.load(open(pmc_path))
-            if pm.get("config") == args.config:
+            # only a measurement of this config and of the kernel this run launches counts
+            if pm.get("config") == args.config and pm.get("kernel", "").startswith(
+                    "grad_rows_kernel" if L.tune("grad_variant") == 3 else "grad_kernel<IoF32"):
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -202,7 +216,10 @@ def main():
                          "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4) if achieved else None,
                          "traffic": traffic, "algorithmic_bytes_per_launch": grad_bytes,
-                         "avg_launch_ms": round(g_ms, 4) if g_ms else None},
+                         "avg_launch_ms": round(g_ms, 4) if g_ms else None,
+                         "live_rows": live, "inband_rows": n_band,
+                         "formula_bytes_per_launch": formula_grad_bytes,
+                         "formula_gbps": round(formula_grad_bytes / (g_ms * 1e-3) / 1e9, 1) if g_ms else None},
             "kernels": {
                 "log_softmax": {"avg_ms": round(s_ms, 4) if s_ms else None,
                                 "gbps": round(softmax_bytes / (s_ms * 1e-3) / 1e9, 1) if s_ms else None},
@@ -210,11 +227,23 @@ def main():
                 "grad": {"avg_ms": round(g_ms, 4) if g_ms else None, "gbps": round(achieved, 1) if achieved else None},
             },
             "cpu_baseline": cpu,
+            "tune": args.tune or None,
+            "alloc": {"acts": acts.data_ptr(), "grads": acts.grad.data_ptr()},
             "loss_check": float(loss.item()),
         }
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def live_rows(op, L, acts, labels, T, S, dev):
+    """In-band rows the gradient kernel reads on this workload (mrnnt_grad_live_rows after one forward)."""
+    prep = op._Prepared(acts.detach(), labels, T, S, None, 0, 0)
+    _, ws = op._forward(prep, with_beta=True)
+    cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    L.check(L.load().mrnnt_grad_live_rows(ctypes.byref(prep.problem), ctypes.c_void_p(ws.data_ptr()),
+                                          ctypes.c_void_p(cnt.data_ptr()), prep.stream()), "grad_live_rows")
+    return int(cnt.item())
 
 
 def cpu_baseline(lib, L, acts, labels, T, S, V, n_sample, stream):

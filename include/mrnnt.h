@@ -89,6 +89,13 @@ RNNTStatus mrnnt_read_loglik(const mrnnt_problem *p, const void *workspace, doub
 /* Message describing the last non-success status returned on this thread. */
 const char *mrnnt_last_error(void);
 
+/* Number of in-band lattice rows whose acts the gradient kernel reads ("live" rows) for the problem of the
+ * last mrnnt_forward(with_beta=1) on this workspace, written to *count_dev (device uint64). A row whose
+ * occupancy exp(alpha(t-1,s) + beta(t,s) - ll) is below e^-110 has an exactly-zero fp32 gradient and is
+ * stored without reading acts ("occ_skip" knob, on by default). Inspection/bench only; asynchronous. */
+RNNTStatus mrnnt_grad_live_rows(const mrnnt_problem *p, const void *workspace, unsigned long long *count_dev,
+                                hipStream_t stream);
+
 int mrnnt_version(void);
 
 /* Kernel-time accounting over HIP events recorded around each launch on its stream.
@@ -102,7 +109,8 @@ int mrnnt_profile_read(double *total_ms, int64_t *launches, int n);
  * of the log-softmax kernel: 0 one, 2 two), "grad_variant" (0 one row per wave, 2 two rows, 3 row-stride
  * sweep for the packed layout), "softmax_grid_per_cu" / "grad_grid_per_cu" (persistent workgroups per
  * CU, 0 = one workgroup per lattice column; "grid_per_cu" sets both), "nt_store" / "nt_load" (0/1:
- * nontemporal grads stores / acts loads).
+ * nontemporal grads stores / acts loads), "occ_skip" (0/1: skip the acts read of rows
+ * whose gradient is exactly zero, see mrnnt_grad_live_rows).
  * Sets `key` to `value` (value < 0: query only) and returns the previous value, or -1 for an unknown key.
  * Process-global; not thread-safe against concurrent launches. */
 int mrnnt_tune(const char *key, int value);

@@ -133,6 +133,7 @@ DevProblem make_dev(const mrnnt_problem *p, const Plan &pl, const void *ws) {
     d.B = pl.B;
     d.V = pl.V;
     d.blank = p->blank;
+    d.occ_skip = tuning().occ_skip;
     d.num_cols = pl.cols;
     d.num_rows = pl.N;
     d.pad_T = pl.pad_T;
@@ -295,6 +296,18 @@ RNNTStatus mrnnt_read_loglik(const mrnnt_problem *p, const void *ws, double *ll_
     return RNNT_STATUS_SUCCESS;
 }
 
+RNNTStatus mrnnt_grad_live_rows(const mrnnt_problem *p, const void *ws, unsigned long long *count_dev,
+                                hipStream_t stream) {
+    Plan pl;
+    RNNTStatus st = make_plan(p, &pl);
+    if (st != RNNT_STATUS_SUCCESS) return st;
+    if ((st = check_pointers(p)) != RNNT_STATUS_SUCCESS) return st;
+    if (!ws || !count_dev) return fail(RNNT_STATUS_INVALID_VALUE, "workspace / count is null");
+    const hipError_t e = launch_count_live(make_dev(p, pl, ws), count_dev, stream);
+    if (e != hipSuccess) return fail_hip(e, "live-row count kernel");
+    return RNNT_STATUS_SUCCESS;
+}
+
 void mrnnt_profile_enable(int enable) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
     for (auto &r : g_prof) {
@@ -345,6 +358,7 @@ int mrnnt_tune(const char *key, int value) {
     }
     else if (!std::strcmp(key, "nt_store")) slot = &t.nt_store;
     else if (!std::strcmp(key, "nt_load")) slot = &t.nt_load;
+    else if (!std::strcmp(key, "occ_skip")) slot = &t.occ_skip;
     if (!slot) return -1;
     const int prev = *slot;
     if (value >= 0) *slot = value;

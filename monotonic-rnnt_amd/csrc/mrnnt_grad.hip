@@ -8,26 +8,38 @@
 // then one conversion to the output element type. Out-of-band lattice rows store 0 * grad_scale (the
 // reference's backward multiplies its zero rows by grad_output); padding rows of the padded layout
 // store 0 (launch_pad_zero).
+#include <algorithm>
+
 #include "mrnnt_device.h"
 
 namespace mrnnt {
 
 struct RowCoef {
-    float c2;  // (den + alpha(t-1,s) + beta(t,s) - ll) * log2(e)
-    float cb;  // blank correction
-    float ce;  // label correction
-    int lab;   // label(s) (-1 for s == S or label == blank)
+    float c2;   // (den + alpha(t-1,s) + beta(t,s) - ll) * log2(e)
+    float cb;   // blank correction
+    float ce;   // label correction
+    int lab;    // label(s) (-1 for s == S or label == blank)
+    bool live;  // false: the row's gradient is exactly 0 (kDeadLogOcc) and acts need not be read
 };
+
+// alpha(t-1, s) of an in-band row (alpha(-1, s) = [s == 0])
+__device__ __forceinline__ double alpha_prev(const DevProblem &p, int t, int s, int64_t row, int W) {
+    return (t == 0) ? (s == 0 ? 0.0 : NEG_INF_D) : p.alpha[row - W];
+}
+
+// The dead-row predicate (mrnnt_internal.h kDeadLogOcc); NaN state is live.
+__device__ __forceinline__ bool row_live(double log_occ) { return !(log_occ < kDeadLogOcc); }
 
 __device__ __forceinline__ RowCoef row_coef(const DevProblem &p, int t, int T, int S, int s, int64_t row, double ll,
                                             const int *__restrict__ lab_b) {
     const int W = S + 1;
-    const double am = (t == 0) ? (s == 0 ? 0.0 : NEG_INF_D) : p.alpha[row - W];
+    const double am = alpha_prev(p, t, s, row, W);
     const double b0 = p.beta[row];
     const double b1 = (t == T - 1) ? (s == S ? 0.0 : NEG_INF_D) : p.beta[row + W];
     const double b2 = (s == S) ? NEG_INF_D : ((t == T - 1) ? (s + 1 == S ? 0.0 : NEG_INF_D) : p.beta[row + W + 1]);
     const double base = am - ll;
     RowCoef rc;
+    rc.live = !p.occ_skip || row_live(base + b0);
     rc.c2 = (float)(((double)p.den[row] + base + b0) * kLog2eD);
     rc.cb = (float)exp(p.lpb[row] + base + b1);
     rc.ce = (s < S) ? (float)exp(p.lpe[row] + base + b2) : 0.0f;
@@ -91,8 +103,12 @@ __global__ __launch_bounds__(256) void grad_kernel(DevProblem p, const float *__
                 const int sr = s + r;
                 ok[r] = sr <= S;
                 inb[r] = ok[r] && sr >= lo && sr <= hi;
-                if (inb[r]) rc[r] = row_coef(p, t, T, S, sr, rowc + sr, ll, lab_b);
-                else rc[r] = RowCoef{0.0f, 0.0f, 0.0f, -1};
+                if (inb[r]) {
+                    rc[r] = row_coef(p, t, T, S, sr, rowc + sr, ll, lab_b);
+                    inb[r] = rc[r].live;  // dead rows are stored like out-of-band rows
+                } else {
+                    rc[r] = RowCoef{0.0f, 0.0f, 0.0f, -1, false};
+                }
             }
             for (int base = 0; base < VL; base += 64 * U) {
                 Vec x[R][U];
@@ -146,12 +162,13 @@ __global__ __launch_bounds__(256) void grad_rows_kernel(DevProblem p, const floa
         const bool inb = s <= t && (S - s) <= (T - t);
         const float sc = scale ? scale[b] : 1.0f;
         Vec *__restrict__ out = gv + row * (int64_t)VL;
-        if (!inb) {
+        RowCoef rc;
+        if (inb) rc = row_coef(p, t, T, S, s, row, p.ll[b], p.labels + (int64_t)b * p.label_stride);
+        if (!inb || !rc.live) {
             const Vec zv = splat<IO>(0.0f * sc);
             for (int j = lane; j < VL; j += 64) vstore<NTS>(out + j, zv);
             continue;
         }
-        const RowCoef rc = row_coef(p, t, T, S, s, row, p.ll[b], p.labels + (int64_t)b * p.label_stride);
         for (int base = 0; base < VL; base += 64 * U) {
             Vec x[U];
 #pragma unroll
@@ -196,11 +213,13 @@ __global__ __launch_bounds__(256) void grad_scalar_kernel(DevProblem p, const fl
         const int *__restrict__ lab_b = p.labels + (int64_t)b * p.label_stride;
         for (int s = wave; s <= S; s += 4) {
             Sc *__restrict__ g = gs + (arow + s) * (int64_t)V;
-            if (s < lo || s > hi) {
+            RowCoef rc;
+            const bool inb = s >= lo && s <= hi;
+            if (inb) rc = row_coef(p, t, T, S, s, rowc + s, ll, lab_b);
+            if (!inb || !rc.live) {
                 for (int v = lane; v < V; v += 64) g[v] = zs;
                 continue;
             }
-            const RowCoef rc = row_coef(p, t, T, S, s, rowc + s, ll, lab_b);
             const Sc *__restrict__ z = acts + (arow + s) * (int64_t)V;
             for (int v = lane; v < V; v += 64) {
                 float gv = fast_exp2(fmaf(IO::to_f(z[v]), kLog2e, rc.c2));
@@ -210,6 +229,42 @@ __global__ __launch_bounds__(256) void grad_scalar_kernel(DevProblem p, const fl
             }
         }
     }
+}
+
+// Number of in-band rows whose acts the gradient kernels read (live rows; all in-band rows with
+// occ_skip = 0). Not on the hot path: bench/inspection only (mrnnt_grad_live_rows).
+__global__ __launch_bounds__(256) void count_live_kernel(DevProblem p, unsigned long long *__restrict__ count) {
+    __shared__ unsigned long long part[4];
+    unsigned long long n = 0;
+    Cursor cur;
+    cur.init(p.col_off, p.B, blockIdx.x);
+    for (int64_t c = blockIdx.x; c < p.num_cols; c += gridDim.x) {
+        cur.advance(p.col_off, c);
+        const int b = cur.b;
+        const int T = p.T[b], S = p.S[b], W = S + 1;
+        const int t = (int)(c - p.col_off[b]);
+        const int64_t rowc = p.row_off[b] + (int64_t)t * W;
+        const int lo = max(0, t - (T - S));
+        const int hi = min(t, S);
+        const double ll = p.ll[b];
+        for (int s = lo + threadIdx.x; s <= hi; s += blockDim.x) {
+            const int64_t row = rowc + s;
+            n += (!p.occ_skip || row_live(alpha_prev(p, t, s, row, W) - ll + p.beta[row])) ? 1 : 0;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) n += __shfl_xor(n, off);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = n;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(count, part[0] + part[1] + part[2] + part[3]);
+}
+
+hipError_t launch_count_live(const DevProblem &p, unsigned long long *count, hipStream_t stream) {
+    const hipError_t e = hipMemsetAsync(count, 0, sizeof(*count), stream);
+    if (e != hipSuccess) return e;
+    const int64_t blocks = std::min<int64_t>(std::max<int64_t>(p.num_cols, 1), 2048);
+    count_live_kernel<<<(int)blocks, 256, 0, stream>>>(p, count);
+    return hipGetLastError();
 }
 
 // Padded layout: rows (b, t, s) with t >= T_b or s > S_b are not lattice rows; their gradient is 0.

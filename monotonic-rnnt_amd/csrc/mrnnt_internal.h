@@ -25,6 +25,7 @@ struct DevProblem {
     const int *min_s;           // [cols] alignment band (nullptr = unrestricted)
     const int *max_s;           // [cols]
     int B, V, blank;
+    int occ_skip;               // skip the acts read of rows whose gradient is exactly zero (mrnnt_grad.hip)
     int64_t num_cols;           // sum_b T_b
     int64_t num_rows;           // N = sum_b T_b (S_b + 1)
     int64_t pad_T, pad_S1;      // padded acts layout (pad_S1 == 0: packed)
@@ -45,6 +46,7 @@ struct Tuning {
     int grad_grid_per_cu = 32;    // same for the gradient kernel
     int nt_store = 1;             // nontemporal stores of grads
     int nt_load = 1;              // nontemporal loads of acts (both streaming kernels)
+    int occ_skip = 1;             // gradient: no acts read for rows with log-occupancy < kDeadLogOcc
 };
 Tuning &tuning();
 
@@ -57,8 +59,16 @@ hipError_t launch_align(const DevProblem &p, const int *alignment, int64_t align
 hipError_t launch_softmax(const DevProblem &p, int elem, int grid, hipStream_t stream);
 hipError_t launch_dp(const DevProblem &p, int S_max, int with_beta, float *costs, hipStream_t stream);
 hipError_t launch_grad(const DevProblem &p, int elem, const float *scale, void *grads, int grid, hipStream_t stream);
+hipError_t launch_count_live(const DevProblem &p, unsigned long long *count, hipStream_t stream);
 hipError_t launch_pad_zero(const DevProblem &p, int elem, void *grads, hipStream_t stream);
 hipError_t launch_synth(float *out, int64_t begin, int64_t count, uint64_t seed, int normal, hipStream_t stream);
+
+// A lattice row (t, s) with alpha(t-1, s) + beta(t, s) - ll < kDeadLogOcc has occupancy below e^-110 =
+// 2^-158.7: every element of its fp32 gradient, p_v * occupancy minus the blank / label corrections (each
+// bounded by the occupancy), is below half the smallest fp32 denormal (2^-150) and rounds to exactly 0 --
+// in this kernel and in the reference's fp32 arithmetic alike. Such rows are stored as 0 * grad_scale
+// without reading acts. (NaN state compares false and takes the full path.)
+constexpr double kDeadLogOcc = -110.0;
 
 // Largest S+1 the recursion instantiations cover (8 waves x 64 lanes x 4 cells per lane).
 constexpr int kMaxLabelsPlusOne = 2048;

@@ -82,6 +82,7 @@ def load() -> ctypes.CDLL:
             "mrnnt_backward": (i, [P, vp, vp, vp, vp]),
             "mrnnt_cost_and_grad": (i, [P, vp, sz, vp, vp, vp, vp]),
             "mrnnt_read_loglik": (i, [P, vp, vp, vp, vp]),
+            "mrnnt_grad_live_rows": (i, [P, vp, vp, vp]),
             "mrnnt_last_error": (ctypes.c_char_p, []),
             "mrnnt_version": (i, []),
             "mrnnt_profile_enable": (None, [i]),

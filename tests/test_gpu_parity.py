@@ -382,3 +382,57 @@ def test_reduced_precision_padded_and_aligned(op, dev):
     cr, gr = O.oracle_rnnt(up, labels, T, S, alignment=al, max_shift=2)
     assert_costs(costs.detach().cpu().numpy().astype(np.float64), cr)
     assert (np.abs(g - gr) - 2.0 ** -8 * np.abs(gr)).max() <= GRAD_TOL
+
+
+# ---------------------------------------------------------------------------------------------
+# occupancy skip: rows whose fp32 gradient is exactly zero are stored without reading acts
+
+def _live_rows(op, dev, acts, labels, T, S, alignment=None, k=0):
+    import ctypes
+    import _mrnnt_lib as L
+    a = torch.from_numpy(acts).to(dev)
+    al = None if alignment is None else torch.from_numpy(alignment).to(dev)
+    prep = op._Prepared(a, torch.from_numpy(labels), torch.from_numpy(T), torch.from_numpy(S), al, k, 0)
+    _, ws = op._forward(prep, with_beta=True)
+    cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    L.check(L.load().mrnnt_grad_live_rows(ctypes.byref(prep.problem), ctypes.c_void_p(ws.data_ptr()),
+                                          ctypes.c_void_p(cnt.data_ptr()), prep.stream()), "live_rows")
+    return int(cnt.item())
+
+
+@pytest.mark.parametrize("grad_variant", [0, 2, 3])
+def test_occupancy_skip_is_bit_identical(op, dev, grad_variant):
+    """With occ_skip the gradient kernel does not read acts rows whose occupancy is < e^-110; their fp32
+    gradient is exactly 0 either way, so grads must be bit-identical with the skip on and off (and match the
+    oracle), while the live-row count drops below the in-band row count on long utterances."""
+    import _mrnnt_lib as L
+    rng = np.random.default_rng(606)
+    T = np.array([400, 300, 37, 250], np.int32)
+    S = np.array([80, 120, 5, 0], np.int32)
+    V = 64
+    rows = int(np.sum(T * (S + 1)))
+    acts = (3.0 * rng.standard_normal((rows, V))).astype(np.float32)
+    labels = rng.integers(1, V, (4, int(S.max()))).astype(np.int32)
+    scale = np.array([1.0, -0.5, 2.0, 0.0], np.float32)
+    n_band = int(np.sum((S.astype(np.int64) + 1) * (T - S + 1) - 1))
+    saved_skip, saved_var = L.tune("occ_skip"), L.tune("grad_variant")
+    try:
+        L.tune("grad_variant", grad_variant)
+        out = {}
+        for skip in (0, 1):
+            L.tune("occ_skip", skip)
+            out[skip] = run_gpu(op, dev, acts, labels, T, S, scale=scale)
+            live = _live_rows(op, dev, acts, labels, T, S)
+            if skip:
+                assert live < 0.9 * n_band, (live, n_band)
+            else:
+                assert live == n_band
+        assert np.array_equal(out[0][0], out[1][0])
+        assert np.array_equal(out[0][1].view(np.uint32), out[1][1].view(np.uint32))  # signed zeros included
+        cr, gr = O.oracle_rnnt(acts, labels, T, S, num_threads=4)
+        gr = gr * np.repeat(scale.astype(np.float64), T * (S + 1))[:, None]
+        assert_costs(out[1][0], cr)
+        assert_grads(out[1][1], gr)
+    finally:
+        L.tune("occ_skip", saved_skip)
+        L.tune("grad_variant", saved_var)

@@ -34,7 +34,9 @@ def main():
     ap.add_argument("--config", default="headline")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--variants", default=None)
-    ap.add_argument("--separate-grads", action="store_true", help="allocate grads in its own torch allocation")
+    ap.add_argument("--rank", default="0/1", help="r/N: time rank r's slice of an N-way sharded config")
+    ap.add_argument("--ws-first", action="store_true",
+                    help="allocate the workspace before grads (the order the autograd surface produces)")
     args = ap.parse_args()
     variants = json.loads(args.variants) if args.variants else DEFAULT_VARIANTS
 
@@ -43,9 +45,10 @@ def main():
 
     lib = L.load()
     DEFAULTS = {k: L.tune(k) for k in ("softmax_variant", "grad_variant", "softmax_grid_per_cu", "grad_grid_per_cu",
-                                       "nt_store", "nt_load")}
+                                       "nt_store", "nt_load", "occ_skip")}
     dev = torch.device("cuda:0")
-    T, S, V, workload = lengths_for(args.config, 0, 1)
+    rk, wd = (int(x) for x in args.rank.split("/"))
+    T, S, V, workload = lengths_for(args.config, rk, wd)
     B = len(T)
     rows = int(np.sum(T.astype(np.int64) * (S + 1)))
     n_band = int(np.sum((S.astype(np.int64) + 1) * (T - S + 1) - 1))
@@ -53,8 +56,8 @@ def main():
     acts = torch.empty((rows, V), dtype=torch.float32, device=dev)
     L.check(lib.mrnnt_synth_acts(ctypes.c_void_p(acts.data_ptr()), 0, rows * V, 0, 1, stream), "synth")
     MAX_OFF_KB = 8192
-    grads_store = torch.empty(rows * V + MAX_OFF_KB * 256, dtype=torch.float32, device=dev)
-    grads_holder = {"t": grads_store[: rows * V].view(rows, V)}
+    if not args.ws_first:
+        grads_store = torch.empty(rows * V + MAX_OFF_KB * 256, dtype=torch.float32, device=dev)
     labels = torch.from_numpy(np.random.default_rng(1).integers(1, V, (B, int(S.max()))).astype(np.int32)).to(dev)
     T_dev = torch.from_numpy(T).to(dev)
     S_dev = torch.from_numpy(S).to(dev)
@@ -68,6 +71,10 @@ def main():
     n = ctypes.c_size_t(0)
     L.check(lib.mrnnt_workspace_size(ctypes.byref(p), ctypes.byref(n)), "ws")
     ws = torch.empty(n.value, dtype=torch.uint8, device=dev)
+    if args.ws_first:
+        grads_store = torch.empty(rows * V + MAX_OFF_KB * 256, dtype=torch.float32, device=dev)
+    grads_holder = {"t": grads_store[: rows * V].view(rows, V)}
+    out_alloc = {"acts": acts.data_ptr(), "grads": grads_store.data_ptr(), "ws": ws.data_ptr()}
 
     def run_once():
         L.check(lib.mrnnt_forward(ctypes.byref(p), ctypes.c_void_p(ws.data_ptr()), n.value,
@@ -101,7 +108,7 @@ def main():
                 continue  # warm-up round
             for k in times[i]:
                 times[i][k].append(prof[k][0])
-    out = {"workload": workload, "rows": rows, "inband_rows": n_band, "V": V, "variants": []}
+    out = {"alloc": out_alloc, "workload": workload, "rows": rows, "inband_rows": n_band, "V": V, "variants": []}
     gb = (n_band + rows) * V * 4 / 1e9
     sb = n_band * V * 4 / 1e9
     for v, t in zip(variants, times):
