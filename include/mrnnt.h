@@ -96,6 +96,49 @@ const char *mrnnt_last_error(void);
 RNNTStatus mrnnt_grad_live_rows(const mrnnt_problem *p, const void *workspace, unsigned long long *count_dev,
                                 hipStream_t stream);
 
+/* ---- fused joint network + loss (extension) -------------------------------------
+ * The logits are not an input: z(b,t,s,:) = weight * tanh(enc[b,t,:] + pred[b,s,:]) + bias is formed on the
+ * matrix cores inside the log-softmax and gradient passes and never stored (bf16 operands, fp32 accumulate).
+ * Labels, lengths, blank and costs have the meaning of mrnnt_problem. H must be 128, 256, 384, 512 or 640. */
+typedef struct mrnnt_joint_problem {
+    int B;
+    int V;
+    int H;
+    int blank;
+    const int *T_host;       /* host [B] */
+    const int *S_host;       /* host [B] */
+    const int *T_dev;        /* device [B] */
+    const int *S_dev;        /* device [B] */
+    const int *labels;       /* device [B, label_stride] */
+    int64_t label_stride;
+    const void *enc;         /* device bf16, row (b, t) at enc + b*enc_stride + t*H (elements) */
+    int64_t enc_stride;      /* multiple of 8, >= max_b T_b * H */
+    const void *pred;        /* device bf16, row (b, s) at pred + b*pred_stride + s*H */
+    int64_t pred_stride;     /* multiple of 8, >= (max_b S_b + 1) * H */
+    const void *weight;      /* device bf16 [V, H] */
+    const float *bias;       /* device fp32 [V] or NULL */
+} mrnnt_joint_problem;
+
+RNNTStatus mrnnt_joint_workspace_size(const mrnnt_joint_problem *p, size_t *bytes);
+
+/* Forward: costs_dev[b] = -log P(labels_b | enc_b, pred_b); with_beta as in mrnnt_forward. */
+RNNTStatus mrnnt_joint_forward(const mrnnt_joint_problem *p, void *workspace, size_t workspace_bytes,
+                               float *costs_dev, int with_beta, hipStream_t stream);
+
+/* After mrnnt_joint_forward(with_beta=1): list the live lattice rows (those with a non-zero fp32 logit
+ * gradient) in the workspace and write their number to *count_dev (device uint64). */
+RNNTStatus mrnnt_joint_live_rows(const mrnnt_joint_problem *p, void *workspace, unsigned long long *count_dev,
+                                 hipStream_t stream);
+
+/* After mrnnt_joint_live_rows: for live row i (n_live = the count it produced, read back by the caller),
+ * G[i, :] = grad_scale[b] * dcost_b/dz (bf16 [n_live, V]), Hact[i, :] = tanh(enc + pred) (bf16 [n_live, H]),
+ * bt_idx[i] = b*(enc_stride/H) + t and bs_idx[i] = b*(pred_stride/H) + s (int64). Then
+ * dweight = G^T Hact, dbias = sum_i G[i], and with dpre = (G weight) * (1 - Hact^2):
+ * denc[bt_idx[i]] += dpre[i], dpred[bs_idx[i]] += dpre[i]. grad_scale may be NULL (= 1). */
+RNNTStatus mrnnt_joint_backward(const mrnnt_joint_problem *p, void *workspace, int64_t n_live,
+                                const float *grad_scale, void *G, void *Hact, int64_t *bt_idx, int64_t *bs_idx,
+                                hipStream_t stream);
+
 int mrnnt_version(void);
 
 /* Kernel-time accounting over HIP events recorded around each launch on its stream.

@@ -308,6 +308,182 @@ RNNTStatus mrnnt_grad_live_rows(const mrnnt_problem *p, const void *ws, unsigned
     return RNNT_STATUS_SUCCESS;
 }
 
+// ---- fused joint network + loss ------------------------------------------------------------------
+
+}  // extern "C"
+
+namespace {
+
+struct JointPlan {
+    Plan base;
+    int64_t n_inband = 0;
+    size_t off_cnt = 0, off_lcol = 0, off_ls = 0, off_total = 0, total = 0;
+};
+
+mrnnt_problem base_problem(const mrnnt_joint_problem *jp) {
+    mrnnt_problem p;
+    std::memset(&p, 0, sizeof(p));
+    p.B = jp->B;
+    p.V = jp->V;
+    p.blank = jp->blank;
+    p.T_host = jp->T_host;
+    p.S_host = jp->S_host;
+    p.T_dev = jp->T_dev;
+    p.S_dev = jp->S_dev;
+    p.acts = jp->enc;  // the lattice kernels never read acts on this path
+    p.labels = jp->labels;
+    p.label_stride = jp->label_stride;
+    p.num_rows = -1;
+    return p;
+}
+
+bool aligned16(const void *ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; }
+
+RNNTStatus make_joint_plan(const mrnnt_joint_problem *jp, JointPlan *jl) {
+    if (!jp) return fail(RNNT_STATUS_INVALID_VALUE, "null joint problem");
+    const mrnnt_problem p = base_problem(jp);
+    JointPlan q;
+    RNNTStatus st = make_plan(&p, &q.base);
+    if (st != RNNT_STATUS_SUCCESS) return st;
+    const int H = jp->H;
+    if (H != 128 && H != 256 && H != 384 && H != 512 && H != 640)
+        return fail(RNNT_STATUS_INVALID_VALUE, "joint H must be 128, 256, 384, 512 or 640 (got " + std::to_string(H) + ")");
+    if (jp->enc_stride % 8 || jp->pred_stride % 8)
+        return fail(RNNT_STATUS_INVALID_VALUE, "enc/pred utterance strides must be multiples of 8 elements");
+    if (jp->enc_stride < (int64_t)q.base.T_max * H || jp->pred_stride < (int64_t)(q.base.S_max + 1) * H)
+        return fail(RNNT_STATUS_INVALID_VALUE, "enc/pred utterance strides smaller than max T * H / (max S + 1) * H");
+    for (int b = 0; b < jp->B; ++b) {
+        const int T = jp->T_host[b], S = jp->S_host[b];
+        for (int t = 0; t < T; ++t) q.n_inband += std::min(t, S) - std::max(0, t - (T - S)) + 1;
+    }
+    size_t o = q.base.total;
+    auto take = [&](size_t bytes) {
+        const size_t at = o;
+        o = align_up(o + bytes);
+        return at;
+    };
+    q.off_cnt = take(sizeof(int64_t) * (q.base.cols + 1));
+    q.off_lcol = take(sizeof(int) * std::max<int64_t>(1, q.n_inband));
+    q.off_ls = take(sizeof(int) * std::max<int64_t>(1, q.n_inband));
+    q.off_total = take(sizeof(unsigned long long));
+    q.total = o;
+    *jl = q;
+    return RNNT_STATUS_SUCCESS;
+}
+
+RNNTStatus check_joint_pointers(const mrnnt_joint_problem *jp) {
+    if (!jp->enc || !jp->pred || !jp->weight) return fail(RNNT_STATUS_INVALID_VALUE, "enc / pred / weight is null");
+    if (!aligned16(jp->enc) || !aligned16(jp->pred) || !aligned16(jp->weight))
+        return fail(RNNT_STATUS_INVALID_VALUE, "enc / pred / weight must be 16-byte aligned");
+    if (!jp->T_dev || !jp->S_dev) return fail(RNNT_STATUS_INVALID_VALUE, "device lengths are required");
+    if (!jp->labels) return fail(RNNT_STATUS_INVALID_VALUE, "labels is null");
+    return RNNT_STATUS_SUCCESS;
+}
+
+JointArgs joint_args(const mrnnt_joint_problem *jp, const JointPlan &jl, void *ws, int64_t n) {
+    char *w = static_cast<char *>(ws);
+    JointArgs j;
+    std::memset(&j, 0, sizeof(j));
+    j.enc = static_cast<const unsigned short *>(jp->enc);
+    j.enc_sb = jp->enc_stride;
+    j.pred = static_cast<const unsigned short *>(jp->pred);
+    j.pred_sb = jp->pred_stride;
+    j.W = static_cast<const unsigned short *>(jp->weight);
+    j.bias = jp->bias;
+    j.H = jp->H;
+    j.lcol = reinterpret_cast<const int *>(w + jl.off_lcol);
+    j.ls = reinterpret_cast<const int *>(w + jl.off_ls);
+    j.n = n;
+    return j;
+}
+
+}  // namespace
+
+extern "C" {
+
+RNNTStatus mrnnt_joint_workspace_size(const mrnnt_joint_problem *jp, size_t *bytes) {
+    if (!bytes) return fail(RNNT_STATUS_INVALID_VALUE, "null size pointer");
+    JointPlan jl;
+    const RNNTStatus st = make_joint_plan(jp, &jl);
+    if (st != RNNT_STATUS_SUCCESS) return st;
+    *bytes = jl.total;
+    return RNNT_STATUS_SUCCESS;
+}
+
+RNNTStatus mrnnt_joint_forward(const mrnnt_joint_problem *jp, void *ws, size_t ws_bytes, float *costs_dev,
+                               int with_beta, hipStream_t stream) {
+    JointPlan jl;
+    RNNTStatus st = make_joint_plan(jp, &jl);
+    if (st != RNNT_STATUS_SUCCESS) return st;
+    if ((st = check_joint_pointers(jp)) != RNNT_STATUS_SUCCESS) return st;
+    if (!ws || ws_bytes < jl.total)
+        return fail(RNNT_STATUS_INVALID_VALUE, "workspace too small: need " + std::to_string(jl.total) + " bytes");
+    const Plan &pl = jl.base;
+    const mrnnt_problem p = base_problem(jp);
+    DevProblem d = make_dev(&p, pl, ws);
+    char *w = static_cast<char *>(ws);
+    hipError_t e = timed(K_SETUP, stream, [&] {
+        return launch_setup(jp->T_dev, jp->S_dev, pl.B, reinterpret_cast<int64_t *>(w + pl.off_row),
+                            reinterpret_cast<int64_t *>(w + pl.off_col), stream);
+    });
+    if (e != hipSuccess) return fail_hip(e, "setup kernel");
+    // out-of-band lp entries must be finite for the recursion (the acts path zero-fills them in its pass)
+    if ((e = launch_zero(w + pl.off_lpb, pl.off_alpha - pl.off_lpb, stream)) != hipSuccess)
+        return fail_hip(e, "lp zero fill");
+    e = launch_row_list(d, 0, reinterpret_cast<int64_t *>(w + jl.off_cnt), reinterpret_cast<int *>(w + jl.off_lcol),
+                        reinterpret_cast<int *>(w + jl.off_ls), reinterpret_cast<unsigned long long *>(w + jl.off_total),
+                        stream);
+    if (e != hipSuccess) return fail_hip(e, "row list kernels");
+    const JointArgs j = joint_args(jp, jl, ws, jl.n_inband);
+    e = timed(K_JOINT_FWD, stream, [&] { return launch_joint_forward(d, j, stream); });
+    if (e != hipSuccess) return fail_hip(e, "joint log-softmax kernel");
+    e = timed(K_DP, stream, [&] { return launch_dp(d, pl.S_max, with_beta ? 1 : 0, costs_dev, stream); });
+    if (e != hipSuccess) return fail_hip(e, "alpha/beta kernel");
+    return RNNT_STATUS_SUCCESS;
+}
+
+RNNTStatus mrnnt_joint_live_rows(const mrnnt_joint_problem *jp, void *ws, unsigned long long *count_dev,
+                                 hipStream_t stream) {
+    JointPlan jl;
+    RNNTStatus st = make_joint_plan(jp, &jl);
+    if (st != RNNT_STATUS_SUCCESS) return st;
+    if (!ws || !count_dev) return fail(RNNT_STATUS_INVALID_VALUE, "workspace / count is null");
+    const mrnnt_problem p = base_problem(jp);
+    DevProblem d = make_dev(&p, jl.base, ws);
+    char *w = static_cast<char *>(ws);
+    hipError_t e = launch_row_list(d, 1, reinterpret_cast<int64_t *>(w + jl.off_cnt),
+                                   reinterpret_cast<int *>(w + jl.off_lcol), reinterpret_cast<int *>(w + jl.off_ls),
+                                   count_dev, stream);
+    if (e != hipSuccess) return fail_hip(e, "live row list kernels");
+    return RNNT_STATUS_SUCCESS;
+}
+
+RNNTStatus mrnnt_joint_backward(const mrnnt_joint_problem *jp, void *ws, int64_t n_live, const float *grad_scale,
+                                void *G, void *Hact, int64_t *bt_idx, int64_t *bs_idx, hipStream_t stream) {
+    JointPlan jl;
+    RNNTStatus st = make_joint_plan(jp, &jl);
+    if (st != RNNT_STATUS_SUCCESS) return st;
+    if ((st = check_joint_pointers(jp)) != RNNT_STATUS_SUCCESS) return st;
+    if (!ws) return fail(RNNT_STATUS_INVALID_VALUE, "workspace is null");
+    if (n_live < 0 || n_live > jl.n_inband)
+        return fail(RNNT_STATUS_INVALID_VALUE, "n_live outside [0, in-band rows]");
+    if (n_live > 0 && (!G || !Hact || !bt_idx || !bs_idx))
+        return fail(RNNT_STATUS_INVALID_VALUE, "G / Hact / bt_idx / bs_idx is null");
+    if (n_live > 0 && (!aligned16(G) || !aligned16(Hact)))
+        return fail(RNNT_STATUS_INVALID_VALUE, "G / Hact must be 16-byte aligned");
+    const mrnnt_problem p = base_problem(jp);
+    DevProblem d = make_dev(&p, jl.base, ws);
+    JointArgs j = joint_args(jp, jl, ws, n_live);
+    j.G = static_cast<unsigned short *>(G);
+    j.Hact = static_cast<unsigned short *>(Hact);
+    j.bt_idx = bt_idx;
+    j.bs_idx = bs_idx;
+    j.scale = grad_scale;
+    const hipError_t e = timed(K_JOINT_BWD, stream, [&] { return launch_joint_backward(d, j, stream); });
+    if (e != hipSuccess) return fail_hip(e, "joint gradient kernel");
+    return RNNT_STATUS_SUCCESS;
+}
+
 void mrnnt_profile_enable(int enable) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
     for (auto &r : g_prof) {

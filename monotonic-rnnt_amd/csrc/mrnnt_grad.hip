@@ -14,40 +14,6 @@
 
 namespace mrnnt {
 
-struct RowCoef {
-    float c2;   // (den + alpha(t-1,s) + beta(t,s) - ll) * log2(e)
-    float cb;   // blank correction
-    float ce;   // label correction
-    int lab;    // label(s) (-1 for s == S or label == blank)
-    bool live;  // false: the row's gradient is exactly 0 (kDeadLogOcc) and acts need not be read
-};
-
-// alpha(t-1, s) of an in-band row (alpha(-1, s) = [s == 0])
-__device__ __forceinline__ double alpha_prev(const DevProblem &p, int t, int s, int64_t row, int W) {
-    return (t == 0) ? (s == 0 ? 0.0 : NEG_INF_D) : p.alpha[row - W];
-}
-
-// The dead-row predicate (mrnnt_internal.h kDeadLogOcc); NaN state is live.
-__device__ __forceinline__ bool row_live(double log_occ) { return !(log_occ < kDeadLogOcc); }
-
-__device__ __forceinline__ RowCoef row_coef(const DevProblem &p, int t, int T, int S, int s, int64_t row, double ll,
-                                            const int *__restrict__ lab_b) {
-    const int W = S + 1;
-    const double am = alpha_prev(p, t, s, row, W);
-    const double b0 = p.beta[row];
-    const double b1 = (t == T - 1) ? (s == S ? 0.0 : NEG_INF_D) : p.beta[row + W];
-    const double b2 = (s == S) ? NEG_INF_D : ((t == T - 1) ? (s + 1 == S ? 0.0 : NEG_INF_D) : p.beta[row + W + 1]);
-    const double base = am - ll;
-    RowCoef rc;
-    rc.live = !p.occ_skip || row_live(base + b0);
-    rc.c2 = (float)(((double)p.den[row] + base + b0) * kLog2eD);
-    rc.cb = (float)exp(p.lpb[row] + base + b1);
-    rc.ce = (s < S) ? (float)exp(p.lpe[row] + base + b2) : 0.0f;
-    const int lab = (s < S) ? lab_b[s] : -1;
-    rc.lab = (lab == p.blank) ? -1 : lab;
-    return rc;
-}
-
 template <class IO>
 __device__ __forceinline__ typename IO::V grad_vec(const typename IO::V &xv, const RowCoef &rc, int j, int blank,
                                                    float sc) {

@@ -38,6 +38,34 @@ struct DevProblem {
     double *llb;                // [B]  beta(0, 0)
 };
 
+// Fused joint network (mrnnt_joint.hip): logits z(b,t,s,:) = W * tanh(enc[b,t,:] + pred[b,s,:]) + bias are
+// formed on MFMA inside the log-softmax and gradient passes and never stored. Operands are bf16 bit patterns.
+struct JointArgs {
+    const unsigned short *enc;   // [B, *, H]: row (b, t) at enc + b*enc_sb + t*H
+    int64_t enc_sb;
+    const unsigned short *pred;  // [B, *, H]: row (b, s) at pred + b*pred_sb + s*H
+    int64_t pred_sb;
+    const unsigned short *W;     // [V, H] (torch Linear weight layout)
+    const float *bias;           // [V] or nullptr
+    int H;
+    const int *lcol;             // row list: lattice column and label position of entry i
+    const int *ls;
+    int64_t n;                   // entries in the list
+    // backward outputs, one row per list entry
+    unsigned short *G;           // [n, V] bf16 dL/dz
+    unsigned short *Hact;        // [n, H] bf16 tanh(enc + pred)
+    int64_t *bt_idx;             // [n] b * enc_sb / H + t   (row of enc viewed as [B * T_slots, H])
+    int64_t *bs_idx;             // [n] b * pred_sb / H + s  (row of pred viewed as [B * S_slots, H])
+    const float *scale;          // [B] upstream dL/dcost or nullptr
+};
+
+// Row lists over the lattice: mode 0 = every in-band row, mode 1 = live rows (needs alpha/beta/ll).
+hipError_t launch_row_list(const DevProblem &p, int mode, int64_t *col_cnt, int *lcol, int *ls,
+                           unsigned long long *total, hipStream_t stream);
+hipError_t launch_joint_forward(const DevProblem &p, const JointArgs &j, hipStream_t stream);
+hipError_t launch_joint_backward(const DevProblem &p, const JointArgs &j, hipStream_t stream);
+hipError_t launch_zero(void *ptr, size_t bytes, hipStream_t stream);
+
 // Launch-shape knobs (experiment hook: mrnnt_tune in mrnnt_capi.cpp). Defaults are the tuned values.
 struct Tuning {
     int softmax_variant = 2;      // rows per wave of the log-softmax kernel: 0 -> 1 row, 2 -> 2 rows (large V)
@@ -51,7 +79,8 @@ struct Tuning {
 Tuning &tuning();
 
 // Kernel-family ids for the profiling counters (mrnnt_profile_read order).
-enum KernelId { K_BAND = 0, K_SOFTMAX = 1, K_DP = 2, K_GRAD = 3, K_SETUP = 4, K_COUNT = 5 };
+enum KernelId { K_BAND = 0, K_SOFTMAX = 1, K_DP = 2, K_GRAD = 3, K_SETUP = 4, K_JOINT_FWD = 5, K_JOINT_BWD = 6,
+                K_COUNT = 7 };
 
 hipError_t launch_setup(const int *T, const int *S, int B, int64_t *row_off, int64_t *col_off, hipStream_t stream);
 hipError_t launch_align(const DevProblem &p, const int *alignment, int64_t align_stride, int align_blank,

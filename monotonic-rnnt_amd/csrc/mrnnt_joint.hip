@@ -1,0 +1,403 @@
+// mrnnt_joint.hip -- the joint network fused into the loss ("fusing the joint network's
+// final projection with the softmax pass so the N x V tensor is never materialised").
+//
+//   z(b,t,s,:) = W * tanh(enc[b,t,:] + pred[b,s,:]) + bias          (W: [V, H] bf16, fp32 accumulate)
+//
+// The packed logits the reference's loss takes as `acts` (monotonic_rnnt_op.py:133-140) are formed on MFMA
+// (v_mfma_f32_32x32x16_bf16) tile by tile inside two passes and never written to HBM:
+//   forward  : per in-band lattice row the log-softmax denominator and the blank / label log-probs (what
+//              mrnnt_softmax.hip computes from stored acts), then the unchanged alpha/beta recursion;
+//   backward : per LIVE row (the occupancy-skip predicate of mrnnt_grad.hip) the logit gradient
+//              g = dL/dz (bf16) and the joint activation tanh(enc + pred) (bf16), so that dW = G^T Hact,
+//              dH = G W and dbias = sum G are plain GEMMs / reductions over live rows only.
+//
+// Tiling: a workgroup of 4 waves owns 128 consecutive rows of a row list; a wave owns 32 rows and keeps their
+// activations as the MFMA B operand in registers (lane l: row l&31, k = 16 ks + 8 (l>>5) + [0,8)), built
+// once from enc/pred with a fast tanh. W streams through LDS in 32-vocabulary chunks (double-buffered,
+// padded rows against bank conflicts) shared by the 4 waves; each chunk is one 32x32 output tile per wave,
+// D[vocab][row] = sum_k W[vocab][k] h[row][k]: the accumulator holds 16 vocabulary entries of ONE row per
+// lane (vocab = (i&3) + 8 (i>>2) + 4 (l>>5)), so the per-row online softmax is register-local and the two
+// lane halves merge once at the end.
+#include "mrnnt_device.h"
+
+namespace mrnnt {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float bf16_lo(unsigned u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float bf16_hi(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
+
+// tanh(x) = sign(x) (1 - e) / (1 + e), e = exp(-2|x|): v_exp_f32 + v_rcp_f32, |error| ~ 1e-7
+__device__ __forceinline__ float fast_tanh(float x) {
+    const float e = fast_exp2(-2.0f * kLog2e * fabsf(x));
+    return copysignf((1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e), x);
+}
+
+// x[c] for a runtime c, as a sum of selects (a select chain gets rewritten into a scratch-indexed load)
+template <int N>
+__device__ __forceinline__ float pick_n(const float (&x)[N], int c) {
+    float r = 0.0f;
+#pragma unroll
+    for (int i = 0; i < N; ++i) r += (c == i) ? x[i] : 0.0f;
+    return r;
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// row lists: entries (column, s) in column order, s ascending; mode 0 = in-band rows, 1 = live rows
+
+__device__ __forceinline__ bool list_pred(const DevProblem &p, int mode, int t, int s, int64_t row, int W,
+                                          double ll) {
+    if (mode == 0 || !p.occ_skip) return true;
+    return row_live(alpha_prev(p, t, s, row, W) - ll + p.beta[row]);
+}
+
+template <bool WRITE>
+__global__ __launch_bounds__(256) void row_list_kernel(DevProblem p, int mode, int64_t *__restrict__ cnt,
+                                                       int *__restrict__ lcol, int *__restrict__ ls) {
+    const int lane = threadIdx.x & 63;
+    const int64_t col = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (col >= p.num_cols) return;
+    Cursor cur;
+    cur.init(p.col_off, p.B, col);
+    const int b = cur.b;
+    const int T = p.T[b], S = p.S[b], W = S + 1;
+    const int t = (int)(col - p.col_off[b]);
+    const int64_t rowc = p.row_off[b] + (int64_t)t * W;
+    const int lo = max(0, t - (T - S));
+    const int hi = min(t, S);
+    const double ll = mode ? p.ll[b] : 0.0;
+    int64_t base = WRITE ? cnt[col] : 0;
+    int n = 0;
+    for (int s0 = lo; s0 <= hi; s0 += 64) {
+        const int s = s0 + lane;
+        const bool ok = s <= hi && list_pred(p, mode, t, s, rowc + s, W, ll);
+        const unsigned long long mask = __ballot(ok);
+        if (WRITE && ok) {
+            const int rank = __popcll(mask & ((1ull << lane) - 1ull));
+            lcol[base + rank] = (int)col;
+            ls[base + rank] = s;
+        }
+        base += __popcll(mask);
+        n += __popcll(mask);
+    }
+    if (!WRITE && lane == 0) cnt[col] = n;
+}
+
+// exclusive scan of a[0..n) in place, a[n] = total (one workgroup; n = lattice columns)
+__global__ __launch_bounds__(1024) void scan_kernel(int64_t *__restrict__ a, int64_t n,
+                                                    unsigned long long *__restrict__ total) {
+    __shared__ int64_t part[1024];
+    const int tid = threadIdx.x;
+    const int64_t seg = (n + 1023) / 1024;
+    const int64_t lo = min(n, tid * seg), hi = min(n, lo + seg);
+    int64_t loc = 0;
+    for (int64_t i = lo; i < hi; ++i) loc += a[i];
+    part[tid] = loc;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
+        const int64_t v = tid >= off ? part[tid - off] : 0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    int64_t run = part[tid] - loc;
+    for (int64_t i = lo; i < hi; ++i) {
+        const int64_t v = a[i];
+        a[i] = run;
+        run += v;
+    }
+    if (tid == 1023) {
+        a[n] = part[1023];
+        if (total) *total = (unsigned long long)part[1023];
+    }
+}
+
+hipError_t launch_row_list(const DevProblem &p, int mode, int64_t *col_cnt, int *lcol, int *ls,
+                           unsigned long long *total, hipStream_t stream) {
+    const int64_t blocks = (p.num_cols + 3) / 4;
+    row_list_kernel<false><<<(int)blocks, 256, 0, stream>>>(p, mode, col_cnt, lcol, ls);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    scan_kernel<<<1, 1024, 0, stream>>>(col_cnt, p.num_cols, total);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    row_list_kernel<true><<<(int)blocks, 256, 0, stream>>>(p, mode, col_cnt, lcol, ls);
+    return hipGetLastError();
+}
+
+hipError_t launch_zero(void *ptr, size_t bytes, hipStream_t stream) { return hipMemsetAsync(ptr, 0, bytes, stream); }
+
+// ---------------------------------------------------------------------------------------------------------
+// the fused tile
+
+struct RowPos {
+    bool valid;
+    int b, t, s, T, S, lab;
+    int64_t row;  // packed lattice row
+};
+
+__device__ __forceinline__ RowPos row_pos(const DevProblem &p, const JointArgs &j, int64_t i) {
+    RowPos q{false, 0, 0, 0, 1, 0, -1, 0};
+    if (i >= j.n) return q;
+    const int col = j.lcol[i];
+    q.s = j.ls[i];
+    Cursor c;
+    c.init(p.col_off, p.B, col);
+    q.b = c.b;
+    q.t = (int)(col - p.col_off[q.b]);
+    q.T = p.T[q.b];
+    q.S = p.S[q.b];
+    q.row = p.row_off[q.b] + (int64_t)q.t * (q.S + 1) + q.s;
+    q.lab = q.s < q.S ? p.labels[(int64_t)q.b * p.label_stride + q.s] : -1;
+    q.valid = true;
+    return q;
+}
+
+// B operand: h = bf16(tanh(enc[b,t] + pred[b,s])) for k = 16 ks + 8 half + [0, 8); optionally stored to Hact.
+template <int KS, bool STORE>
+__device__ __forceinline__ void build_act(const JointArgs &j, const RowPos &q, int half, int64_t i,
+                                          bf16x8 (&bfr)[KS]) {
+    constexpr int H = 16 * KS;
+    const unsigned short *er = j.enc + (int64_t)q.b * j.enc_sb + (int64_t)q.t * H + 8 * half;
+    const unsigned short *pr = j.pred + (int64_t)q.b * j.pred_sb + (int64_t)q.s * H + 8 * half;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+        bf16x8 h;
+        if (q.valid) {
+            const u4 ev = *reinterpret_cast<const u4 *>(er + 16 * ks);
+            const u4 pv = *reinterpret_cast<const u4 *>(pr + 16 * ks);
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                h[2 * w] = (__bf16)fast_tanh(bf16_lo(ev[w]) + bf16_lo(pv[w]));
+                h[2 * w + 1] = (__bf16)fast_tanh(bf16_hi(ev[w]) + bf16_hi(pv[w]));
+            }
+            if (STORE) *reinterpret_cast<bf16x8 *>(j.Hact + i * H + 16 * ks + 8 * half) = h;
+        } else {
+#pragma unroll
+            for (int w = 0; w < 8; ++w) h[w] = (__bf16)0.0f;
+        }
+        bfr[ks] = h;
+    }
+}
+
+// W chunk staging: 32 vocabulary rows x H bf16 into a padded LDS image (row stride H + 8 elements)
+template <int KS>
+struct WStage {
+    static constexpr int H = 16 * KS;
+    static constexpr int LDW = H + 8;
+    static constexpr int PPT = H / 64;  // 16-byte pieces per thread (32 rows * H / 8 pieces / 256 threads)
+    u4 reg[PPT];
+    float breg;
+    __device__ __forceinline__ void load(const JointArgs &j, int V, int c) {
+#pragma unroll
+        for (int m = 0; m < PPT; ++m) {
+            const int q = threadIdx.x + 256 * m;
+            const int rw = q / (H / 8), c8 = q % (H / 8);
+            const int v = 32 * c + rw;
+            reg[m] = v < V ? *reinterpret_cast<const u4 *>(j.W + (int64_t)v * H + 8 * c8) : (u4){0u, 0u, 0u, 0u};
+        }
+        if (threadIdx.x < 32) {
+            const int v = 32 * c + threadIdx.x;
+            breg = v < V ? (j.bias ? j.bias[v] : 0.0f) : 0.0f;
+        }
+    }
+    __device__ __forceinline__ void store(unsigned short *wsh, float *bsh) const {
+#pragma unroll
+        for (int m = 0; m < PPT; ++m) {
+            const int q = threadIdx.x + 256 * m;
+            const int rw = q / (H / 8), c8 = q % (H / 8);
+            *reinterpret_cast<u4 *>(wsh + rw * LDW + 8 * c8) = reg[m];
+        }
+        if (threadIdx.x < 32) bsh[threadIdx.x] = breg;
+    }
+};
+
+template <int KS>
+__device__ __forceinline__ f32x16 tile_mma(const unsigned short *wsh, const bf16x8 (&bfr)[KS], int lane) {
+    constexpr int LDW = 16 * KS + 8;
+    const unsigned short *wrow = wsh + (lane & 31) * LDW + 8 * (lane >> 5);
+    f32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8 *>(wrow + 16 * ks);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bfr[ks], acc, 0, 0, 0);
+    }
+    return acc;
+}
+
+// index of the accumulator register holding vocabulary offset jj (0..31) of a chunk, or -1 if the other lane
+// half holds it
+__device__ __forceinline__ int acc_reg_of(int jj, int half) {
+    return (((jj >> 2) & 1) == half) ? ((jj & 3) + 4 * (jj >> 3)) : -1;
+}
+
+template <int KS>
+__global__ __launch_bounds__(256) void joint_fwd_kernel(DevProblem p, JointArgs j) {
+    constexpr int LDW = WStage<KS>::LDW;
+    __shared__ __attribute__((aligned(16))) unsigned short wsh[2][32 * LDW];
+    __shared__ float bsh[2][32];
+    const int lane = threadIdx.x & 63, half = lane >> 5;
+    const int64_t i = (int64_t)blockIdx.x * 128 + (threadIdx.x >> 6) * 32 + (lane & 31);
+    const RowPos q = row_pos(p, j, i);
+    bf16x8 bfr[KS];
+    build_act<KS, false>(j, q, half, i, bfr);
+
+    const int V = p.V, blank = p.blank;
+    const int nch = (V + 31) / 32;
+    WStage<KS> st;
+    st.load(j, V, 0);
+    st.store(wsh[0], bsh[0]);
+    __syncthreads();
+
+    float m = NEG_INF_F, sum = 0.0f, zb = 0.0f, ze = 0.0f;
+    bool fb = false, fe = false;
+    for (int c = 0; c < nch; ++c) {
+        const int buf = c & 1;
+        if (c + 1 < nch) st.load(j, V, c + 1);
+        const f32x16 acc = tile_mma<KS>(wsh[buf], bfr, lane);
+        float z[16];
+        float cm = NEG_INF_F;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int jj = (r & 3) + 8 * (r >> 2) + 4 * half;
+            z[r] = (32 * c + jj < V) ? acc[r] + bsh[buf][jj] : NEG_INF_F;
+            cm = fmaxf(cm, z[r]);
+        }
+        const float mn = fmaxf(m, cm);
+        const float mr = (mn == NEG_INF_F) ? 0.0f : mn;
+        float a = sum * fast_exp2((m - mr) * kLog2e);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) a += fast_exp2((z[r] - mr) * kLog2e);
+        sum = a;
+        m = mn;
+        const int jb = blank - 32 * c;
+        if (jb >= 0 && jb < 32) {
+            const int rb = acc_reg_of(jb, half);
+            if (rb >= 0) {
+                zb = pick_n<16>(z, rb);
+                fb = true;
+            }
+        }
+        const int jl = q.lab - 32 * c;
+        if (q.lab >= 0 && jl >= 0 && jl < 32) {
+            const int rl = acc_reg_of(jl, half);
+            if (rl >= 0) {
+                ze = pick_n<16>(z, rl);
+                fe = true;
+            }
+        }
+        if (c + 1 < nch) st.store(wsh[buf ^ 1], bsh[buf ^ 1]);
+        __syncthreads();
+    }
+    // merge the two lane halves (same row, disjoint vocabulary)
+    const float m2 = __shfl_xor(m, 32), s2 = __shfl_xor(sum, 32);
+    const float zb2 = __shfl_xor(zb, 32), ze2 = __shfl_xor(ze, 32);
+    const int fb2 = __shfl_xor((int)fb, 32), fe2 = __shfl_xor((int)fe, 32);
+    const float mn = fmaxf(m, m2);
+    const float mr = (mn == NEG_INF_F) ? 0.0f : mn;
+    sum = sum * fast_exp2((m - mr) * kLog2e) + s2 * fast_exp2((m2 - mr) * kLog2e);
+    if (!fb && fb2) zb = zb2;
+    if (!fe && fe2) ze = ze2;
+    if (q.valid && half == 0) {
+        const double den = -(double)mn - log((double)sum);
+        p.den[q.row] = (float)den;
+        p.lpb[q.row] = (double)zb + den;
+        p.lpe[q.row] = (q.lab >= 0 ? (double)ze : 0.0) + den;
+    }
+}
+
+template <int KS>
+__global__ __launch_bounds__(256) void joint_bwd_kernel(DevProblem p, JointArgs j) {
+    constexpr int LDW = WStage<KS>::LDW;
+    __shared__ __attribute__((aligned(16))) unsigned short wsh[2][32 * LDW];
+    __shared__ float bsh[2][32];
+    const int lane = threadIdx.x & 63, half = lane >> 5;
+    const int64_t i = (int64_t)blockIdx.x * 128 + (threadIdx.x >> 6) * 32 + (lane & 31);
+    const RowPos q = row_pos(p, j, i);
+    RowCoef rc{0.0f, 0.0f, 0.0f, -1, false};
+    float sc = 0.0f;
+    if (q.valid) {
+        rc = row_coef(p, q.t, q.T, q.S, q.s, q.row, p.ll[q.b], p.labels + (int64_t)q.b * p.label_stride);
+        sc = j.scale ? j.scale[q.b] : 1.0f;
+        if (half == 0) {
+            j.bt_idx[i] = (int64_t)q.b * (j.enc_sb / j.H) + q.t;
+            j.bs_idx[i] = (int64_t)q.b * (j.pred_sb / j.H) + q.s;
+        }
+    }
+    bf16x8 bfr[KS];
+    build_act<KS, true>(j, q, half, i, bfr);
+
+    const int V = p.V, blank = p.blank;
+    const int nch = (V + 31) / 32;
+    const bool vec_out = (V & 3) == 0;
+    unsigned short *grow = j.G + i * V;
+    WStage<KS> st;
+    st.load(j, V, 0);
+    st.store(wsh[0], bsh[0]);
+    __syncthreads();
+    for (int c = 0; c < nch; ++c) {
+        const int buf = c & 1;
+        if (c + 1 < nch) st.load(j, V, c + 1);
+        const f32x16 acc = tile_mma<KS>(wsh[buf], bfr, lane);
+        float g[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int jj = (r & 3) + 8 * (r >> 2) + 4 * half;
+            const int v = 32 * c + jj;
+            float x = fast_exp2(fmaf(acc[r] + bsh[buf][jj], kLog2e, rc.c2));
+            x -= (v == blank ? rc.cb : 0.0f) + (v == rc.lab ? rc.ce : 0.0f);
+            g[r] = x * sc;
+        }
+        if (q.valid) {
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd) {
+                const int v0 = 32 * c + 8 * qd + 4 * half;
+                if (vec_out && v0 + 3 < V) {
+                    const unsigned lo = IoBF16::pack2(g[4 * qd], g[4 * qd + 1]);
+                    const unsigned hi = IoBF16::pack2(g[4 * qd + 2], g[4 * qd + 3]);
+                    *reinterpret_cast<uint2 *>(grow + v0) = make_uint2(lo, hi);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (v0 + e < V) grow[v0 + e] = IoBF16::from_f(g[4 * qd + e]);
+                }
+            }
+        }
+        if (c + 1 < nch) st.store(wsh[buf ^ 1], bsh[buf ^ 1]);
+        __syncthreads();
+    }
+}
+
+template <int KS>
+static void launch_kh(const DevProblem &p, const JointArgs &j, bool bwd, hipStream_t stream) {
+    const int64_t blocks = (j.n + 127) / 128;
+    if (bwd)
+        joint_bwd_kernel<KS><<<(int)blocks, 256, 0, stream>>>(p, j);
+    else
+        joint_fwd_kernel<KS><<<(int)blocks, 256, 0, stream>>>(p, j);
+}
+
+static hipError_t launch_joint(const DevProblem &p, const JointArgs &j, bool bwd, hipStream_t stream) {
+    if (j.n <= 0) return hipSuccess;
+    switch (j.H) {
+        case 128: launch_kh<8>(p, j, bwd, stream); break;
+        case 256: launch_kh<16>(p, j, bwd, stream); break;
+        case 384: launch_kh<24>(p, j, bwd, stream); break;
+        case 512: launch_kh<32>(p, j, bwd, stream); break;
+        case 640: launch_kh<40>(p, j, bwd, stream); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_joint_forward(const DevProblem &p, const JointArgs &j, hipStream_t stream) {
+    return launch_joint(p, j, false, stream);
+}
+
+hipError_t launch_joint_backward(const DevProblem &p, const JointArgs &j, hipStream_t stream) {
+    return launch_joint(p, j, true, stream);
+}
+
+}  // namespace mrnnt

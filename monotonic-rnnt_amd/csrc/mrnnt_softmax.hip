@@ -30,8 +30,8 @@ __device__ __forceinline__ void write_row(const DevProblem &p, int64_t row, floa
 
 // Vector path: V % E == 0, 16-byte aligned rows. U = vector loads per lane per chunk (a chunk covers
 // 64*U*E elements), R = rows a wave reduces at once (U*R vector loads in flight per lane).
-template <class IO, int U, int R, bool NTL>
-__global__ __launch_bounds__(256) void softmax_kernel(DevProblem p) {
+template <class IO, int U, int R, bool NTL, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void softmax_kernel(DevProblem p) {
     constexpr int E = IO::E;
     typedef typename IO::V Vec;
     const int lane = threadIdx.x & 63;
@@ -56,7 +56,7 @@ __global__ __launch_bounds__(256) void softmax_kernel(DevProblem p) {
         const int *__restrict__ lab_b = p.labels + (int64_t)b * p.label_stride;
         zero_fill_outside_band(p, rowc, S, lo, hi);
 
-        for (int s = lo + wave * R; s <= hi; s += 4 * R) {
+        for (int s = lo + wave * R; s <= hi; s += NW * R) {
             float m[R], sum[R], zb[R], ze[R];
             int lab[R];
             bool ok[R];
@@ -173,14 +173,22 @@ __global__ __launch_bounds__(256) void softmax_scalar_kernel(DevProblem p) {
 template <class IO, bool NTL>
 static void launch_vec(const DevProblem &p, int grid, hipStream_t stream) {
     const int VL = p.V / IO::E;
-    if (VL >= 192 && tuning().softmax_variant == 2)
-        softmax_kernel<IO, 4, 2, NTL><<<grid, 256, 0, stream>>>(p);
-    else if (VL >= 192)
-        softmax_kernel<IO, 4, 1, NTL><<<grid, 256, 0, stream>>>(p);
-    else if (VL >= 96)
+    const int v = tuning().softmax_variant;
+    if (VL >= 192) {
+        switch (v) {  // rows per wave (R) and waves per workgroup for a row of >= 192 vectors
+            case 0: softmax_kernel<IO, 4, 1, NTL><<<grid, 256, 0, stream>>>(p); break;
+            case 3: softmax_kernel<IO, 4, 3, NTL><<<grid, 256, 0, stream>>>(p); break;
+            case 4: softmax_kernel<IO, 4, 4, NTL><<<grid, 256, 0, stream>>>(p); break;
+            case 5: softmax_kernel<IO, 4, 2, NTL, 8><<<grid, 512, 0, stream>>>(p); break;
+            case 6: softmax_kernel<IO, 4, 1, NTL, 8><<<grid, 512, 0, stream>>>(p); break;
+            case 7: softmax_kernel<IO, 2, 4, NTL><<<grid, 256, 0, stream>>>(p); break;
+            default: softmax_kernel<IO, 4, 2, NTL><<<grid, 256, 0, stream>>>(p); break;
+        }
+    } else if (VL >= 96) {
         softmax_kernel<IO, 2, 2, NTL><<<grid, 256, 0, stream>>>(p);
-    else
+    } else {
         softmax_kernel<IO, 1, 4, NTL><<<grid, 256, 0, stream>>>(p);
+    }
 }
 
 template <class IO>

@@ -26,7 +26,7 @@ MRNNT_BF16 = 1
 MRNNT_F16 = 2
 
 # kernel-family order of mrnnt_profile_read
-KERNELS = ("band", "log_softmax", "alpha_beta", "grad", "setup")
+KERNELS = ("band", "log_softmax", "alpha_beta", "grad", "setup", "joint_fwd", "joint_bwd")
 
 
 class MrnntProblem(ctypes.Structure):
@@ -53,6 +53,27 @@ class MrnntProblem(ctypes.Structure):
     ]
 
 
+class MrnntJointProblem(ctypes.Structure):
+    _fields_ = [
+        ("B", ctypes.c_int),
+        ("V", ctypes.c_int),
+        ("H", ctypes.c_int),
+        ("blank", ctypes.c_int),
+        ("T_host", ctypes.c_void_p),
+        ("S_host", ctypes.c_void_p),
+        ("T_dev", ctypes.c_void_p),
+        ("S_dev", ctypes.c_void_p),
+        ("labels", ctypes.c_void_p),
+        ("label_stride", ctypes.c_int64),
+        ("enc", ctypes.c_void_p),
+        ("enc_stride", ctypes.c_int64),
+        ("pred", ctypes.c_void_p),
+        ("pred_stride", ctypes.c_int64),
+        ("weight", ctypes.c_void_p),
+        ("bias", ctypes.c_void_p),
+    ]
+
+
 class MrnntError(RuntimeError):
     def __init__(self, status: int, where: str, message: str):
         self.status = status
@@ -75,6 +96,7 @@ def load() -> ctypes.CDLL:
                               "(run `python __graft_entry__.py` or `make -C monotonic-rnnt_amd`)")
         lib = ctypes.CDLL(LIB_PATH)
         P = ctypes.POINTER(MrnntProblem)
+        JP = ctypes.POINTER(MrnntJointProblem)
         vp, i, i64, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_size_t
         sig = {
             "mrnnt_workspace_size": (i, [P, ctypes.POINTER(sz)]),
@@ -83,6 +105,10 @@ def load() -> ctypes.CDLL:
             "mrnnt_cost_and_grad": (i, [P, vp, sz, vp, vp, vp, vp]),
             "mrnnt_read_loglik": (i, [P, vp, vp, vp, vp]),
             "mrnnt_grad_live_rows": (i, [P, vp, vp, vp]),
+            "mrnnt_joint_workspace_size": (i, [JP, ctypes.POINTER(sz)]),
+            "mrnnt_joint_forward": (i, [JP, vp, sz, vp, i, vp]),
+            "mrnnt_joint_live_rows": (i, [JP, vp, vp, vp]),
+            "mrnnt_joint_backward": (i, [JP, vp, i64, vp, vp, vp, vp, vp, vp]),
             "mrnnt_last_error": (ctypes.c_char_p, []),
             "mrnnt_version": (i, []),
             "mrnnt_profile_enable": (None, [i]),

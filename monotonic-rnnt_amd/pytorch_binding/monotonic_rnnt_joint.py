@@ -1,0 +1,168 @@
+"""Fused joint network + monotonic RNN-T loss (extension).
+
+    costs = monotonic_rnnt_joint_loss(enc, pred, weight, bias, labels, input_lengths, label_lengths, blank_label=0)
+
+computes the loss of `monotonic_rnnt_loss(acts, ...)` for the packed logits
+
+    acts[(b, t, s), :] = weight @ tanh(enc[b, t] + pred[b, s]) + bias      (t < T_b, s <= S_b)
+
+without materialising them: the HIP kernels of `mrnnt_joint.hip` form each tile of logits on the matrix cores
+(bf16 operands, fp32 accumulation) inside the log-softmax pass and again, for the live lattice rows only,
+inside the gradient pass. Backward returns gradients for enc, pred, weight and bias: the fused kernel writes
+the logit gradient G and the activations tanh(enc + pred) of the live rows (bf16), and dweight = G^T Hact,
+dbias = sum G, dpre = (G weight) (1 - Hact^2) and its scatter into enc / pred rows are plain library GEMMs and
+reductions (hipBLASLt through torch) over those rows.
+
+Shapes: enc [B, T_slots >= max T, H], pred [B, S_slots >= max S + 1, H], weight [V, H] (torch.nn.Linear
+layout), bias [V] or None; H in {128, 256, 384, 512, 640}. Inputs of other floating dtypes are cast to bf16
+(the cast is differentiable, so their gradients come back in their own dtype). Costs are fp32 on the device.
+There is no CPU or eager fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import numpy as np
+import torch
+
+try:
+    from . import _mrnnt_lib as _L
+except ImportError:
+    import _mrnnt_lib as _L
+
+_L.load()
+
+JOINT_H = (128, 256, 384, 512, 640)
+
+
+def _vp(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+class _JointPrepared:
+    def __init__(self, enc, pred, weight, bias, labels, input_lengths, label_lengths, blank_label):
+        for name, x in (("enc", enc), ("pred", pred), ("weight", weight)):
+            if not x.is_cuda:
+                raise RuntimeError(f"monotonic_rnnt_joint: {name} must be a GPU tensor (no CPU implementation)")
+            if x.dtype != torch.bfloat16:
+                raise RuntimeError(f"monotonic_rnnt_joint: {name} must be bfloat16 here")
+        if enc.dim() != 3 or pred.dim() != 3 or weight.dim() != 2:
+            raise RuntimeError("monotonic_rnnt_joint: expected enc [B, T, H], pred [B, S+1, H], weight [V, H]")
+        B, _, H = enc.shape
+        V = weight.size(0)
+        if pred.size(0) != B or pred.size(2) != H or weight.size(1) != H:
+            raise RuntimeError(f"monotonic_rnnt_joint: shape mismatch enc {tuple(enc.shape)}, "
+                               f"pred {tuple(pred.shape)}, weight {tuple(weight.shape)}")
+        if H not in JOINT_H:
+            raise RuntimeError(f"monotonic_rnnt_joint: H = {H} not supported (one of {JOINT_H})")
+        dev = enc.device
+        self.enc = enc.contiguous()
+        self.pred = pred.contiguous()
+        self.weight = weight.contiguous()
+        self.bias = None if bias is None else bias.detach().to(dev, torch.float32).contiguous()
+        self.T_host = np.ascontiguousarray(input_lengths.detach().to("cpu", torch.int32).numpy()).reshape(-1)
+        self.S_host = np.ascontiguousarray(label_lengths.detach().to("cpu", torch.int32).numpy()).reshape(-1)
+        if self.T_host.size != B or self.S_host.size != B:
+            raise RuntimeError(f"monotonic_rnnt_joint: expected {B} input/label lengths")
+        if B and (self.T_host.max() > enc.size(1) or self.S_host.max() + 1 > pred.size(1)):
+            raise RuntimeError("monotonic_rnnt_joint: enc/pred have fewer frames/label positions than the lengths")
+        self.T_dev = input_lengths.detach().to(dev, torch.int32).contiguous()
+        self.S_dev = label_lengths.detach().to(dev, torch.int32).contiguous()
+        lab = labels.detach().to(dev, torch.int32)
+        if lab.dim() == 1:
+            lab = lab.view(B, -1)
+        self.labels = lab.contiguous() if lab.numel() else torch.zeros(B, 1, dtype=torch.int32, device=dev)
+        p = _L.MrnntJointProblem()
+        p.B, p.V, p.H, p.blank = B, V, H, int(blank_label)
+        p.T_host, p.S_host = self.T_host.ctypes.data, self.S_host.ctypes.data
+        p.T_dev, p.S_dev = self.T_dev.data_ptr(), self.S_dev.data_ptr()
+        p.labels, p.label_stride = self.labels.data_ptr(), self.labels.size(1)
+        p.enc, p.enc_stride = self.enc.data_ptr(), self.enc.size(1) * H
+        p.pred, p.pred_stride = self.pred.data_ptr(), self.pred.size(1) * H
+        p.weight = self.weight.data_ptr()
+        p.bias = self.bias.data_ptr() if self.bias is not None else None
+        self.problem = p
+        self.device = dev
+        self.B, self.V, self.H = B, V, H
+
+    def stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def forward(self, with_beta: bool):
+        lib = _L.load()
+        n = ctypes.c_size_t(0)
+        _L.check(lib.mrnnt_joint_workspace_size(ctypes.byref(self.problem), ctypes.byref(n)), "joint_workspace_size")
+        with torch.cuda.device(self.device):
+            ws = torch.empty(max(1, n.value), dtype=torch.uint8, device=self.device)
+            costs = torch.empty(self.B, dtype=torch.float32, device=self.device)
+            _L.check(lib.mrnnt_joint_forward(ctypes.byref(self.problem), _vp(ws), ws.numel(), _vp(costs),
+                                             1 if with_beta else 0, self.stream()), "mrnnt_joint_forward")
+        return costs, ws
+
+    def backward_rows(self, ws, grad_scale):
+        """The fused gradient pass: (G [n, V], Hact [n, H], bt_idx [n], bs_idx [n]) over the live rows."""
+        lib = _L.load()
+        with torch.cuda.device(self.device):
+            cnt = torch.zeros(1, dtype=torch.int64, device=self.device)
+            _L.check(lib.mrnnt_joint_live_rows(ctypes.byref(self.problem), _vp(ws), _vp(cnt), self.stream()),
+                     "mrnnt_joint_live_rows")
+            n = int(cnt.item())  # one 8-byte read-back sizes the row buffers
+            G = torch.empty(max(1, n), self.V, dtype=torch.bfloat16, device=self.device)
+            Hact = torch.empty(max(1, n), self.H, dtype=torch.bfloat16, device=self.device)
+            bt = torch.empty(max(1, n), dtype=torch.int64, device=self.device)
+            bs = torch.empty(max(1, n), dtype=torch.int64, device=self.device)
+            if grad_scale is not None:
+                grad_scale = grad_scale.detach().to(self.device, torch.float32).contiguous()
+            _L.check(lib.mrnnt_joint_backward(ctypes.byref(self.problem), _vp(ws), n, _vp(grad_scale), _vp(G),
+                                              _vp(Hact), _vp(bt), _vp(bs), self.stream()), "mrnnt_joint_backward")
+        return G[:n], Hact[:n], bt[:n], bs[:n]
+
+
+class MonotonicRNNTJointFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, enc, pred, weight, bias, labels, input_lengths, label_lengths, blank_label=0):
+        prep = _JointPrepared(enc, pred, weight, bias, labels, input_lengths, label_lengths, blank_label)
+        need = any(ctx.needs_input_grad[:4])
+        costs, ws = prep.forward(with_beta=need)
+        if need:
+            ctx.save_for_backward(enc, pred, weight)
+            ctx.prep, ctx.ws = prep, ws
+            ctx.bias_dtype = None if bias is None else bias.dtype
+        return costs
+
+    @staticmethod
+    def backward(ctx, grad_costs):
+        prep, ws = ctx.prep, ctx.ws
+        G, Hact, bt, bs = prep.backward_rows(ws, grad_costs)
+        ctx.prep = ctx.ws = None
+        B, H = prep.B, prep.H
+        d_enc = d_pred = d_w = d_b = None
+        if ctx.needs_input_grad[2]:
+            d_w = (G.t() @ Hact).to(prep.weight.dtype)  # [V, H]
+        if ctx.bias_dtype is not None and ctx.needs_input_grad[3]:
+            d_b = G.sum(0, dtype=torch.float32).to(ctx.bias_dtype)
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+            hf = Hact.float()
+            dpre = (G @ prep.weight).float() * (1.0 - hf * hf)  # [n, H]
+            if ctx.needs_input_grad[0]:
+                d_enc = torch.zeros(B * prep.enc.size(1), H, dtype=torch.float32, device=G.device)
+                d_enc.index_add_(0, bt, dpre)
+                d_enc = d_enc.view(B, prep.enc.size(1), H).to(prep.enc.dtype)
+            if ctx.needs_input_grad[1]:
+                d_pred = torch.zeros(B * prep.pred.size(1), H, dtype=torch.float32, device=G.device)
+                d_pred.index_add_(0, bs, dpre)
+                d_pred = d_pred.view(B, prep.pred.size(1), H).to(prep.pred.dtype)
+        return d_enc, d_pred, d_w, d_b, None, None, None, None
+
+
+def monotonic_rnnt_joint_loss(enc: torch.Tensor, pred: torch.Tensor, weight: torch.Tensor,
+                              bias: Optional[torch.Tensor], labels: torch.Tensor, input_lengths: torch.Tensor,
+                              label_lengths: torch.Tensor, blank_label: int = 0) -> torch.Tensor:
+    """Monotonic RNN-T loss of the joint network tanh(enc + pred) @ weight.T + bias, fused (see module doc)."""
+    cast = lambda x: x if x is None or x.dtype == torch.bfloat16 else x.to(torch.bfloat16)  # noqa: E731
+    return MonotonicRNNTJointFunction.apply(cast(enc), cast(pred), cast(weight), bias, labels, input_lengths,
+                                            label_lengths, blank_label)
+
+
+__all__ = ["MonotonicRNNTJointFunction", "monotonic_rnnt_joint_loss"]

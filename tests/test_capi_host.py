@@ -120,13 +120,16 @@ def test_torch_op_rejects_cpu_tensors():
         op.monotonic_rnnt_cpp.cpu_monotonic_rnnt(acts, None, None, None, None, None, 0, 0)
 
 
-def test_ctypes_problem_struct_matches_c_layout():
-    """The ctypes mirror of mrnnt_problem has the C header's size and field offsets (checked with gcc)."""
+@pytest.mark.parametrize("cname,pyname", [("mrnnt_problem", "MrnntProblem"),
+                                          ("mrnnt_joint_problem", "MrnntJointProblem")])
+def test_ctypes_problem_struct_matches_c_layout(cname, pyname):
+    """The ctypes mirrors of the ABI structs have the C header's size and field offsets (checked with gcc)."""
     import _mrnnt_lib as L
-    fields = [f for f, _ in L.MrnntProblem._fields_]
-    body = "".join(f'printf("%zu\\n", offsetof(mrnnt_problem, {f}));' for f in fields)
+    cls = getattr(L, pyname)
+    fields = [f for f, _ in cls._fields_]
+    body = "".join(f'printf("%zu\\n", offsetof({cname}, {f}));' for f in fields)
     src = ('#include <stddef.h>\n#include <stdio.h>\n#include "mrnnt.h"\n'
-           f'int main(void){{ printf("%zu\\n", sizeof(mrnnt_problem)); {body} return 0; }}\n')
+           f'int main(void){{ printf("%zu\\n", sizeof({cname})); {body} return 0; }}\n')
     import tempfile
     with tempfile.TemporaryDirectory() as d:
         exe = os.path.join(d, "layout")
@@ -134,8 +137,8 @@ def test_ctypes_problem_struct_matches_c_layout():
                            capture_output=True, text=True)
         assert r.returncode == 0, r.stderr
         vals = [int(x) for x in subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()]
-    assert vals[0] == ctypes.sizeof(L.MrnntProblem)
-    assert vals[1:] == [getattr(L.MrnntProblem, f).offset for f in fields]
+    assert vals[0] == ctypes.sizeof(cls)
+    assert vals[1:] == [getattr(cls, f).offset for f in fields]
 
 
 def test_padded_layout_and_dtype_validation(lib):
@@ -156,3 +159,25 @@ def test_padded_layout_and_dtype_validation(lib):
         p.acts_dtype = dt
         st = lib.mrnnt_workspace_size(ctypes.byref(p), ctypes.byref(n))
         assert (st == L.RNNT_STATUS_SUCCESS) == ok, dt
+
+
+def test_joint_workspace_size_and_validation(lib):
+    import _mrnnt_lib as L
+    T = np.array([4, 7], np.int32)
+    S = np.array([2, 5], np.int32)
+    p = L.MrnntJointProblem()
+    p.B, p.V, p.H, p.blank = 2, 64, 256, 0
+    p.T_host, p.S_host = T.ctypes.data, S.ctypes.data
+    p.enc_stride, p.pred_stride = 7 * 256, 6 * 256
+    n = ctypes.c_size_t(0)
+    assert lib.mrnnt_joint_workspace_size(ctypes.byref(p), ctypes.byref(n)) == L.RNNT_STATUS_SUCCESS
+    assert n.value >= (4 * 3 + 7 * 6) * (4 + 4 * 8)
+    p.H = 200  # unsupported hidden size
+    assert lib.mrnnt_joint_workspace_size(ctypes.byref(p), ctypes.byref(n)) == L.RNNT_STATUS_INVALID_VALUE
+    assert b"joint H" in lib.mrnnt_last_error()
+    p.H, p.pred_stride = 256, 5 * 256  # fewer label positions than max S + 1
+    assert lib.mrnnt_joint_workspace_size(ctypes.byref(p), ctypes.byref(n)) == L.RNNT_STATUS_INVALID_VALUE
+    p.pred_stride = 6 * 256 + 4  # not a multiple of 8
+    assert lib.mrnnt_joint_workspace_size(ctypes.byref(p), ctypes.byref(n)) == L.RNNT_STATUS_INVALID_VALUE
+    p.pred_stride = 6 * 256
+    assert lib.mrnnt_joint_forward(ctypes.byref(p), None, 0, None, 1, None) == L.RNNT_STATUS_INVALID_VALUE

@@ -1,0 +1,148 @@
+"""Parity of the fused joint network + loss (monotonic_rnnt_joint.py / mrnnt_joint.hip) against a host reference.
+
+Reference = the composition the fused op replaces, evaluated on the host in fp64 from the same bf16 inputs:
+  h    = bf16(tanh(enc + pred))                  (fp32 tanh, round-to-nearest-even to bf16, like the kernel)
+  acts = h @ weight.T + bias  (fp64, then fp32)  -> the oracle (cpu_rnnt.h<double> restatement) for costs, dacts
+  dweight = dacts^T h, dbias = sum dacts, dpre = (dacts weight) (1 - h^2), denc/dpred = dpre summed over s / t.
+
+Tolerances (floating-point extension on bf16 matrix cores, stated here):
+  costs : |dc| <= 1e-5 * max(1, |c|)   (fp32 accumulation of exact bf16 products; the kernel's fast tanh can land on
+                                         the other side of a bf16 rounding boundary than the host's for rare elements)
+  grads : max |dg| <= 1.5e-2 * max |g_ref| + 1e-5 per tensor (the logit gradient is stored as bf16, 2^-9 relative,
+                                         and dH = G weight runs as a bf16 GEMM)
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def jop():
+    import monotonic_rnnt_joint
+    return monotonic_rnnt_joint
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available()
+    return torch.device("cuda:0")
+
+
+def make_case(seed, B, Trange, Smax, H, V, scale_in=1.0):
+    rng = np.random.default_rng(seed)
+    T = rng.integers(Trange[0], Trange[1] + 1, B).astype(np.int32)
+    S = np.array([rng.integers(0, min(t, Smax) + 1) for t in T], np.int32)
+    Tm, Sm = int(T.max()), int(S.max())
+    enc = torch.from_numpy(scale_in * rng.standard_normal((B, Tm + 1, H)).astype(np.float32)).to(torch.bfloat16)
+    pred = torch.from_numpy(scale_in * rng.standard_normal((B, Sm + 2, H)).astype(np.float32)).to(torch.bfloat16)
+    w = torch.from_numpy((rng.standard_normal((V, H)) / np.sqrt(H) * 2.0).astype(np.float32)).to(torch.bfloat16)
+    bias = torch.from_numpy(0.1 * rng.standard_normal(V).astype(np.float32))
+    labels = rng.integers(1, V, (B, max(1, Sm))).astype(np.int32)
+    return enc, pred, w, bias, labels, T, S
+
+
+def host_reference(enc, pred, w, bias, labels, T, S, blank=0, scale=None):
+    B = len(T)
+    W64 = w.double()
+    hs, rows = [], []
+    for b in range(B):
+        e = enc[b, : T[b]].float()
+        p = pred[b, : S[b] + 1].float()
+        h = torch.tanh(e[:, None, :] + p[None, :, :]).to(torch.bfloat16).double()  # [T, S+1, H]
+        hs.append(h)
+        rows.append((h @ W64.T + bias.double()).reshape(-1, w.shape[0]))
+    acts = torch.cat(rows).float().numpy()
+    costs, dz = O.oracle_rnnt(acts, labels, T, S, blank=blank, num_threads=4)
+    if scale is not None:
+        dz = dz * np.repeat(np.asarray(scale, np.float64), T * (S + 1))[:, None]
+    dz = torch.from_numpy(dz)
+    d_enc = torch.zeros(enc.shape, dtype=torch.float64)
+    d_pred = torch.zeros(pred.shape, dtype=torch.float64)
+    d_w = torch.zeros(w.shape, dtype=torch.float64)
+    r = 0
+    for b in range(B):
+        n = int(T[b]) * (int(S[b]) + 1)
+        g = dz[r:r + n]
+        h = hs[b].reshape(n, -1)
+        d_w += g.T @ h
+        dpre = ((g @ W64) * (1 - h * h)).reshape(T[b], S[b] + 1, -1)
+        d_enc[b, : T[b]] = dpre.sum(1)
+        d_pred[b, : S[b] + 1] = dpre.sum(0)
+        r += n
+    return costs, d_enc, d_pred, d_w, dz.sum(0)
+
+
+def close(x, ref, rel=1.5e-2, name=""):
+    x = x.double().cpu()
+    ref = ref.double()
+    err = (x - ref).abs().max().item()
+    lim = rel * ref.abs().max().item() + 1e-5
+    assert err <= lim, (name, err, lim)
+
+
+def run_joint(jop, dev, enc, pred, w, bias, labels, T, S, blank=0, scale=None):
+    e = enc.to(dev).requires_grad_(True)
+    p = pred.to(dev).requires_grad_(True)
+    ww = w.to(dev).requires_grad_(True)
+    bb = bias.to(dev).requires_grad_(True)
+    costs = jop.monotonic_rnnt_joint_loss(e, p, ww, bb, torch.from_numpy(labels).to(dev), torch.from_numpy(T),
+                                          torch.from_numpy(S), blank)
+    sc = torch.ones(len(T), device=dev) if scale is None else torch.tensor(scale, dtype=torch.float32, device=dev)
+    (costs * sc).sum().backward()
+    torch.cuda.synchronize()
+    return costs.detach().cpu().double().numpy(), e.grad, p.grad, ww.grad, bb.grad
+
+
+@pytest.mark.parametrize("H,V", [(128, 64), (256, 100), (256, 1000), (512, 256), (384, 96), (640, 130)])
+def test_joint_loss_and_grads_vs_host(jop, dev, H, V):
+    enc, pred, w, bias, labels, T, S = make_case(H + V, 3, (1, 24), 8, H, V)
+    scale = [1.0, -0.5, 2.0]
+    c, de, dp, dw, db = run_joint(jop, dev, enc, pred, w, bias, labels, T, S, scale=scale)
+    cr, de_r, dp_r, dw_r, db_r = host_reference(enc, pred, w, bias, labels, T, S, scale=scale)
+    assert np.all(np.abs(c - cr) <= 1e-5 * np.maximum(1.0, np.abs(cr))), (c, cr)
+    close(de, de_r, name="d_enc")
+    close(dp, dp_r, name="d_pred")
+    close(dw, dw_r, name="d_weight")
+    close(db, db_r, name="d_bias")
+    # padding frames / label slots beyond the lengths get exactly zero gradient
+    for b in range(len(T)):
+        assert torch.all(de[b, T[b]:] == 0) and torch.all(dp[b, S[b] + 1:] == 0)
+
+
+def test_joint_blank_last_and_long_utterance(jop, dev):
+    """blank = V-1, an utterance long enough that the occupancy skip removes rows from the backward pass."""
+    H, V = 256, 64
+    enc, pred, w, bias, labels, T, S = make_case(7, 2, (150, 200), 40, H, V, scale_in=2.0)
+    labels = np.where(labels == V - 1, 1, labels).astype(np.int32)
+    c, de, dp, dw, db = run_joint(jop, dev, enc, pred, w, bias, labels, T, S, blank=V - 1)
+    cr, de_r, dp_r, dw_r, db_r = host_reference(enc, pred, w, bias, labels, T, S, blank=V - 1)
+    assert np.all(np.abs(c - cr) <= 1e-5 * np.maximum(1.0, np.abs(cr))), (c, cr)
+    close(de, de_r, name="d_enc")
+    close(dp, dp_r, name="d_pred")
+    close(dw, dw_r, name="d_weight")
+    close(db, db_r, name="d_bias")
+
+
+def test_joint_matches_materialised_acts_path(jop, dev):
+    """The fused op equals monotonic_rnnt_loss on the logits it never materialises (costs; same bf16 h up to
+    rare tanh rounding flips), cost-only forward included."""
+    import monotonic_rnnt_op as op
+    H, V = 256, 256
+    enc, pred, w, bias, labels, T, S = make_case(11, 4, (5, 40), 12, H, V)
+    c_fused = jop.monotonic_rnnt_joint_loss(enc.to(dev), pred.to(dev), w.to(dev), bias.to(dev),
+                                            torch.from_numpy(labels).to(dev), torch.from_numpy(T),
+                                            torch.from_numpy(S)).cpu().double().numpy()
+    rows = []
+    for b in range(len(T)):
+        e = enc[b, : T[b]].to(dev).float()
+        p = pred[b, : S[b] + 1].to(dev).float()
+        h = torch.tanh(e[:, None] + p[None]).to(torch.bfloat16).float()
+        rows.append((h @ w.to(dev).float().T + bias.to(dev)).reshape(-1, V))
+    acts = torch.cat(rows).contiguous()
+    c_acts = op.monotonic_rnnt_loss(acts, torch.from_numpy(labels).to(dev), torch.from_numpy(T),
+                                    torch.from_numpy(S)).cpu().double().numpy()
+    assert np.all(np.abs(c_fused - c_acts) <= 1e-3 * np.maximum(1.0, np.abs(c_acts))), (c_fused, c_acts)
