@@ -132,12 +132,18 @@ RNNTStatus mrnnt_joint_live_rows(const mrnnt_joint_problem *p, void *workspace, 
 
 /* After mrnnt_joint_live_rows: for live row i (n_live = the count it produced, read back by the caller),
  * G[i, :] = grad_scale[b] * dcost_b/dz (bf16 [n_live, V]), Hact[i, :] = tanh(enc + pred) (bf16 [n_live, H]),
- * bt_idx[i] = b*(enc_stride/H) + t and bs_idx[i] = b*(pred_stride/H) + s (int64). Then
+ * bt_idx[i] = b*(enc_stride/H) + t and bs_idx[i] = b*(pred_stride/H) + s (int64; either may be NULL). Then
  * dweight = G^T Hact, dbias = sum_i G[i], and with dpre = (G weight) * (1 - Hact^2):
  * denc[bt_idx[i]] += dpre[i], dpred[bs_idx[i]] += dpre[i]. grad_scale may be NULL (= 1). */
 RNNTStatus mrnnt_joint_backward(const mrnnt_joint_problem *p, void *workspace, int64_t n_live,
                                 const float *grad_scale, void *G, void *Hact, int64_t *bt_idx, int64_t *bs_idx,
                                 hipStream_t stream);
+
+/* After mrnnt_joint_backward, with dH = G weight (bf16 [n_live, H], e.g. a library GEMM): accumulate
+ * dpre = dH * (1 - Hact^2) into d_enc (fp32, enc's [B, enc_stride/H, H] shape; rows (b, t < T_b) are
+ * overwritten) and d_pred (fp32, pred's shape; added to: zero it first). Zero d_enc's padding rows yourself. */
+RNNTStatus mrnnt_joint_reduce(const mrnnt_joint_problem *p, void *workspace, int64_t n_live, const void *dH,
+                              const void *Hact, float *d_enc, float *d_pred, hipStream_t stream);
 
 int mrnnt_version(void);
 

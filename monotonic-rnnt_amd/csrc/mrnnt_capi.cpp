@@ -467,8 +467,7 @@ RNNTStatus mrnnt_joint_backward(const mrnnt_joint_problem *jp, void *ws, int64_t
     if (!ws) return fail(RNNT_STATUS_INVALID_VALUE, "workspace is null");
     if (n_live < 0 || n_live > jl.n_inband)
         return fail(RNNT_STATUS_INVALID_VALUE, "n_live outside [0, in-band rows]");
-    if (n_live > 0 && (!G || !Hact || !bt_idx || !bs_idx))
-        return fail(RNNT_STATUS_INVALID_VALUE, "G / Hact / bt_idx / bs_idx is null");
+    if (n_live > 0 && (!G || !Hact)) return fail(RNNT_STATUS_INVALID_VALUE, "G / Hact is null");
     if (n_live > 0 && (!aligned16(G) || !aligned16(Hact)))
         return fail(RNNT_STATUS_INVALID_VALUE, "G / Hact must be 16-byte aligned");
     const mrnnt_problem p = base_problem(jp);
@@ -481,6 +480,29 @@ RNNTStatus mrnnt_joint_backward(const mrnnt_joint_problem *jp, void *ws, int64_t
     j.scale = grad_scale;
     const hipError_t e = timed(K_JOINT_BWD, stream, [&] { return launch_joint_backward(d, j, stream); });
     if (e != hipSuccess) return fail_hip(e, "joint gradient kernel");
+    return RNNT_STATUS_SUCCESS;
+}
+
+RNNTStatus mrnnt_joint_reduce(const mrnnt_joint_problem *jp, void *ws, int64_t n_live, const void *dH,
+                              const void *Hact, float *d_enc, float *d_pred, hipStream_t stream) {
+    JointPlan jl;
+    RNNTStatus st = make_joint_plan(jp, &jl);
+    if (st != RNNT_STATUS_SUCCESS) return st;
+    if ((st = check_joint_pointers(jp)) != RNNT_STATUS_SUCCESS) return st;
+    if (!ws || !d_enc || !d_pred) return fail(RNNT_STATUS_INVALID_VALUE, "workspace / d_enc / d_pred is null");
+    if (n_live < 0 || n_live > jl.n_inband) return fail(RNNT_STATUS_INVALID_VALUE, "n_live outside [0, in-band rows]");
+    if (n_live > 0 && (!dH || !Hact || (reinterpret_cast<uintptr_t>(dH) & 7) || (reinterpret_cast<uintptr_t>(Hact) & 7)))
+        return fail(RNNT_STATUS_INVALID_VALUE, "dH / Hact null or not 8-byte aligned");
+    const mrnnt_problem p = base_problem(jp);
+    DevProblem d = make_dev(&p, jl.base, ws);
+    JointArgs j = joint_args(jp, jl, ws, n_live);
+    j.Hact = static_cast<unsigned short *>(const_cast<void *>(Hact));
+    const int64_t *off = reinterpret_cast<const int64_t *>(static_cast<char *>(ws) + jl.off_cnt);
+    const hipError_t e = timed(K_JOINT_RED, stream, [&] {
+        return launch_joint_reduce(d, j, off, jl.base.T_max, jl.base.S_max, static_cast<const unsigned short *>(dH),
+                                   d_enc, d_pred, stream);
+    });
+    if (e != hipSuccess) return fail_hip(e, "joint reduce kernel");
     return RNNT_STATUS_SUCCESS;
 }
 

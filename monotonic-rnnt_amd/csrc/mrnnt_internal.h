@@ -64,6 +64,8 @@ hipError_t launch_row_list(const DevProblem &p, int mode, int64_t *col_cnt, int 
                            unsigned long long *total, hipStream_t stream);
 hipError_t launch_joint_forward(const DevProblem &p, const JointArgs &j, hipStream_t stream);
 hipError_t launch_joint_backward(const DevProblem &p, const JointArgs &j, hipStream_t stream);
+hipError_t launch_joint_reduce(const DevProblem &p, const JointArgs &j, const int64_t *off, int T_max, int S_max,
+                               const unsigned short *dH, float *d_enc, float *d_pred, hipStream_t stream);
 hipError_t launch_zero(void *ptr, size_t bytes, hipStream_t stream);
 
 // Launch-shape knobs (experiment hook: mrnnt_tune in mrnnt_capi.cpp). Defaults are the tuned values.
@@ -80,7 +82,7 @@ Tuning &tuning();
 
 // Kernel-family ids for the profiling counters (mrnnt_profile_read order).
 enum KernelId { K_BAND = 0, K_SOFTMAX = 1, K_DP = 2, K_GRAD = 3, K_SETUP = 4, K_JOINT_FWD = 5, K_JOINT_BWD = 6,
-                K_COUNT = 7 };
+                K_JOINT_RED = 7, K_COUNT = 8 };
 
 hipError_t launch_setup(const int *T, const int *S, int B, int64_t *row_off, int64_t *col_off, hipStream_t stream);
 hipError_t launch_align(const DevProblem &p, const int *alignment, int64_t align_stride, int align_blank,

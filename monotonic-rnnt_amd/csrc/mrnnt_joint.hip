@@ -18,6 +18,8 @@
 // D[vocab][row] = sum_k W[vocab][k] h[row][k]: the accumulator holds 16 vocabulary entries of ONE row per
 // lane (vocab = (i&3) + 8 (i>>2) + 4 (l>>5)), so the per-row online softmax is register-local and the two
 // lane halves merge once at the end.
+#include <type_traits>
+
 #include "mrnnt_device.h"
 
 namespace mrnnt {
@@ -321,10 +323,8 @@ __global__ __launch_bounds__(256) void joint_bwd_kernel(DevProblem p, JointArgs 
     if (q.valid) {
         rc = row_coef(p, q.t, q.T, q.S, q.s, q.row, p.ll[q.b], p.labels + (int64_t)q.b * p.label_stride);
         sc = j.scale ? j.scale[q.b] : 1.0f;
-        if (half == 0) {
-            j.bt_idx[i] = (int64_t)q.b * (j.enc_sb / j.H) + q.t;
-            j.bs_idx[i] = (int64_t)q.b * (j.pred_sb / j.H) + q.s;
-        }
+        if (half == 0 && j.bt_idx) j.bt_idx[i] = (int64_t)q.b * (j.enc_sb / j.H) + q.t;
+        if (half == 0 && j.bs_idx) j.bs_idx[i] = (int64_t)q.b * (j.pred_sb / j.H) + q.s;
     }
     bf16x8 bfr[KS];
     build_act<KS, true>(j, q, half, i, bfr);
@@ -368,6 +368,95 @@ __global__ __launch_bounds__(256) void joint_bwd_kernel(DevProblem p, JointArgs 
         if (c + 1 < nch) st.store(wsh[buf ^ 1], bsh[buf ^ 1]);
         __syncthreads();
     }
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// backward tail: dpre = dH * (1 - Hact^2) over the live rows, summed into denc[b, t] (over s; written once per
+// column) and dpred[b, s] (over t; accumulated in LDS over a block of TT columns, then one fp32 atomic per
+// (s, h) per block). One workgroup per (utterance, block of TT frames, slice of HS hidden units); 4 hidden
+// units per thread (8-byte loads), 256/(HS/4) rows in flight.
+
+constexpr int kReduceTT = 64;
+
+template <int HS>
+__global__ __launch_bounds__(256) void joint_reduce_kernel(DevProblem p, JointArgs j, const int64_t *__restrict__ off,
+                                                           const unsigned short *__restrict__ dH,
+                                                           float *__restrict__ d_enc, float *__restrict__ d_pred,
+                                                           int ntb) {
+    constexpr int TPR = HS / 4;     // threads per row slice
+    constexpr int RP = 256 / TPR;   // rows in parallel
+    extern __shared__ float lds[];  // acc[(S_b+1) * HS] then red[RP][HS]
+    const int b = blockIdx.x / ntb;
+    const int t0 = (blockIdx.x % ntb) * kReduceTT;
+    const int T = p.T[b], S = p.S[b];
+    if (t0 >= T) return;
+    const int H = j.H;
+    const int h0 = blockIdx.y * HS;
+    const int tid = threadIdx.x;
+    const int hl = (tid % TPR) * 4, rsub = tid / TPR;
+    float *acc = lds;
+    float *red = lds + (S + 1) * HS;
+    for (int i = tid; i < (S + 1) * HS; i += 256) acc[i] = 0.0f;
+    __syncthreads();
+    const int64_t tslots = j.enc_sb / H, sslots = j.pred_sb / H;
+    const int t1 = min(t0 + kReduceTT, T);
+    for (int t = t0; t < t1; ++t) {
+        const int64_t col = p.col_off[b] + t;
+        const int64_t r0 = off[col], r1 = off[col + 1];
+        float e0 = 0.0f, e1 = 0.0f, e2 = 0.0f, e3 = 0.0f;
+        for (int64_t r = r0 + rsub; r < r1; r += RP) {
+            const int s = j.ls[r];
+            const uint2 dv = *reinterpret_cast<const uint2 *>(dH + r * H + h0 + hl);
+            const uint2 hv = *reinterpret_cast<const uint2 *>(j.Hact + r * H + h0 + hl);
+            const float h_0 = bf16_lo(hv.x), h_1 = bf16_hi(hv.x), h_2 = bf16_lo(hv.y), h_3 = bf16_hi(hv.y);
+            const float v0 = bf16_lo(dv.x) * (1.0f - h_0 * h_0), v1 = bf16_hi(dv.x) * (1.0f - h_1 * h_1);
+            const float v2 = bf16_lo(dv.y) * (1.0f - h_2 * h_2), v3 = bf16_hi(dv.y) * (1.0f - h_3 * h_3);
+            e0 += v0;
+            e1 += v1;
+            e2 += v2;
+            e3 += v3;
+            float *a = acc + s * HS + hl;  // distinct s within a column: one writer per element
+            a[0] += v0;
+            a[1] += v1;
+            a[2] += v2;
+            a[3] += v3;
+        }
+        float *rr = red + rsub * HS + hl;
+        rr[0] = e0;
+        rr[1] = e1;
+        rr[2] = e2;
+        rr[3] = e3;
+        __syncthreads();
+        if (tid < HS) {
+            float sum = 0.0f;
+#pragma unroll 4
+            for (int g = 0; g < RP; ++g) sum += red[g * HS + tid];
+            d_enc[((int64_t)b * tslots + t) * H + h0 + tid] = sum;
+        }
+        __syncthreads();
+    }
+    for (int i = tid; i < (S + 1) * HS; i += 256) {
+        const float v = acc[i];
+        if (v != 0.0f) atomicAdd(&d_pred[((int64_t)b * sslots + i / HS) * H + h0 + i % HS], v);
+    }
+}
+
+hipError_t launch_joint_reduce(const DevProblem &p, const JointArgs &j, const int64_t *off, int T_max, int S_max,
+                               const unsigned short *dH, float *d_enc, float *d_pred, hipStream_t stream) {
+    const int ntb = (T_max + kReduceTT - 1) / kReduceTT;
+    const int W = S_max + 1;
+    auto go = [&](auto hs_tag) {
+        constexpr int HS = decltype(hs_tag)::value;
+        const size_t lds = sizeof(float) * ((size_t)W * HS + 256 / (HS / 4) * HS);
+        joint_reduce_kernel<HS><<<dim3(p.B * ntb, j.H / HS), 256, lds, stream>>>(p, j, off, dH, d_enc, d_pred, ntb);
+    };
+    // LDS = W * HS + 4 KiB of fp32 <= 64 KiB
+    if (W <= 224) go(std::integral_constant<int, 64>());
+    else if (W <= 448) go(std::integral_constant<int, 32>());
+    else if (W <= 896) go(std::integral_constant<int, 16>());
+    else if (W <= 1792) go(std::integral_constant<int, 8>());
+    else go(std::integral_constant<int, 4>());
+    return hipGetLastError();
 }
 
 template <int KS>

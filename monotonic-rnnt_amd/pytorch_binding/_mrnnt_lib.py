@@ -26,7 +26,7 @@ MRNNT_BF16 = 1
 MRNNT_F16 = 2
 
 # kernel-family order of mrnnt_profile_read
-KERNELS = ("band", "log_softmax", "alpha_beta", "grad", "setup", "joint_fwd", "joint_bwd")
+KERNELS = ("band", "log_softmax", "alpha_beta", "grad", "setup", "joint_fwd", "joint_bwd", "joint_reduce")
 
 
 class MrnntProblem(ctypes.Structure):
@@ -109,6 +109,7 @@ def load() -> ctypes.CDLL:
             "mrnnt_joint_forward": (i, [JP, vp, sz, vp, i, vp]),
             "mrnnt_joint_live_rows": (i, [JP, vp, vp, vp]),
             "mrnnt_joint_backward": (i, [JP, vp, i64, vp, vp, vp, vp, vp, vp]),
+            "mrnnt_joint_reduce": (i, [JP, vp, i64, vp, vp, vp, vp, vp]),
             "mrnnt_last_error": (ctypes.c_char_p, []),
             "mrnnt_version": (i, []),
             "mrnnt_profile_enable": (None, [i]),

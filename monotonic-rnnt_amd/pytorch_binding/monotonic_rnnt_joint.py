@@ -9,9 +9,10 @@ computes the loss of `monotonic_rnnt_loss(acts, ...)` for the packed logits
 without materialising them: the HIP kernels of `mrnnt_joint.hip` form each tile of logits on the matrix cores
 (bf16 operands, fp32 accumulation) inside the log-softmax pass and again, for the live lattice rows only,
 inside the gradient pass. Backward returns gradients for enc, pred, weight and bias: the fused kernel writes
-the logit gradient G and the activations tanh(enc + pred) of the live rows (bf16), and dweight = G^T Hact,
-dbias = sum G, dpre = (G weight) (1 - Hact^2) and its scatter into enc / pred rows are plain library GEMMs and
-reductions (hipBLASLt through torch) over those rows.
+the logit gradient G and the activations tanh(enc + pred) of the live rows (bf16); dweight = G^T Hact (split-K
+batched GEMM, fp32 out), dH = G weight and dbias = sum G are plain library GEMMs / reductions over those rows
+(hipBLASLt through torch), and mrnnt_joint_reduce folds dpre = dH (1 - Hact^2) into denc (sum over s) and dpred
+(sum over t) in one pass.
 
 Shapes: enc [B, T_slots >= max T, H], pred [B, S_slots >= max S + 1, H], weight [V, H] (torch.nn.Linear
 layout), bias [V] or None; H in {128, 256, 384, 512, 640}. Inputs of other floating dtypes are cast to bf16
@@ -100,8 +101,9 @@ class _JointPrepared:
                                              1 if with_beta else 0, self.stream()), "mrnnt_joint_forward")
         return costs, ws
 
-    def backward_rows(self, ws, grad_scale):
-        """The fused gradient pass: (G [n, V], Hact [n, H], bt_idx [n], bs_idx [n]) over the live rows."""
+    def backward_rows(self, ws, grad_scale, with_index=False):
+        """The fused gradient pass over the live rows: (G [n, V], Hact [n, H]) and, with_index, the enc / pred
+        row of each live row (bt_idx, bs_idx)."""
         lib = _L.load()
         with torch.cuda.device(self.device):
             cnt = torch.zeros(1, dtype=torch.int64, device=self.device)
@@ -110,13 +112,42 @@ class _JointPrepared:
             n = int(cnt.item())  # one 8-byte read-back sizes the row buffers
             G = torch.empty(max(1, n), self.V, dtype=torch.bfloat16, device=self.device)
             Hact = torch.empty(max(1, n), self.H, dtype=torch.bfloat16, device=self.device)
-            bt = torch.empty(max(1, n), dtype=torch.int64, device=self.device)
-            bs = torch.empty(max(1, n), dtype=torch.int64, device=self.device)
+            bt = bs = None
+            if with_index:
+                bt = torch.empty(max(1, n), dtype=torch.int64, device=self.device)
+                bs = torch.empty(max(1, n), dtype=torch.int64, device=self.device)
             if grad_scale is not None:
                 grad_scale = grad_scale.detach().to(self.device, torch.float32).contiguous()
             _L.check(lib.mrnnt_joint_backward(ctypes.byref(self.problem), _vp(ws), n, _vp(grad_scale), _vp(G),
                                               _vp(Hact), _vp(bt), _vp(bs), self.stream()), "mrnnt_joint_backward")
-        return G[:n], Hact[:n], bt[:n], bs[:n]
+        if with_index:
+            return G[:n], Hact[:n], bt[:n], bs[:n]
+        return G[:n], Hact[:n]
+
+    def reduce(self, ws, dH, Hact, need_enc, need_pred):
+        """d_enc / d_pred (fp32) from dH = G weight over the live rows (mrnnt_joint_reduce)."""
+        d_enc = torch.zeros(self.enc.shape, dtype=torch.float32, device=self.device)
+        d_pred = torch.zeros(self.pred.shape, dtype=torch.float32, device=self.device)
+        with torch.cuda.device(self.device):
+            _L.check(_L.load().mrnnt_joint_reduce(ctypes.byref(self.problem), _vp(ws), dH.shape[0], _vp(dH),
+                                                  _vp(Hact), _vp(d_enc), _vp(d_pred), self.stream()),
+                     "mrnnt_joint_reduce")
+        return d_enc if need_enc else None, d_pred if need_pred else None
+
+
+def _split_k_weight_grad(G, Hact, chunks=32):
+    """dW = G^T Hact over n live rows (K = n, output [V, H]): split K into batched GEMMs with fp32 outputs, then
+    sum (a single long-K GEMM leaves most of the chip idle)."""
+    n = G.shape[0]
+    m = n // chunks
+    if m < 1024:
+        return torch.mm(G.t(), Hact, out_dtype=torch.float32)
+    head = chunks * m
+    part = torch.bmm(G[:head].view(chunks, m, -1).transpose(1, 2), Hact[:head].view(chunks, m, -1),
+                     out_dtype=torch.float32).sum(0)
+    if head < n:
+        part += torch.mm(G[head:].t(), Hact[head:], out_dtype=torch.float32)
+    return part
 
 
 class MonotonicRNNTJointFunction(torch.autograd.Function):
@@ -134,25 +165,18 @@ class MonotonicRNNTJointFunction(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_costs):
         prep, ws = ctx.prep, ctx.ws
-        G, Hact, bt, bs = prep.backward_rows(ws, grad_costs)
+        G, Hact = prep.backward_rows(ws, grad_costs)
         ctx.prep = ctx.ws = None
-        B, H = prep.B, prep.H
         d_enc = d_pred = d_w = d_b = None
         if ctx.needs_input_grad[2]:
-            d_w = (G.t() @ Hact).to(prep.weight.dtype)  # [V, H]
+            d_w = _split_k_weight_grad(G, Hact).to(prep.weight.dtype)  # [V, H]
         if ctx.bias_dtype is not None and ctx.needs_input_grad[3]:
             d_b = G.sum(0, dtype=torch.float32).to(ctx.bias_dtype)
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
-            hf = Hact.float()
-            dpre = (G @ prep.weight).float() * (1.0 - hf * hf)  # [n, H]
-            if ctx.needs_input_grad[0]:
-                d_enc = torch.zeros(B * prep.enc.size(1), H, dtype=torch.float32, device=G.device)
-                d_enc.index_add_(0, bt, dpre)
-                d_enc = d_enc.view(B, prep.enc.size(1), H).to(prep.enc.dtype)
-            if ctx.needs_input_grad[1]:
-                d_pred = torch.zeros(B * prep.pred.size(1), H, dtype=torch.float32, device=G.device)
-                d_pred.index_add_(0, bs, dpre)
-                d_pred = d_pred.view(B, prep.pred.size(1), H).to(prep.pred.dtype)
+            dH = G @ prep.weight  # [n, H] bf16 (hipBLASLt)
+            d_enc, d_pred = prep.reduce(ws, dH, Hact, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+            d_enc = None if d_enc is None else d_enc.to(prep.enc.dtype)
+            d_pred = None if d_pred is None else d_pred.to(prep.pred.dtype)
         return d_enc, d_pred, d_w, d_b, None, None, None, None
 
 
