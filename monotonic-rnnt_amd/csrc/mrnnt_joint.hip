@@ -156,77 +156,97 @@ __device__ __forceinline__ RowPos row_pos(const DevProblem &p, const JointArgs &
 }
 
 // B operand: h = bf16(tanh(enc[b,t] + pred[b,s])) for k = 16 ks + 8 half + [0, 8); optionally stored to Hact.
+// Invalid lanes (past the end of the list) read row 0 and zero the result: no branch around the loads (a
+// branch per load makes hipcc wait vmcnt(0) after each one).
 template <int KS, bool STORE>
 __device__ __forceinline__ void build_act(const JointArgs &j, const RowPos &q, int half, int64_t i,
                                           bf16x8 (&bfr)[KS]) {
     constexpr int H = 16 * KS;
-    const unsigned short *er = j.enc + (int64_t)q.b * j.enc_sb + (int64_t)q.t * H + 8 * half;
-    const unsigned short *pr = j.pred + (int64_t)q.b * j.pred_sb + (int64_t)q.s * H + 8 * half;
+    const bool v = q.valid;
+    const unsigned short *er = j.enc + (v ? (int64_t)q.b * j.enc_sb + (int64_t)q.t * H : 0) + 8 * half;
+    const unsigned short *pr = j.pred + (v ? (int64_t)q.b * j.pred_sb + (int64_t)q.s * H : 0) + 8 * half;
+    const float keep = v ? 1.0f : 0.0f;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
+        const u4 ev = *reinterpret_cast<const u4 *>(er + 16 * ks);
+        const u4 pv = *reinterpret_cast<const u4 *>(pr + 16 * ks);
         bf16x8 h;
-        if (q.valid) {
-            const u4 ev = *reinterpret_cast<const u4 *>(er + 16 * ks);
-            const u4 pv = *reinterpret_cast<const u4 *>(pr + 16 * ks);
 #pragma unroll
-            for (int w = 0; w < 4; ++w) {
-                h[2 * w] = (__bf16)fast_tanh(bf16_lo(ev[w]) + bf16_lo(pv[w]));
-                h[2 * w + 1] = (__bf16)fast_tanh(bf16_hi(ev[w]) + bf16_hi(pv[w]));
-            }
-            if (STORE) *reinterpret_cast<bf16x8 *>(j.Hact + i * H + 16 * ks + 8 * half) = h;
-        } else {
-#pragma unroll
-            for (int w = 0; w < 8; ++w) h[w] = (__bf16)0.0f;
+        for (int w = 0; w < 4; ++w) {
+            h[2 * w] = (__bf16)(keep * fast_tanh(bf16_lo(ev[w]) + bf16_lo(pv[w])));
+            h[2 * w + 1] = (__bf16)(keep * fast_tanh(bf16_hi(ev[w]) + bf16_hi(pv[w])));
         }
+        if (STORE && v) *reinterpret_cast<bf16x8 *>(j.Hact + i * H + 16 * ks + 8 * half) = h;
         bfr[ks] = h;
     }
 }
 
-// W chunk staging: 32 vocabulary rows x H bf16 into a padded LDS image (row stride H + 8 elements)
+// W chunk (32 vocabulary rows x H bf16) in LDS: unpadded, the 16-byte piece p of row r stored at piece
+// p ^ (r & 15) (T2 XOR swizzle: the 16 lanes of a ds_read_b128 group read 16 distinct rows at one column and
+// land on 16 distinct bank quads). Filled by LDS-DMA (global_load_lds_dwordx4: 1 KiB per wave-instruction,
+// lane-linear destination, so the swizzle goes on the per-lane SOURCE address) -- no staging registers.
 template <int KS>
-struct WStage {
+struct WTile {
     static constexpr int H = 16 * KS;
-    static constexpr int LDW = H + 8;
-    static constexpr int PPT = H / 64;  // 16-byte pieces per thread (32 rows * H / 8 pieces / 256 threads)
-    u4 reg[PPT];
-    float breg;
-    __device__ __forceinline__ void load(const JointArgs &j, int V, int c) {
+    static constexpr int CPR = H / 8;    // 16-byte pieces per row (a multiple of 16 for H % 128 == 0)
+    static constexpr int NI = CPR / 2;   // wave-instructions per tile: 32 * CPR / 64
+    static constexpr int ELEMS = 32 * H; // bf16 elements per tile
+
+    // issue the DMA of vocabulary chunk c into wbuf (rows >= V read row V-1; the epilogue masks them)
+    __device__ static __forceinline__ void stage(const JointArgs &j, int V, int c, unsigned short *wbuf) {
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
-        for (int m = 0; m < PPT; ++m) {
-            const int q = threadIdx.x + 256 * m;
-            const int rw = q / (H / 8), c8 = q % (H / 8);
-            const int v = 32 * c + rw;
-            reg[m] = v < V ? *reinterpret_cast<const u4 *>(j.W + (int64_t)v * H + 8 * c8) : (u4){0u, 0u, 0u, 0u};
-        }
-        if (threadIdx.x < 32) {
-            const int v = 32 * c + threadIdx.x;
-            breg = v < V ? (j.bias ? j.bias[v] : 0.0f) : 0.0f;
+        for (int ii = 0; ii < NI / 4; ++ii) {
+            const int i = 4 * ii + wave;
+            const int L = 64 * i + lane;
+            const int r = L / CPR, pc = L % CPR;
+            const int v = min(32 * c + r, V - 1);
+            const unsigned short *g = j.W + (int64_t)v * H + 8 * (pc ^ (r & 15));
+            __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void *)(wbuf + 512 * i), 16, 0, 0);
         }
     }
-    __device__ __forceinline__ void store(unsigned short *wsh, float *bsh) const {
+
+    // one 32x32 output tile: D[vocab][row] = sum_k W[vocab][k] h[row][k]; A fragments stream from LDS
+    // through a 4-deep register ring so no MFMA waits on a ds_read it has just issued. The swizzled piece of
+    // k-step ks = 8m + k' is 16m + ((2k' + half) ^ (r & 15)): 8 base addresses, m in the immediate offset.
+    __device__ static __forceinline__ f32x16 mma(const unsigned short *wbuf, const bf16x8 (&bfr)[KS], int lane) {
+        const int r = lane & 31, half = lane >> 5;
+        const unsigned short *row = wbuf + r * H;
+        const unsigned short *base[8];
 #pragma unroll
-        for (int m = 0; m < PPT; ++m) {
-            const int q = threadIdx.x + 256 * m;
-            const int rw = q / (H / 8), c8 = q % (H / 8);
-            *reinterpret_cast<u4 *>(wsh + rw * LDW + 8 * c8) = reg[m];
+        for (int k = 0; k < 8; ++k) base[k] = row + 8 * ((2 * k + half) ^ (r & 15));
+        auto rd = [&](int ks) { return *reinterpret_cast<const bf16x8 *>(base[ks & 7] + 128 * (ks >> 3)); };
+        constexpr int D = KS < 4 ? KS : 4;
+        bf16x8 a[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d) a[d] = rd(d);
+        f32x16 acc;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks % D], bfr[ks], acc, 0, 0, 0);
+            if (ks + D < KS) a[ks % D] = rd(ks + D);
         }
-        if (threadIdx.x < 32) bsh[threadIdx.x] = breg;
+        return acc;
     }
 };
 
-template <int KS>
-__device__ __forceinline__ f32x16 tile_mma(const unsigned short *wsh, const bf16x8 (&bfr)[KS], int lane) {
-    constexpr int LDW = 16 * KS + 8;
-    const unsigned short *wrow = wsh + (lane & 31) * LDW + 8 * (lane >> 5);
-    f32x16 acc;
+__device__ __forceinline__ void wait_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// z for the 16 accumulator entries of a lane: + bias, -inf past V. bias_lds holds the whole (padded) bias.
+__device__ __forceinline__ void logits(const f32x16 &acc, const float *bias_lds, int c, int half, int V,
+                                       float (&z)[16]) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+    for (int q4 = 0; q4 < 4; ++q4) {
+        const int v0 = 32 * c + 8 * q4 + 4 * half;
+        const f4 bv = *reinterpret_cast<const f4 *>(bias_lds + v0);
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8 *>(wrow + 16 * ks);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bfr[ks], acc, 0, 0, 0);
+        for (int e = 0; e < 4; ++e) {
+            const float x = acc[4 * q4 + e] + bv[e];
+            z[4 * q4 + e] = (v0 + e < V) ? x : NEG_INF_F;
+        }
     }
-    return acc;
 }
 
 // index of the accumulator register holding vocabulary offset jj (0..31) of a chunk, or -1 if the other lane
@@ -235,38 +255,72 @@ __device__ __forceinline__ int acc_reg_of(int jj, int half) {
     return (((jj >> 2) & 1) == half) ? ((jj & 3) + 4 * (jj >> 3)) : -1;
 }
 
+// Chunk pipeline shared by both passes: chunk c's MFMAs (from LDS buffer c & 1) run beside the epilogue of
+// chunk c-1 (registers only) while the DMA of chunk c+1 fills the other buffer; one barrier per chunk.
+template <int KS, class Epi>
+__device__ __forceinline__ void chunk_loop(const JointArgs &j, int V, unsigned short *wsh, const bf16x8 (&bfr)[KS],
+                                           int lane, Epi &&epi) {
+    using WT = WTile<KS>;
+    const int nch = (V + 31) / 32;
+    unsigned short *b0 = wsh, *b1 = wsh + WT::ELEMS;
+    WT::stage(j, V, 0, b0);
+    wait_dma();
+    __syncthreads();
+    if (nch > 1) WT::stage(j, V, 1, b1);
+    f32x16 acc0 = WT::mma(b0, bfr, lane), acc1;
+    wait_dma();
+    __syncthreads();
+    // two chunks per trip so the ping-pong accumulators keep fixed registers
+    for (int c = 1;; c += 2) {
+        if (c >= nch) {
+            epi(acc0, c - 1);
+            break;
+        }
+        if (c + 1 < nch) WT::stage(j, V, c + 1, b0);
+        acc1 = WT::mma(b1, bfr, lane);
+        epi(acc0, c - 1);
+        wait_dma();
+        __syncthreads();
+        if (c + 1 >= nch) {
+            epi(acc1, c);
+            break;
+        }
+        if (c + 2 < nch) WT::stage(j, V, c + 2, b1);
+        acc0 = WT::mma(b0, bfr, lane);
+        epi(acc1, c);
+        wait_dma();
+        __syncthreads();
+    }
+}
+
+// LDS: two W tiles, then the bias padded to whole chunks
+template <int KS>
+__device__ __forceinline__ float *load_bias(const JointArgs &j, int V, unsigned short *wsh) {
+    float *bl = reinterpret_cast<float *>(wsh + 2 * WTile<KS>::ELEMS);
+    const int nb = (V + 31) / 32 * 32;
+    for (int v = threadIdx.x; v < nb; v += blockDim.x) bl[v] = (v < V && j.bias) ? j.bias[v] : 0.0f;
+    return bl;
+}
+
 template <int KS>
 __global__ __launch_bounds__(256) void joint_fwd_kernel(DevProblem p, JointArgs j) {
-    constexpr int LDW = WStage<KS>::LDW;
-    __shared__ __attribute__((aligned(16))) unsigned short wsh[2][32 * LDW];
-    __shared__ float bsh[2][32];
+    extern __shared__ __attribute__((aligned(16))) unsigned short wsh[];
     const int lane = threadIdx.x & 63, half = lane >> 5;
     const int64_t i = (int64_t)blockIdx.x * 128 + (threadIdx.x >> 6) * 32 + (lane & 31);
     const RowPos q = row_pos(p, j, i);
+    const int V = p.V, blank = p.blank;
+    const float *bias = load_bias<KS>(j, V, wsh);
     bf16x8 bfr[KS];
     build_act<KS, false>(j, q, half, i, bfr);
 
-    const int V = p.V, blank = p.blank;
-    const int nch = (V + 31) / 32;
-    WStage<KS> st;
-    st.load(j, V, 0);
-    st.store(wsh[0], bsh[0]);
-    __syncthreads();
-
     float m = NEG_INF_F, sum = 0.0f, zb = 0.0f, ze = 0.0f;
     bool fb = false, fe = false;
-    for (int c = 0; c < nch; ++c) {
-        const int buf = c & 1;
-        if (c + 1 < nch) st.load(j, V, c + 1);
-        const f32x16 acc = tile_mma<KS>(wsh[buf], bfr, lane);
+    chunk_loop<KS>(j, V, wsh, bfr, lane, [&](const f32x16 &acc, int c) {
         float z[16];
-        float cm = NEG_INF_F;
+        logits(acc, bias, c, half, V, z);
+        float cm = z[0];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int jj = (r & 3) + 8 * (r >> 2) + 4 * half;
-            z[r] = (32 * c + jj < V) ? acc[r] + bsh[buf][jj] : NEG_INF_F;
-            cm = fmaxf(cm, z[r]);
-        }
+        for (int r = 1; r < 16; ++r) cm = fmaxf(cm, z[r]);
         const float mn = fmaxf(m, cm);
         const float mr = (mn == NEG_INF_F) ? 0.0f : mn;
         float a = sum * fast_exp2((m - mr) * kLog2e);
@@ -283,16 +337,12 @@ __global__ __launch_bounds__(256) void joint_fwd_kernel(DevProblem p, JointArgs 
             }
         }
         const int jl = q.lab - 32 * c;
-        if (q.lab >= 0 && jl >= 0 && jl < 32) {
-            const int rl = acc_reg_of(jl, half);
-            if (rl >= 0) {
-                ze = pick_n<16>(z, rl);
-                fe = true;
-            }
+        const int rl = acc_reg_of(jl & 31, half);
+        if (q.lab >= 0 && jl >= 0 && jl < 32 && rl >= 0) {
+            ze = pick_n<16>(z, rl);
+            fe = true;
         }
-        if (c + 1 < nch) st.store(wsh[buf ^ 1], bsh[buf ^ 1]);
-        __syncthreads();
-    }
+    });
     // merge the two lane halves (same row, disjoint vocabulary)
     const float m2 = __shfl_xor(m, 32), s2 = __shfl_xor(sum, 32);
     const float zb2 = __shfl_xor(zb, 32), ze2 = __shfl_xor(ze, 32);
@@ -312,9 +362,7 @@ __global__ __launch_bounds__(256) void joint_fwd_kernel(DevProblem p, JointArgs 
 
 template <int KS>
 __global__ __launch_bounds__(256) void joint_bwd_kernel(DevProblem p, JointArgs j) {
-    constexpr int LDW = WStage<KS>::LDW;
-    __shared__ __attribute__((aligned(16))) unsigned short wsh[2][32 * LDW];
-    __shared__ float bsh[2][32];
+    extern __shared__ __attribute__((aligned(16))) unsigned short wsh[];
     const int lane = threadIdx.x & 63, half = lane >> 5;
     const int64_t i = (int64_t)blockIdx.x * 128 + (threadIdx.x >> 6) * 32 + (lane & 31);
     const RowPos q = row_pos(p, j, i);
@@ -326,27 +374,21 @@ __global__ __launch_bounds__(256) void joint_bwd_kernel(DevProblem p, JointArgs 
         if (half == 0 && j.bt_idx) j.bt_idx[i] = (int64_t)q.b * (j.enc_sb / j.H) + q.t;
         if (half == 0 && j.bs_idx) j.bs_idx[i] = (int64_t)q.b * (j.pred_sb / j.H) + q.s;
     }
+    const int V = p.V, blank = p.blank;
+    const float *bias = load_bias<KS>(j, V, wsh);
     bf16x8 bfr[KS];
     build_act<KS, true>(j, q, half, i, bfr);
 
-    const int V = p.V, blank = p.blank;
-    const int nch = (V + 31) / 32;
     const bool vec_out = (V & 3) == 0;
-    unsigned short *grow = j.G + i * V;
-    WStage<KS> st;
-    st.load(j, V, 0);
-    st.store(wsh[0], bsh[0]);
-    __syncthreads();
-    for (int c = 0; c < nch; ++c) {
-        const int buf = c & 1;
-        if (c + 1 < nch) st.load(j, V, c + 1);
-        const f32x16 acc = tile_mma<KS>(wsh[buf], bfr, lane);
+    unsigned short *grow = j.G + (q.valid ? i : 0) * V;
+    chunk_loop<KS>(j, V, wsh, bfr, lane, [&](const f32x16 &acc, int c) {
+        float z[16];
+        logits(acc, bias, c, half, V, z);
         float g[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const int jj = (r & 3) + 8 * (r >> 2) + 4 * half;
-            const int v = 32 * c + jj;
-            float x = fast_exp2(fmaf(acc[r] + bsh[buf][jj], kLog2e, rc.c2));
+            const int v = 32 * c + (r & 3) + 8 * (r >> 2) + 4 * half;
+            float x = fast_exp2(fmaf(z[r], kLog2e, rc.c2));
             x -= (v == blank ? rc.cb : 0.0f) + (v == rc.lab ? rc.ce : 0.0f);
             g[r] = x * sc;
         }
@@ -365,9 +407,7 @@ __global__ __launch_bounds__(256) void joint_bwd_kernel(DevProblem p, JointArgs 
                 }
             }
         }
-        if (c + 1 < nch) st.store(wsh[buf ^ 1], bsh[buf ^ 1]);
-        __syncthreads();
-    }
+    });
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -460,25 +500,29 @@ hipError_t launch_joint_reduce(const DevProblem &p, const JointArgs &j, const in
 }
 
 template <int KS>
-static void launch_kh(const DevProblem &p, const JointArgs &j, bool bwd, hipStream_t stream) {
+static hipError_t launch_kh(const DevProblem &p, const JointArgs &j, bool bwd, hipStream_t stream) {
     const int64_t blocks = (j.n + 127) / 128;
-    if (bwd)
-        joint_bwd_kernel<KS><<<(int)blocks, 256, 0, stream>>>(p, j);
-    else
-        joint_fwd_kernel<KS><<<(int)blocks, 256, 0, stream>>>(p, j);
+    const size_t lds = sizeof(unsigned short) * 2 * WTile<KS>::ELEMS + sizeof(float) * ((p.V + 31) / 32 * 32);
+    auto kern = bwd ? joint_bwd_kernel<KS> : joint_fwd_kernel<KS>;
+    if (lds > 65536) {
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    kern<<<(int)blocks, 256, lds, stream>>>(p, j);
+    return hipGetLastError();
 }
 
 static hipError_t launch_joint(const DevProblem &p, const JointArgs &j, bool bwd, hipStream_t stream) {
     if (j.n <= 0) return hipSuccess;
     switch (j.H) {
-        case 128: launch_kh<8>(p, j, bwd, stream); break;
-        case 256: launch_kh<16>(p, j, bwd, stream); break;
-        case 384: launch_kh<24>(p, j, bwd, stream); break;
-        case 512: launch_kh<32>(p, j, bwd, stream); break;
-        case 640: launch_kh<40>(p, j, bwd, stream); break;
+        case 128: return launch_kh<8>(p, j, bwd, stream);
+        case 256: return launch_kh<16>(p, j, bwd, stream);
+        case 384: return launch_kh<24>(p, j, bwd, stream);
+        case 512: return launch_kh<32>(p, j, bwd, stream);
+        case 640: return launch_kh<40>(p, j, bwd, stream);
         default: return hipErrorInvalidValue;
     }
-    return hipGetLastError();
 }
 
 hipError_t launch_joint_forward(const DevProblem &p, const JointArgs &j, hipStream_t stream) {
