@@ -557,6 +557,7 @@ int mrnnt_tune(const char *key, int value) {
     else if (!std::strcmp(key, "nt_store")) slot = &t.nt_store;
     else if (!std::strcmp(key, "nt_load")) slot = &t.nt_load;
     else if (!std::strcmp(key, "occ_skip")) slot = &t.occ_skip;
+    else if (!std::strcmp(key, "joint_variant")) slot = &t.joint_variant;
     if (!slot) return -1;
     const int prev = *slot;
     if (value >= 0) *slot = value;

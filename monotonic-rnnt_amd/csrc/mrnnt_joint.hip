@@ -209,6 +209,7 @@ struct WTile {
     // one 32x32 output tile: D[vocab][row] = sum_k W[vocab][k] h[row][k]; A fragments stream from LDS
     // through a 4-deep register ring so no MFMA waits on a ds_read it has just issued. The swizzled piece of
     // k-step ks = 8m + k' is 16m + ((2k' + half) ^ (r & 15)): 8 base addresses, m in the immediate offset.
+    template <int RING = 4>
     __device__ static __forceinline__ f32x16 mma(const unsigned short *wbuf, const bf16x8 (&bfr)[KS], int lane) {
         const int r = lane & 31, half = lane >> 5;
         const unsigned short *row = wbuf + r * H;
@@ -216,7 +217,7 @@ struct WTile {
 #pragma unroll
         for (int k = 0; k < 8; ++k) base[k] = row + 8 * ((2 * k + half) ^ (r & 15));
         auto rd = [&](int ks) { return *reinterpret_cast<const bf16x8 *>(base[ks & 7] + 128 * (ks >> 3)); };
-        constexpr int D = KS < 4 ? KS : 4;
+        constexpr int D = KS < RING ? KS : RING;
         bf16x8 a[D];
 #pragma unroll
         for (int d = 0; d < D; ++d) a[d] = rd(d);
@@ -234,6 +235,14 @@ struct WTile {
 
 __device__ __forceinline__ void wait_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// wait until at most N vector-memory operations of this wave are outstanding (in-order completion): the
+// DMA of the chunk after next stays in flight across the barrier
+template <int N>
+__device__ __forceinline__ void wait_dma_leave() {
+    static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
 // z for the 16 accumulator entries of a lane: + bias, -inf past V. bias_lds holds the whole (padded) bias.
 __device__ __forceinline__ void logits(const f32x16 &acc, const float *bias_lds, int c, int half, int V,
                                        float (&z)[16]) {
@@ -242,10 +251,12 @@ __device__ __forceinline__ void logits(const f32x16 &acc, const float *bias_lds,
         const int v0 = 32 * c + 8 * q4 + 4 * half;
         const f4 bv = *reinterpret_cast<const f4 *>(bias_lds + v0);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const float x = acc[4 * q4 + e] + bv[e];
-            z[4 * q4 + e] = (v0 + e < V) ? x : NEG_INF_F;
-        }
+        for (int e = 0; e < 4; ++e) z[4 * q4 + e] = acc[4 * q4 + e] + bv[e];
+    }
+    if (32 * c + 32 > V) {  // only the last chunk can reach past the vocabulary
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            if (32 * c + (r & 3) + 8 * (r >> 2) + 4 * half >= V) z[r] = NEG_INF_F;
     }
 }
 
@@ -255,67 +266,102 @@ __device__ __forceinline__ int acc_reg_of(int jj, int half) {
     return (((jj >> 2) & 1) == half) ? ((jj & 3) + 4 * (jj >> 3)) : -1;
 }
 
-// Chunk pipeline shared by both passes: chunk c's MFMAs (from LDS buffer c & 1) run beside the epilogue of
-// chunk c-1 (registers only) while the DMA of chunk c+1 fills the other buffer; one barrier per chunk.
-template <int KS, class Epi>
+// Chunk pipeline shared by both passes: NB LDS buffers; chunk c's MFMAs run beside the epilogue of chunk c-1
+// (registers only) while the DMAs of chunks c+1 .. c+NB-1 are in flight; one raw s_barrier per chunk (a
+// __syncthreads would drain every DMA with vmcnt(0)).
+template <int KS, int NB, class Epi>
 __device__ __forceinline__ void chunk_loop(const JointArgs &j, int V, unsigned short *wsh, const bf16x8 (&bfr)[KS],
                                            int lane, Epi &&epi) {
     using WT = WTile<KS>;
+    constexpr int NPW = WT::NI / 4;  // DMA instructions per wave per chunk
     const int nch = (V + 31) / 32;
-    unsigned short *b0 = wsh, *b1 = wsh + WT::ELEMS;
-    WT::stage(j, V, 0, b0);
-    wait_dma();
-    __syncthreads();
-    if (nch > 1) WT::stage(j, V, 1, b1);
-    f32x16 acc0 = WT::mma(b0, bfr, lane), acc1;
-    wait_dma();
-    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < NB - 1; ++c)
+        if (c < nch) WT::stage(j, V, c, wsh + c * WT::ELEMS);
+    auto ready = [&](int c) {  // chunk c landed in LDS for every wave
+        if (c + NB - 2 < nch) wait_dma_leave<(NB - 2) * NPW>();
+        else wait_dma();
+        __builtin_amdgcn_s_barrier();
+    };
+    auto buf = [&](int c) { return wsh + (c % NB) * WT::ELEMS; };
+    ready(0);
+    if (NB - 1 < nch) WT::stage(j, V, NB - 1, buf(NB - 1));
+    f32x16 acc0 = WT::mma(buf(0), bfr, lane), acc1;
+    if (nch > 1) ready(1);
     // two chunks per trip so the ping-pong accumulators keep fixed registers
     for (int c = 1;; c += 2) {
         if (c >= nch) {
             epi(acc0, c - 1);
             break;
         }
-        if (c + 1 < nch) WT::stage(j, V, c + 1, b0);
-        acc1 = WT::mma(b1, bfr, lane);
+        if (c + NB - 1 < nch) WT::stage(j, V, c + NB - 1, buf(c + NB - 1));
+        acc1 = WT::mma(buf(c), bfr, lane);
         epi(acc0, c - 1);
-        wait_dma();
-        __syncthreads();
         if (c + 1 >= nch) {
             epi(acc1, c);
             break;
         }
-        if (c + 2 < nch) WT::stage(j, V, c + 2, b1);
-        acc0 = WT::mma(b0, bfr, lane);
+        ready(c + 1);
+        if (c + NB < nch) WT::stage(j, V, c + NB, buf(c + NB));
+        acc0 = WT::mma(buf(c + 1), bfr, lane);
         epi(acc1, c);
-        wait_dma();
-        __syncthreads();
+        if (c + 2 < nch) ready(c + 2);
     }
 }
 
-// LDS: two W tiles, then the bias padded to whole chunks
-template <int KS>
+// Simple chunk loop for two workgroups per CU (two waves per SIMD): double-buffered DMA, one accumulator; the
+// partner workgroup's MFMAs cover this one's epilogue and activation build.
+template <int KS, class Epi>
+__device__ __forceinline__ void chunk_loop_simple(const JointArgs &j, int V, unsigned short *wsh,
+                                                  const bf16x8 (&bfr)[KS], int lane, Epi &&epi) {
+    using WT = WTile<KS>;
+    const int nch = (V + 31) / 32;
+    WT::stage(j, V, 0, wsh);
+    wait_dma();
+    __builtin_amdgcn_s_barrier();
+    for (int c = 0; c < nch; ++c) {
+        if (c + 1 < nch) WT::stage(j, V, c + 1, wsh + ((c + 1) & 1) * WT::ELEMS);
+        const f32x16 acc = WT::template mma<2>(wsh + (c & 1) * WT::ELEMS, bfr, lane);
+        epi(acc, c);
+        wait_dma();
+        __builtin_amdgcn_s_barrier();
+    }
+}
+
+template <int KS, int NB, int OCC, class Epi>
+__device__ __forceinline__ void run_chunks(const JointArgs &j, int V, unsigned short *wsh, const bf16x8 (&bfr)[KS],
+                                           int lane, Epi &&epi) {
+    if constexpr (OCC == 1)
+        chunk_loop<KS, NB>(j, V, wsh, bfr, lane, epi);
+    else
+        chunk_loop_simple<KS>(j, V, wsh, bfr, lane, epi);
+}
+
+// LDS: NB W tiles, then the bias padded to whole chunks
+template <int KS, int NB>
 __device__ __forceinline__ float *load_bias(const JointArgs &j, int V, unsigned short *wsh) {
-    float *bl = reinterpret_cast<float *>(wsh + 2 * WTile<KS>::ELEMS);
+    float *bl = reinterpret_cast<float *>(wsh + NB * WTile<KS>::ELEMS);
     const int nb = (V + 31) / 32 * 32;
     for (int v = threadIdx.x; v < nb; v += blockDim.x) bl[v] = (v < V && j.bias) ? j.bias[v] : 0.0f;
     return bl;
 }
 
-template <int KS>
-__global__ __launch_bounds__(256) void joint_fwd_kernel(DevProblem p, JointArgs j) {
+template <int KS, int NB, int OCC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void joint_fwd_kernel(DevProblem p,
+                                                                                          JointArgs j) {
     extern __shared__ __attribute__((aligned(16))) unsigned short wsh[];
     const int lane = threadIdx.x & 63, half = lane >> 5;
     const int64_t i = (int64_t)blockIdx.x * 128 + (threadIdx.x >> 6) * 32 + (lane & 31);
     const RowPos q = row_pos(p, j, i);
     const int V = p.V, blank = p.blank;
-    const float *bias = load_bias<KS>(j, V, wsh);
+    const float *bias = load_bias<KS, NB>(j, V, wsh);
+    __syncthreads();
     bf16x8 bfr[KS];
     build_act<KS, false>(j, q, half, i, bfr);
 
     float m = NEG_INF_F, sum = 0.0f, zb = 0.0f, ze = 0.0f;
     bool fb = false, fe = false;
-    chunk_loop<KS>(j, V, wsh, bfr, lane, [&](const f32x16 &acc, int c) {
+    run_chunks<KS, NB, OCC>(j, V, wsh, bfr, lane, [&](const f32x16 &acc, int c) {
         float z[16];
         logits(acc, bias, c, half, V, z);
         float cm = z[0];
@@ -360,8 +406,9 @@ __global__ __launch_bounds__(256) void joint_fwd_kernel(DevProblem p, JointArgs 
     }
 }
 
-template <int KS>
-__global__ __launch_bounds__(256) void joint_bwd_kernel(DevProblem p, JointArgs j) {
+template <int KS, int NB, int OCC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void joint_bwd_kernel(DevProblem p,
+                                                                                          JointArgs j) {
     extern __shared__ __attribute__((aligned(16))) unsigned short wsh[];
     const int lane = threadIdx.x & 63, half = lane >> 5;
     const int64_t i = (int64_t)blockIdx.x * 128 + (threadIdx.x >> 6) * 32 + (lane & 31);
@@ -375,13 +422,14 @@ __global__ __launch_bounds__(256) void joint_bwd_kernel(DevProblem p, JointArgs 
         if (half == 0 && j.bs_idx) j.bs_idx[i] = (int64_t)q.b * (j.pred_sb / j.H) + q.s;
     }
     const int V = p.V, blank = p.blank;
-    const float *bias = load_bias<KS>(j, V, wsh);
+    const float *bias = load_bias<KS, NB>(j, V, wsh);
+    __syncthreads();
     bf16x8 bfr[KS];
     build_act<KS, true>(j, q, half, i, bfr);
 
     const bool vec_out = (V & 3) == 0;
     unsigned short *grow = j.G + (q.valid ? i : 0) * V;
-    chunk_loop<KS>(j, V, wsh, bfr, lane, [&](const f32x16 &acc, int c) {
+    run_chunks<KS, NB, OCC>(j, V, wsh, bfr, lane, [&](const f32x16 &acc, int c) {
         float z[16];
         logits(acc, bias, c, half, V, z);
         float g[16];
@@ -426,12 +474,15 @@ __global__ __launch_bounds__(256) void joint_reduce_kernel(DevProblem p, JointAr
     constexpr int TPR = HS / 4;     // threads per row slice
     constexpr int RP = 256 / TPR;   // rows in parallel
     extern __shared__ float lds[];  // acc[(S_b+1) * HS] then red[RP][HS]
-    const int b = blockIdx.x / ntb;
-    const int t0 = (blockIdx.x % ntb) * kReduceTT;
+    const int H = j.H;
+    const int nh = H / HS;
+    // the h-slices of one block of frames are consecutive workgroups: they read the same rows (L2 reuse)
+    const int bx = blockIdx.x / nh;
+    const int h0 = (blockIdx.x % nh) * HS;
+    const int b = bx / ntb;
+    const int t0 = (bx % ntb) * kReduceTT;
     const int T = p.T[b], S = p.S[b];
     if (t0 >= T) return;
-    const int H = j.H;
-    const int h0 = blockIdx.y * HS;
     const int tid = threadIdx.x;
     const int hl = (tid % TPR) * 4, rsub = tid / TPR;
     float *acc = lds;
@@ -488,22 +539,20 @@ hipError_t launch_joint_reduce(const DevProblem &p, const JointArgs &j, const in
     auto go = [&](auto hs_tag) {
         constexpr int HS = decltype(hs_tag)::value;
         const size_t lds = sizeof(float) * ((size_t)W * HS + 256 / (HS / 4) * HS);
-        joint_reduce_kernel<HS><<<dim3(p.B * ntb, j.H / HS), 256, lds, stream>>>(p, j, off, dH, d_enc, d_pred, ntb);
+        joint_reduce_kernel<HS><<<p.B * ntb * (j.H / HS), 256, lds, stream>>>(p, j, off, dH, d_enc, d_pred, ntb);
     };
-    // LDS = W * HS + 4 KiB of fp32 <= 64 KiB
-    if (W <= 224) go(std::integral_constant<int, 64>());
-    else if (W <= 448) go(std::integral_constant<int, 32>());
+    // LDS = W * HS + 4 KiB of fp32: about 30 KiB at the headline (several workgroups per CU), <= 64 KiB always
+    if (W <= 448) go(std::integral_constant<int, 32>());
     else if (W <= 896) go(std::integral_constant<int, 16>());
     else if (W <= 1792) go(std::integral_constant<int, 8>());
     else go(std::integral_constant<int, 4>());
     return hipGetLastError();
 }
 
-template <int KS>
-static hipError_t launch_kh(const DevProblem &p, const JointArgs &j, bool bwd, hipStream_t stream) {
+template <int KS, int NB, int OCC>
+static hipError_t launch_knb(const DevProblem &p, const JointArgs &j, bool bwd, size_t lds, hipStream_t stream) {
     const int64_t blocks = (j.n + 127) / 128;
-    const size_t lds = sizeof(unsigned short) * 2 * WTile<KS>::ELEMS + sizeof(float) * ((p.V + 31) / 32 * 32);
-    auto kern = bwd ? joint_bwd_kernel<KS> : joint_fwd_kernel<KS>;
+    auto kern = bwd ? joint_bwd_kernel<KS, NB, OCC> : joint_fwd_kernel<KS, NB, OCC>;
     if (lds > 65536) {
         const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -511,6 +560,19 @@ static hipError_t launch_kh(const DevProblem &p, const JointArgs &j, bool bwd, h
     }
     kern<<<(int)blocks, 256, lds, stream>>>(p, j);
     return hipGetLastError();
+}
+
+// joint_variant 0: one workgroup per CU, ping-pong accumulators, three LDS buffers when they fit (else two);
+// joint_variant 1: two workgroups per CU (256 registers per lane), double-buffered simple loop
+template <int KS>
+static hipError_t launch_kh(const DevProblem &p, const JointArgs &j, bool bwd, hipStream_t stream) {
+    const size_t bias = sizeof(float) * ((p.V + 31) / 32 * 32);
+    const size_t tile = sizeof(unsigned short) * WTile<KS>::ELEMS;
+    if (tuning().joint_variant == 1 && 2 * (2 * tile + bias) <= 160 * 1024)
+        return launch_knb<KS, 2, 2>(p, j, bwd, 2 * tile + bias, stream);
+    if (3 * tile + bias <= 160 * 1024) return launch_knb<KS, 3, 1>(p, j, bwd, 3 * tile + bias, stream);
+    if (2 * tile + bias <= 160 * 1024) return launch_knb<KS, 2, 1>(p, j, bwd, 2 * tile + bias, stream);
+    return hipErrorInvalidValue;
 }
 
 static hipError_t launch_joint(const DevProblem &p, const JointArgs &j, bool bwd, hipStream_t stream) {

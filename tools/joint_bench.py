@@ -34,11 +34,15 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-unfused", action="store_true")
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE")
     a = ap.parse_args()
     import _mrnnt_lib as L
     import monotonic_rnnt_joint as J
     import monotonic_rnnt_op as op
 
+    for kv in a.tune:
+        k, v = kv.split("=")
+        assert L.tune(k, int(v)) >= 0, k
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     B, T, S, V, H = a.B, a.T, a.S, a.V, a.H
@@ -83,7 +87,8 @@ def main():
             L.profile_enable(False)
         return dt, c.detach(), pr
 
-    out = {"config": {"B": B, "T": T, "S": S, "V": V, "H": H, "dtype": "bf16 operands, fp32 accumulate"}}
+    out = {"config": {"B": B, "T": T, "S": S, "V": V, "H": H, "dtype": "bf16 operands, fp32 accumulate"},
+           "tune": a.tune or None}
     dt, c_f, pr = timeit(fused, prof=True)
     # live rows of the backward pass (the gradient kernel's row count)
     prep = J._JointPrepared(enc.detach(), pred.detach(), W.detach(), bias.detach(), labels, Tl, Sl, 0)
