@@ -117,6 +117,10 @@ typedef struct mrnnt_joint_problem {
     int64_t pred_stride;     /* multiple of 8, >= (max_b S_b + 1) * H */
     const void *weight;      /* device bf16 [V, H] */
     const float *bias;       /* device fp32 [V] or NULL */
+    const int *alignment;    /* device [B, align_stride] or NULL: restriction as in mrnnt_problem */
+    int64_t align_stride;
+    int align_blank;
+    int max_shift;
 } mrnnt_joint_problem;
 
 RNNTStatus mrnnt_joint_workspace_size(const mrnnt_joint_problem *p, size_t *bytes);

@@ -333,6 +333,10 @@ mrnnt_problem base_problem(const mrnnt_joint_problem *jp) {
     p.acts = jp->enc;  // the lattice kernels never read acts on this path
     p.labels = jp->labels;
     p.label_stride = jp->label_stride;
+    p.alignment = jp->alignment;
+    p.align_stride = jp->align_stride;
+    p.align_blank = jp->align_blank;
+    p.max_shift = jp->max_shift;
     p.num_rows = -1;
     return p;
 }
@@ -427,6 +431,14 @@ RNNTStatus mrnnt_joint_forward(const mrnnt_joint_problem *jp, void *ws, size_t w
                             reinterpret_cast<int64_t *>(w + pl.off_col), stream);
     });
     if (e != hipSuccess) return fail_hip(e, "setup kernel");
+    if (pl.align) {
+        e = timed(K_BAND, stream, [&] {
+            return launch_align(d, p.alignment, p.align_stride, p.align_blank, p.max_shift,
+                                reinterpret_cast<int *>(w + pl.off_mtmp), reinterpret_cast<int *>(w + pl.off_min),
+                                reinterpret_cast<int *>(w + pl.off_max), stream);
+        });
+        if (e != hipSuccess) return fail_hip(e, "alignment band kernels");
+    }
     // out-of-band lp entries must be finite for the recursion (the acts path zero-fills them in its pass)
     if ((e = launch_zero(w + pl.off_lpb, pl.off_alpha - pl.off_lpb, stream)) != hipSuccess)
         return fail_hip(e, "lp zero fill");
@@ -557,7 +569,7 @@ int mrnnt_tune(const char *key, int value) {
     else if (!std::strcmp(key, "nt_store")) slot = &t.nt_store;
     else if (!std::strcmp(key, "nt_load")) slot = &t.nt_load;
     else if (!std::strcmp(key, "occ_skip")) slot = &t.occ_skip;
-    else if (!std::strcmp(key, "joint_variant")) slot = &t.joint_variant;
+    else if (!std::strcmp(key, "joint_nbuf")) slot = &t.joint_nbuf;
     if (!slot) return -1;
     const int prev = *slot;
     if (value >= 0) *slot = value;

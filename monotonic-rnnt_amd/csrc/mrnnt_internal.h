@@ -77,7 +77,7 @@ struct Tuning {
     int nt_store = 1;             // nontemporal stores of grads
     int nt_load = 1;              // nontemporal loads of acts (both streaming kernels)
     int occ_skip = 1;             // gradient: no acts read for rows with log-occupancy < kDeadLogOcc
-    int joint_variant = 1;        // fused joint kernels: 0 one workgroup/CU pipelined, 1 two workgroups/CU
+    int joint_nbuf = 2;           // fused joint kernels: LDS buffers for the weight chunks (2 or 3)
 };
 Tuning &tuning();
 

@@ -26,6 +26,7 @@ namespace mrnnt {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ float bf16_lo(unsigned u) { return __uint_as_float(u << 16); }
 __device__ __forceinline__ float bf16_hi(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
@@ -34,15 +35,6 @@ __device__ __forceinline__ float bf16_hi(unsigned u) { return __uint_as_float(u 
 __device__ __forceinline__ float fast_tanh(float x) {
     const float e = fast_exp2(-2.0f * kLog2e * fabsf(x));
     return copysignf((1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e), x);
-}
-
-// x[c] for a runtime c, as a sum of selects (a select chain gets rewritten into a scratch-indexed load)
-template <int N>
-__device__ __forceinline__ float pick_n(const float (&x)[N], int c) {
-    float r = 0.0f;
-#pragma unroll
-    for (int i = 0; i < N; ++i) r += (c == i) ? x[i] : 0.0f;
-    return r;
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -192,12 +184,15 @@ struct WTile {
     static constexpr int NI = CPR / 2;   // wave-instructions per tile: 32 * CPR / 64
     static constexpr int ELEMS = 32 * H; // bf16 elements per tile
 
-    // issue the DMA of vocabulary chunk c into wbuf (rows >= V read row V-1; the epilogue masks them)
+    // issue the DMA of vocabulary chunk c into wbuf (rows >= V read row V-1; the epilogue masks them); the NW
+    // waves of the workgroup split the NI wave-instructions
+    template <int NW>
     __device__ static __forceinline__ void stage(const JointArgs &j, int V, int c, unsigned short *wbuf) {
+        static_assert(NI % NW == 0, "DMA instructions must split evenly over the waves");
         const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
-        for (int ii = 0; ii < NI / 4; ++ii) {
-            const int i = 4 * ii + wave;
+        for (int ii = 0; ii < NI / NW; ++ii) {
+            const int i = NW * ii + wave;
             const int L = 64 * i + lane;
             const int r = L / CPR, pc = L % CPR;
             const int v = min(32 * c + r, V - 1);
@@ -243,98 +238,78 @@ __device__ __forceinline__ void wait_dma_leave() {
     __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
 
-// z for the 16 accumulator entries of a lane: + bias, -inf past V. bias_lds holds the whole (padded) bias.
-__device__ __forceinline__ void logits(const f32x16 &acc, const float *bias_lds, int c, int half, int V,
-                                       float (&z)[16]) {
-#pragma unroll
-    for (int q4 = 0; q4 < 4; ++q4) {
-        const int v0 = 32 * c + 8 * q4 + 4 * half;
-        const f4 bv = *reinterpret_cast<const f4 *>(bias_lds + v0);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) z[4 * q4 + e] = acc[4 * q4 + e] + bv[e];
-    }
-    if (32 * c + 32 > V) {  // only the last chunk can reach past the vocabulary
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-            if (32 * c + (r & 3) + 8 * (r >> 2) + 4 * half >= V) z[r] = NEG_INF_F;
-    }
-}
-
 // index of the accumulator register holding vocabulary offset jj (0..31) of a chunk, or -1 if the other lane
 // half holds it
 __device__ __forceinline__ int acc_reg_of(int jj, int half) {
     return (((jj >> 2) & 1) == half) ? ((jj & 3) + 4 * (jj >> 3)) : -1;
 }
 
-// Chunk pipeline shared by both passes: NB LDS buffers; chunk c's MFMAs run beside the epilogue of chunk c-1
-// (registers only) while the DMAs of chunks c+1 .. c+NB-1 are in flight; one raw s_barrier per chunk (a
-// __syncthreads would drain every DMA with vmcnt(0)).
-template <int KS, int NB, class Epi>
+// x[i] for a per-lane runtime i in [0, 16): a 4-level tree of bit selects (v_bfi_b32 on the bit masks of i;
+// plain ternaries over arrays get rewritten into a scratch-indexed load)
+__device__ __forceinline__ unsigned bsel(unsigned m, float a, float b) {  // m ? b : a, m all-ones or zero
+    return (__float_as_uint(a) & ~m) | (__float_as_uint(b) & m);
+}
+__device__ __forceinline__ float tree_pick(const f2 (&x)[8], int i) {
+    const unsigned m0 = 0u - (unsigned)(i & 1), m1 = 0u - (unsigned)((i >> 1) & 1);
+    const unsigned m2 = 0u - (unsigned)((i >> 2) & 1), m3 = 0u - (unsigned)((i >> 3) & 1);
+    const float a0 = __uint_as_float(bsel(m0, x[0].x, x[0].y)), a1 = __uint_as_float(bsel(m0, x[1].x, x[1].y));
+    const float a2 = __uint_as_float(bsel(m0, x[2].x, x[2].y)), a3 = __uint_as_float(bsel(m0, x[3].x, x[3].y));
+    const float a4 = __uint_as_float(bsel(m0, x[4].x, x[4].y)), a5 = __uint_as_float(bsel(m0, x[5].x, x[5].y));
+    const float a6 = __uint_as_float(bsel(m0, x[6].x, x[6].y)), a7 = __uint_as_float(bsel(m0, x[7].x, x[7].y));
+    const float b0 = __uint_as_float(bsel(m1, a0, a1)), b1 = __uint_as_float(bsel(m1, a2, a3));
+    const float b2 = __uint_as_float(bsel(m1, a4, a5)), b3 = __uint_as_float(bsel(m1, a6, a7));
+    const float c0 = __uint_as_float(bsel(m2, b0, b1)), c1 = __uint_as_float(bsel(m2, b2, b3));
+    return __uint_as_float(bsel(m3, c0, c1));
+}
+
+// z = acc + bias as 8 packed pairs (pair k = registers 2k, 2k+1: vocabulary 32c + (2k&3) + 8(k>>1) + 4 half + {0,1}),
+// -inf past V (only the last chunk can reach past it)
+__device__ __forceinline__ void logits2(const f32x16 &acc, const float *bias_lds, int c, int half, int V, f2 (&z)[8]) {
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+        const f4 bv = *reinterpret_cast<const f4 *>(bias_lds + 32 * c + 8 * q4 + 4 * half);
+        z[2 * q4] = (f2){acc[4 * q4], acc[4 * q4 + 1]} + (f2){bv.x, bv.y};
+        z[2 * q4 + 1] = (f2){acc[4 * q4 + 2], acc[4 * q4 + 3]} + (f2){bv.z, bv.w};
+    }
+    if (32 * c + 32 > V) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int v = 32 * c + ((2 * k) & 3) + 8 * (k >> 1) + 4 * half;
+            if (v >= V) z[k].x = NEG_INF_F;
+            if (v + 1 >= V) z[k].y = NEG_INF_F;
+        }
+    }
+}
+
+// Chunk loop: a workgroup of NW waves (NW = 8: two waves per SIMD, 256 rows) shares each W chunk; NB LDS buffers
+// keep NB - 1 chunk DMAs in flight; one raw s_barrier per chunk. `S` = vector stores the epilogue issues per chunk
+// on every wave (0 forward, 4 backward; -1 = unknown): the wait before chunk c leaves the later DMAs and the
+// stores of the epilogues issued after chunk c's DMA in flight (vector memory completes in issue order).
+// (Staggering the two waves of a SIMD by one epilogue, and three buffers, both measured slower: registers.)
+template <int KS, int NB, int NW, class Epi>
 __device__ __forceinline__ void chunk_loop(const JointArgs &j, int V, unsigned short *wsh, const bf16x8 (&bfr)[KS],
-                                           int lane, Epi &&epi) {
+                                           int lane, int S, Epi &&epi) {
     using WT = WTile<KS>;
-    constexpr int NPW = WT::NI / 4;  // DMA instructions per wave per chunk
+    constexpr int NPW = WT::NI / NW;  // DMA instructions per wave per chunk
     const int nch = (V + 31) / 32;
 #pragma unroll
     for (int c = 0; c < NB - 1; ++c)
-        if (c < nch) WT::stage(j, V, c, wsh + c * WT::ELEMS);
-    auto ready = [&](int c) {  // chunk c landed in LDS for every wave
-        if (c + NB - 2 < nch) wait_dma_leave<(NB - 2) * NPW>();
-        else wait_dma();
-        __builtin_amdgcn_s_barrier();
-    };
-    auto buf = [&](int c) { return wsh + (c % NB) * WT::ELEMS; };
-    ready(0);
-    if (NB - 1 < nch) WT::stage(j, V, NB - 1, buf(NB - 1));
-    f32x16 acc0 = WT::mma(buf(0), bfr, lane), acc1;
-    if (nch > 1) ready(1);
-    // two chunks per trip so the ping-pong accumulators keep fixed registers
-    for (int c = 1;; c += 2) {
-        if (c >= nch) {
-            epi(acc0, c - 1);
-            break;
-        }
-        if (c + NB - 1 < nch) WT::stage(j, V, c + NB - 1, buf(c + NB - 1));
-        acc1 = WT::mma(buf(c), bfr, lane);
-        epi(acc0, c - 1);
-        if (c + 1 >= nch) {
-            epi(acc1, c);
-            break;
-        }
-        ready(c + 1);
-        if (c + NB < nch) WT::stage(j, V, c + NB, buf(c + NB));
-        acc0 = WT::mma(buf(c + 1), bfr, lane);
-        epi(acc1, c);
-        if (c + 2 < nch) ready(c + 2);
-    }
-}
-
-// Simple chunk loop for two workgroups per CU (two waves per SIMD): double-buffered DMA, one accumulator; the
-// partner workgroup's MFMAs cover this one's epilogue and activation build.
-template <int KS, class Epi>
-__device__ __forceinline__ void chunk_loop_simple(const JointArgs &j, int V, unsigned short *wsh,
-                                                  const bf16x8 (&bfr)[KS], int lane, Epi &&epi) {
-    using WT = WTile<KS>;
-    const int nch = (V + 31) / 32;
-    WT::stage(j, V, 0, wsh);
-    wait_dma();
-    __builtin_amdgcn_s_barrier();
+        if (c < nch) WT::template stage<NW>(j, V, c, wsh + c * WT::ELEMS);
     for (int c = 0; c < nch; ++c) {
-        if (c + 1 < nch) WT::stage(j, V, c + 1, wsh + ((c + 1) & 1) * WT::ELEMS);
-        const f32x16 acc = WT::template mma<2>(wsh + (c & 1) * WT::ELEMS, bfr, lane);
-        epi(acc, c);
-        wait_dma();
+        // chunk c in LDS for every wave
+        if (c + NB - 2 < nch && S >= 0) {
+            const int older = min(c, NB - 1);  // epilogues issued after chunk c's DMA
+            if (S == 0 || older == 0) wait_dma_leave<(NB - 2) * NPW>();
+            else if (older == 1) wait_dma_leave<(NB - 2) * NPW + 4>();
+            else wait_dma_leave<(NB - 2) * NPW + 8>();  // NB == 3
+        } else {
+            wait_dma();
+        }
         __builtin_amdgcn_s_barrier();
+        if (c + NB - 1 < nch) WT::template stage<NW>(j, V, c + NB - 1, wsh + ((c + NB - 1) % NB) * WT::ELEMS);
+        const f32x16 acc = WT::template mma<2>(wsh + (c % NB) * WT::ELEMS, bfr, lane);
+        epi(acc, c);
     }
-}
-
-template <int KS, int NB, int OCC, class Epi>
-__device__ __forceinline__ void run_chunks(const JointArgs &j, int V, unsigned short *wsh, const bf16x8 (&bfr)[KS],
-                                           int lane, Epi &&epi) {
-    if constexpr (OCC == 1)
-        chunk_loop<KS, NB>(j, V, wsh, bfr, lane, epi);
-    else
-        chunk_loop_simple<KS>(j, V, wsh, bfr, lane, epi);
 }
 
 // LDS: NB W tiles, then the bias padded to whole chunks
@@ -346,12 +321,13 @@ __device__ __forceinline__ float *load_bias(const JointArgs &j, int V, unsigned 
     return bl;
 }
 
-template <int KS, int NB, int OCC>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void joint_fwd_kernel(DevProblem p,
-                                                                                          JointArgs j) {
+// two waves per SIMD: the compiler keeps each kernel within 256 registers per lane
+template <int KS, int NB, int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2))) void joint_fwd_kernel(DevProblem p,
+                                                                                             JointArgs j) {
     extern __shared__ __attribute__((aligned(16))) unsigned short wsh[];
     const int lane = threadIdx.x & 63, half = lane >> 5;
-    const int64_t i = (int64_t)blockIdx.x * 128 + (threadIdx.x >> 6) * 32 + (lane & 31);
+    const int64_t i = (int64_t)blockIdx.x * (32 * NW) + (threadIdx.x >> 6) * 32 + (lane & 31);
     const RowPos q = row_pos(p, j, i);
     const int V = p.V, blank = p.blank;
     const float *bias = load_bias<KS, NB>(j, V, wsh);
@@ -359,34 +335,43 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     bf16x8 bfr[KS];
     build_act<KS, false>(j, q, half, i, bfr);
 
+    const f2 l2e = {kLog2e, kLog2e};
     float m = NEG_INF_F, sum = 0.0f, zb = 0.0f, ze = 0.0f;
     bool fb = false, fe = false;
-    run_chunks<KS, NB, OCC>(j, V, wsh, bfr, lane, [&](const f32x16 &acc, int c) {
-        float z[16];
-        logits(acc, bias, c, half, V, z);
-        float cm = z[0];
+    chunk_loop<KS, NB, NW>(j, V, wsh, bfr, lane, 0, [&](const f32x16 &acc, int c) {
+        f2 z[8];
+        logits2(acc, bias, c, half, V, z);
+        float cm = fmaxf(z[0].x, z[0].y);
 #pragma unroll
-        for (int r = 1; r < 16; ++r) cm = fmaxf(cm, z[r]);
+        for (int k = 1; k < 8; ++k) cm = fmaxf(cm, fmaxf(z[k].x, z[k].y));
         const float mn = fmaxf(m, cm);
         const float mr = (mn == NEG_INF_F) ? 0.0f : mn;
-        float a = sum * fast_exp2((m - mr) * kLog2e);
+        const f2 nb = {-mr * kLog2e, -mr * kLog2e};
+        f2 s2 = {0.0f, 0.0f};
 #pragma unroll
-        for (int r = 0; r < 16; ++r) a += fast_exp2((z[r] - mr) * kLog2e);
-        sum = a;
+        for (int k = 0; k < 8; ++k) {
+            const f2 t = z[k] * l2e + nb;  // v_pk_fma_f32
+            s2 += (f2){fast_exp2(t.x), fast_exp2(t.y)};
+        }
+        sum = sum * fast_exp2((m - mr) * kLog2e) + (s2.x + s2.y);
         m = mn;
-        const int jb = blank - 32 * c;
+        const int jb = blank - 32 * c;  // wave-uniform: one chunk holds the blank
         if (jb >= 0 && jb < 32) {
             const int rb = acc_reg_of(jb, half);
             if (rb >= 0) {
-                zb = pick_n<16>(z, rb);
+                zb = tree_pick(z, rb);
                 fb = true;
             }
         }
         const int jl = q.lab - 32 * c;
         const int rl = acc_reg_of(jl & 31, half);
-        if (q.lab >= 0 && jl >= 0 && jl < 32 && rl >= 0) {
-            ze = pick_n<16>(z, rl);
-            fe = true;
+        const bool mine = q.lab >= 0 && jl >= 0 && jl < 32 && rl >= 0;
+        if (__ballot(mine)) {  // most chunks hold some lane's label; skip the select when none does
+            const float x = tree_pick(z, rl);
+            if (mine) {
+                ze = x;
+                fe = true;
+            }
         }
     });
     // merge the two lane halves (same row, disjoint vocabulary)
@@ -406,12 +391,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     }
 }
 
-template <int KS, int NB, int OCC>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void joint_bwd_kernel(DevProblem p,
-                                                                                          JointArgs j) {
+template <int KS, int NB, int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2))) void joint_bwd_kernel(DevProblem p,
+                                                                                             JointArgs j) {
     extern __shared__ __attribute__((aligned(16))) unsigned short wsh[];
     const int lane = threadIdx.x & 63, half = lane >> 5;
-    const int64_t i = (int64_t)blockIdx.x * 128 + (threadIdx.x >> 6) * 32 + (lane & 31);
+    const int64_t i = (int64_t)blockIdx.x * (32 * NW) + (threadIdx.x >> 6) * 32 + (lane & 31);
     const RowPos q = row_pos(p, j, i);
     RowCoef rc{0.0f, 0.0f, 0.0f, -1, false};
     float sc = 0.0f;
@@ -427,33 +412,47 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     bf16x8 bfr[KS];
     build_act<KS, true>(j, q, half, i, bfr);
 
+    // exactly 4 vector stores per chunk on every wave with a valid lane: leave them in flight at the barrier
     const bool vec_out = (V & 3) == 0;
+    const bool leave = vec_out && __ballot(!q.valid) == 0;
     unsigned short *grow = j.G + (q.valid ? i : 0) * V;
-    run_chunks<KS, NB, OCC>(j, V, wsh, bfr, lane, [&](const f32x16 &acc, int c) {
-        float z[16];
-        logits(acc, bias, c, half, V, z);
-        float g[16];
+    const f2 l2e = {kLog2e, kLog2e}, c2 = {rc.c2, rc.c2}, sc2 = {sc, sc};
+    chunk_loop<KS, NB, NW>(j, V, wsh, bfr, lane, leave ? 4 : -1, [&](const f32x16 &acc, int c) {
+        f2 g[8];
+        logits2(acc, bias, c, half, V, g);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int v = 32 * c + (r & 3) + 8 * (r >> 2) + 4 * half;
-            float x = fast_exp2(fmaf(z[r], kLog2e, rc.c2));
-            x -= (v == blank ? rc.cb : 0.0f) + (v == rc.lab ? rc.ce : 0.0f);
-            g[r] = x * sc;
+        for (int k = 0; k < 8; ++k) {
+            const f2 t = g[k] * l2e + c2;  // v_pk_fma_f32
+            g[k] = (f2){fast_exp2(t.x), fast_exp2(t.y)};
         }
+        // the <= 2 corrected entries of the row are rewritten by a second (2-byte) store after the vector store
+        const int jb = blank - 32 * c;
+        const int rb = (jb >= 0 && jb < 32) ? acc_reg_of(jb, half) : -1;
+        const int jl = rc.lab - 32 * c;
+        const int rl = acc_reg_of(jl & 31, half);
+        const bool mine = rc.lab >= 0 && jl >= 0 && jl < 32 && rl >= 0;
+        float gb = 0.0f, gl = 0.0f;
+        if (rb >= 0) gb = tree_pick(g, rb);
+        if (__ballot(mine)) gl = tree_pick(g, rl);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) g[k] = g[k] * sc2;  // v_pk_mul_f32
         if (q.valid) {
 #pragma unroll
             for (int qd = 0; qd < 4; ++qd) {
                 const int v0 = 32 * c + 8 * qd + 4 * half;
                 if (vec_out && v0 + 3 < V) {
-                    const unsigned lo = IoBF16::pack2(g[4 * qd], g[4 * qd + 1]);
-                    const unsigned hi = IoBF16::pack2(g[4 * qd + 2], g[4 * qd + 3]);
+                    const unsigned lo = IoBF16::pack2(g[2 * qd].x, g[2 * qd].y);
+                    const unsigned hi = IoBF16::pack2(g[2 * qd + 1].x, g[2 * qd + 1].y);
                     *reinterpret_cast<uint2 *>(grow + v0) = make_uint2(lo, hi);
                 } else {
+                    const float e4[4] = {g[2 * qd].x, g[2 * qd].y, g[2 * qd + 1].x, g[2 * qd + 1].y};
 #pragma unroll
                     for (int e = 0; e < 4; ++e)
-                        if (v0 + e < V) grow[v0 + e] = IoBF16::from_f(g[4 * qd + e]);
+                        if (v0 + e < V) grow[v0 + e] = IoBF16::from_f(e4[e]);
                 }
             }
+            if (rb >= 0) grow[blank] = IoBF16::from_f((gb - rc.cb) * sc);
+            if (mine) grow[rc.lab] = IoBF16::from_f((gl - rc.ce) * sc);
         }
     });
 }
@@ -549,29 +548,28 @@ hipError_t launch_joint_reduce(const DevProblem &p, const JointArgs &j, const in
     return hipGetLastError();
 }
 
-template <int KS, int NB, int OCC>
-static hipError_t launch_knb(const DevProblem &p, const JointArgs &j, bool bwd, size_t lds, hipStream_t stream) {
-    const int64_t blocks = (j.n + 127) / 128;
-    auto kern = bwd ? joint_bwd_kernel<KS, NB, OCC> : joint_fwd_kernel<KS, NB, OCC>;
+template <int KS, int NB, int NW>
+static hipError_t launch_knw(const DevProblem &p, const JointArgs &j, bool bwd, size_t lds, hipStream_t stream) {
+    const int64_t blocks = (j.n + 32 * NW - 1) / (32 * NW);
+    auto kern = bwd ? joint_bwd_kernel<KS, NB, NW> : joint_fwd_kernel<KS, NB, NW>;
     if (lds > 65536) {
         const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    kern<<<(int)blocks, 256, lds, stream>>>(p, j);
+    kern<<<(int)blocks, 64 * NW, lds, stream>>>(p, j);
     return hipGetLastError();
 }
 
-// joint_variant 0: one workgroup per CU, ping-pong accumulators, three LDS buffers when they fit (else two);
-// joint_variant 1: two workgroups per CU (256 registers per lane), double-buffered simple loop
+// One workgroup of 8 waves per CU (two per SIMD, 256 rows sharing each W chunk) with three DMA buffers when they
+// fit beside the bias in the CU's 160 KiB, else two.
 template <int KS>
 static hipError_t launch_kh(const DevProblem &p, const JointArgs &j, bool bwd, hipStream_t stream) {
     const size_t bias = sizeof(float) * ((p.V + 31) / 32 * 32);
     const size_t tile = sizeof(unsigned short) * WTile<KS>::ELEMS;
-    if (tuning().joint_variant == 1 && 2 * (2 * tile + bias) <= 160 * 1024)
-        return launch_knb<KS, 2, 2>(p, j, bwd, 2 * tile + bias, stream);
-    if (3 * tile + bias <= 160 * 1024) return launch_knb<KS, 3, 1>(p, j, bwd, 3 * tile + bias, stream);
-    if (2 * tile + bias <= 160 * 1024) return launch_knb<KS, 2, 1>(p, j, bwd, 2 * tile + bias, stream);
+    if (tuning().joint_nbuf >= 3 && 3 * tile + bias <= 160 * 1024)
+        return launch_knw<KS, 3, 8>(p, j, bwd, 3 * tile + bias, stream);
+    if (2 * tile + bias <= 160 * 1024) return launch_knw<KS, 2, 8>(p, j, bwd, 2 * tile + bias, stream);
     return hipErrorInvalidValue;
 }
 

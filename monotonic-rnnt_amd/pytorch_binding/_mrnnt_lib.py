@@ -71,6 +71,10 @@ class MrnntJointProblem(ctypes.Structure):
         ("pred_stride", ctypes.c_int64),
         ("weight", ctypes.c_void_p),
         ("bias", ctypes.c_void_p),
+        ("alignment", ctypes.c_void_p),
+        ("align_stride", ctypes.c_int64),
+        ("align_blank", ctypes.c_int),
+        ("max_shift", ctypes.c_int),
     ]
 
 

@@ -42,7 +42,8 @@ def _vp(t: Optional[torch.Tensor]):
 
 
 class _JointPrepared:
-    def __init__(self, enc, pred, weight, bias, labels, input_lengths, label_lengths, blank_label):
+    def __init__(self, enc, pred, weight, bias, labels, input_lengths, label_lengths, blank_label, alignment=None,
+                 max_shift=0):
         for name, x in (("enc", enc), ("pred", pred), ("weight", weight)):
             if not x.is_cuda:
                 raise RuntimeError(f"monotonic_rnnt_joint: {name} must be a GPU tensor (no CPU implementation)")
@@ -83,6 +84,12 @@ class _JointPrepared:
         p.pred, p.pred_stride = self.pred.data_ptr(), self.pred.size(1) * H
         p.weight = self.weight.data_ptr()
         p.bias = self.bias.data_ptr() if self.bias is not None else None
+        self.alignment = None
+        if alignment is not None:
+            al = alignment.detach().to(dev, torch.int32)
+            self.alignment = (al.view(B, -1) if al.dim() == 1 else al).contiguous()
+            p.alignment, p.align_stride = self.alignment.data_ptr(), self.alignment.size(1)
+            p.align_blank, p.max_shift = int(blank_label), int(max_shift)
         self.problem = p
         self.device = dev
         self.B, self.V, self.H = B, V, H
@@ -152,8 +159,10 @@ def _split_k_weight_grad(G, Hact, chunks=32):
 
 class MonotonicRNNTJointFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, enc, pred, weight, bias, labels, input_lengths, label_lengths, blank_label=0):
-        prep = _JointPrepared(enc, pred, weight, bias, labels, input_lengths, label_lengths, blank_label)
+    def forward(ctx, enc, pred, weight, bias, labels, input_lengths, label_lengths, blank_label=0, alignment=None,
+                max_distance_from_alignment=0):
+        prep = _JointPrepared(enc, pred, weight, bias, labels, input_lengths, label_lengths, blank_label, alignment,
+                              max_distance_from_alignment)
         need = any(ctx.needs_input_grad[:4])
         costs, ws = prep.forward(with_beta=need)
         if need:
@@ -177,16 +186,19 @@ class MonotonicRNNTJointFunction(torch.autograd.Function):
             d_enc, d_pred = prep.reduce(ws, dH, Hact, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
             d_enc = None if d_enc is None else d_enc.to(prep.enc.dtype)
             d_pred = None if d_pred is None else d_pred.to(prep.pred.dtype)
-        return d_enc, d_pred, d_w, d_b, None, None, None, None
+        return d_enc, d_pred, d_w, d_b, None, None, None, None, None, None
 
 
 def monotonic_rnnt_joint_loss(enc: torch.Tensor, pred: torch.Tensor, weight: torch.Tensor,
                               bias: Optional[torch.Tensor], labels: torch.Tensor, input_lengths: torch.Tensor,
-                              label_lengths: torch.Tensor, blank_label: int = 0) -> torch.Tensor:
-    """Monotonic RNN-T loss of the joint network tanh(enc + pred) @ weight.T + bias, fused (see module doc)."""
+                              label_lengths: torch.Tensor, blank_label: int = 0,
+                              alignment: Optional[torch.Tensor] = None,
+                              max_distance_from_alignment: int = 0) -> torch.Tensor:
+    """Monotonic RNN-T loss of the joint network tanh(enc + pred) @ weight.T + bias, fused (see module doc).
+    alignment / max_distance_from_alignment restrict the paths as in monotonic_rnnt_loss."""
     cast = lambda x: x if x is None or x.dtype == torch.bfloat16 else x.to(torch.bfloat16)  # noqa: E731
     return MonotonicRNNTJointFunction.apply(cast(enc), cast(pred), cast(weight), bias, labels, input_lengths,
-                                            label_lengths, blank_label)
+                                            label_lengths, blank_label, alignment, max_distance_from_alignment)
 
 
 __all__ = ["MonotonicRNNTJointFunction", "monotonic_rnnt_joint_loss"]

@@ -45,7 +45,7 @@ def make_case(seed, B, Trange, Smax, H, V, scale_in=1.0):
     return enc, pred, w, bias, labels, T, S
 
 
-def host_reference(enc, pred, w, bias, labels, T, S, blank=0, scale=None):
+def host_reference(enc, pred, w, bias, labels, T, S, blank=0, scale=None, alignment=None, k=0):
     B = len(T)
     W64 = w.double()
     hs, rows = [], []
@@ -56,7 +56,7 @@ def host_reference(enc, pred, w, bias, labels, T, S, blank=0, scale=None):
         hs.append(h)
         rows.append((h @ W64.T + bias.double()).reshape(-1, w.shape[0]))
     acts = torch.cat(rows).float().numpy()
-    costs, dz = O.oracle_rnnt(acts, labels, T, S, blank=blank, num_threads=4)
+    costs, dz = O.oracle_rnnt(acts, labels, T, S, blank=blank, alignment=alignment, max_shift=k, num_threads=4)
     if scale is not None:
         dz = dz * np.repeat(np.asarray(scale, np.float64), T * (S + 1))[:, None]
     dz = torch.from_numpy(dz)
@@ -84,13 +84,14 @@ def close(x, ref, rel=1.5e-2, name=""):
     assert err <= lim, (name, err, lim)
 
 
-def run_joint(jop, dev, enc, pred, w, bias, labels, T, S, blank=0, scale=None):
+def run_joint(jop, dev, enc, pred, w, bias, labels, T, S, blank=0, scale=None, alignment=None, k=0):
     e = enc.to(dev).requires_grad_(True)
     p = pred.to(dev).requires_grad_(True)
     ww = w.to(dev).requires_grad_(True)
     bb = bias.to(dev).requires_grad_(True)
+    al = None if alignment is None else torch.from_numpy(alignment).to(dev)
     costs = jop.monotonic_rnnt_joint_loss(e, p, ww, bb, torch.from_numpy(labels).to(dev), torch.from_numpy(T),
-                                          torch.from_numpy(S), blank)
+                                          torch.from_numpy(S), blank, al, k)
     sc = torch.ones(len(T), device=dev) if scale is None else torch.tensor(scale, dtype=torch.float32, device=dev)
     (costs * sc).sum().backward()
     torch.cuda.synchronize()
@@ -146,3 +147,21 @@ def test_joint_matches_materialised_acts_path(jop, dev):
     c_acts = op.monotonic_rnnt_loss(acts, torch.from_numpy(labels).to(dev), torch.from_numpy(T),
                                     torch.from_numpy(S)).cpu().double().numpy()
     assert np.all(np.abs(c_fused - c_acts) <= 1e-3 * np.maximum(1.0, np.abs(c_acts))), (c_fused, c_acts)
+
+
+@pytest.mark.parametrize("k", [0, 2])
+def test_joint_alignment_restricted(jop, dev, k):
+    """alignment / max_distance_from_alignment on the fused path, against the oracle's restricted loss."""
+    H, V = 256, 64
+    enc, pred, w, bias, labels, T, S = make_case(50 + k, 3, (10, 40), 8, H, V)
+    rng = np.random.default_rng(k)
+    al = np.zeros((3, int(T.max())), np.int32)
+    for b in range(3):
+        al[b, np.sort(rng.choice(T[b], S[b], replace=False))] = labels[b, : S[b]]
+    c, de, dp, dw, db = run_joint(jop, dev, enc, pred, w, bias, labels, T, S, alignment=al, k=k)
+    cr, de_r, dp_r, dw_r, db_r = host_reference(enc, pred, w, bias, labels, T, S, alignment=al, k=k)
+    assert np.all(np.abs(c - cr) <= 1e-5 * np.maximum(1.0, np.abs(cr))), (c, cr)
+    close(de, de_r, name="d_enc")
+    close(dp, dp_r, name="d_pred")
+    close(dw, dw_r, name="d_weight")
+    close(db, db_r, name="d_bias")
