@@ -70,6 +70,8 @@ def main():
     ap.add_argument("--config", default="headline", choices=["headline", "c2", "ragged", "ragged64", "c5"])
     ap.add_argument("--cpu-sample", type=int, default=8, help="utterances in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--acts-dtype", default="f32", choices=["f32", "bf16", "f16"],
+                    help="element type of acts/grads (extension; the headline metric is f32, the reference's type)")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
                     help="launch knob for experiments (mrnnt_tune); the defaults are the tuned values")
     ap.add_argument("--dist-backend", default="nccl",
@@ -116,6 +118,10 @@ def main():
     stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     acts = torch.empty((rows, V), dtype=torch.float32, device=dev)
     L.check(lib.mrnnt_synth_acts(ctypes.c_void_p(acts.data_ptr()), row0 * V, rows * V, 0, 1, stream), "synth")
+    elem = {"f32": 4, "bf16": 2, "f16": 2}[args.acts_dtype]
+    if args.acts_dtype != "f32":
+        acts = acts.to(torch.bfloat16 if args.acts_dtype == "bf16" else torch.float16)
+        torch.cuda.empty_cache()
     rng = np.random.default_rng(1 + rank)
     labels = torch.from_numpy(rng.integers(1, V, (B, max(1, int(S.max())))).astype(np.int32)).to(dev)
     T_t = torch.from_numpy(T)
@@ -163,10 +169,10 @@ def main():
     # live rows: in-band rows whose gradient is not exactly zero in fp32 -- the only acts rows the gradient
     # kernel reads (occupancy skip); counted once after the timed region
     live = live_rows(op, L, acts, labels, T_t, S_t, dev)
-    grad_bytes = (live + rows) * V * 4  # algorithmic: read live acts rows once, write every grads row once
-    formula_grad_bytes = (n_band + rows) * V * 4  # SURVEY.md §8d formula: every in-band row read
-    softmax_bytes = n_band * V * 4
-    step_bytes = (n_band + live + rows) * V * 4
+    grad_bytes = (live + rows) * V * elem  # algorithmic: read live acts rows once, write every grads row once
+    formula_grad_bytes = (n_band + rows) * V * elem  # SURVEY.md §8d formula: every in-band row read
+    softmax_bytes = n_band * V * elem
+    step_bytes = (n_band + live + rows) * V * elem
 
     def avg_ms(name):
         ms, n = prof[name]
@@ -190,7 +196,7 @@ def main():
             traffic = None
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu and args.cpu_sample > 0:
+    if rank == 0 and world == 1 and not args.no_cpu and args.cpu_sample > 0 and args.acts_dtype == "f32":
         cpu = cpu_baseline(lib, L, acts, labels, T, S, V, args.cpu_sample, stream)
 
     if rank == 0:
@@ -205,7 +211,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": args.acts_dtype,
             "data": "synthetic: counter-hash N(0,1)-like acts (seed 0), labels U[1,V-1] (seed 1+rank); inputs resident in HBM",
             "config": {"workload": workload, "utterances_per_gpu": B, "global_batch": total_utts,
                        "rows_per_gpu": rows, "inband_rows_per_gpu": n_band, "V": V,

@@ -49,7 +49,7 @@ struct Plan {
     int elem = ELEM_F32;
     int64_t pad_T = 0, pad_S1 = 0;
     bool align = false;
-    size_t off_row, off_col, off_mtmp, off_min, off_max, off_den, off_lpb, off_lpe, off_alpha, off_beta, off_ll,
+    size_t off_row, off_col, off_colb, off_mtmp, off_min, off_max, off_den, off_lpb, off_lpe, off_alpha, off_beta, off_ll,
         off_llb, total;
 };
 
@@ -103,6 +103,7 @@ RNNTStatus make_plan(const mrnnt_problem *p, Plan *pl) {
     };
     q.off_row = take(sizeof(int64_t) * (q.B + 1));
     q.off_col = take(sizeof(int64_t) * (q.B + 1));
+    q.off_colb = take(sizeof(int) * q.cols);
     q.off_mtmp = q.align ? take(sizeof(int) * (q.cols + q.B)) : 0;
     q.off_min = q.align ? take(sizeof(int) * q.cols) : 0;
     q.off_max = q.align ? take(sizeof(int) * q.cols) : 0;
@@ -128,6 +129,7 @@ DevProblem make_dev(const mrnnt_problem *p, const Plan &pl, const void *ws) {
     d.S = p->S_dev;
     d.row_off = reinterpret_cast<const int64_t *>(w + pl.off_row);
     d.col_off = reinterpret_cast<const int64_t *>(w + pl.off_col);
+    d.col_b = reinterpret_cast<const int *>(w + pl.off_colb);
     d.min_s = pl.align ? reinterpret_cast<const int *>(w + pl.off_min) : nullptr;
     d.max_s = pl.align ? reinterpret_cast<const int *>(w + pl.off_max) : nullptr;
     d.B = pl.B;
@@ -233,7 +235,8 @@ RNNTStatus mrnnt_forward(const mrnnt_problem *p, void *ws, size_t ws_bytes, floa
     hipError_t e;
     e = timed(K_SETUP, stream, [&] {
         return launch_setup(p->T_dev, p->S_dev, pl.B, reinterpret_cast<int64_t *>(w + pl.off_row),
-                            reinterpret_cast<int64_t *>(w + pl.off_col), stream);
+                            reinterpret_cast<int64_t *>(w + pl.off_col),
+                            reinterpret_cast<int *>(w + pl.off_colb), stream);
     });
     if (e != hipSuccess) return fail_hip(e, "setup kernel");
     if (pl.align) {
@@ -428,7 +431,8 @@ RNNTStatus mrnnt_joint_forward(const mrnnt_joint_problem *jp, void *ws, size_t w
     char *w = static_cast<char *>(ws);
     hipError_t e = timed(K_SETUP, stream, [&] {
         return launch_setup(jp->T_dev, jp->S_dev, pl.B, reinterpret_cast<int64_t *>(w + pl.off_row),
-                            reinterpret_cast<int64_t *>(w + pl.off_col), stream);
+                            reinterpret_cast<int64_t *>(w + pl.off_col),
+                            reinterpret_cast<int *>(w + pl.off_colb), stream);
     });
     if (e != hipSuccess) return fail_hip(e, "setup kernel");
     if (pl.align) {

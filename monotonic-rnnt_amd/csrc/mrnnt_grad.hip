@@ -46,7 +46,7 @@ __global__ __launch_bounds__(256) void grad_kernel(DevProblem p, const float *__
     Vec *__restrict__ gv = reinterpret_cast<Vec *>(grads);
 
     Cursor cur;
-    cur.init(p.col_off, p.B, blockIdx.x);
+    cur.b = blockIdx.x < p.num_cols ? p.col_b[blockIdx.x] : 0;
     for (int64_t c = blockIdx.x; c < p.num_cols; c += gridDim.x) {
         cur.advance(p.col_off, c);
         const int b = cur.b;
@@ -163,7 +163,7 @@ __global__ __launch_bounds__(256) void grad_scalar_kernel(DevProblem p, const fl
     const Sc *__restrict__ acts = reinterpret_cast<const Sc *>(p.acts);
     Sc *__restrict__ gs = reinterpret_cast<Sc *>(grads);
     Cursor cur;
-    cur.init(p.col_off, p.B, blockIdx.x);
+    cur.b = blockIdx.x < p.num_cols ? p.col_b[blockIdx.x] : 0;
     for (int64_t c = blockIdx.x; c < p.num_cols; c += gridDim.x) {
         cur.advance(p.col_off, c);
         const int b = cur.b;
@@ -203,7 +203,7 @@ __global__ __launch_bounds__(256) void count_live_kernel(DevProblem p, unsigned 
     __shared__ unsigned long long part[4];
     unsigned long long n = 0;
     Cursor cur;
-    cur.init(p.col_off, p.B, blockIdx.x);
+    cur.b = blockIdx.x < p.num_cols ? p.col_b[blockIdx.x] : 0;
     for (int64_t c = blockIdx.x; c < p.num_cols; c += gridDim.x) {
         cur.advance(p.col_off, c);
         const int b = cur.b;

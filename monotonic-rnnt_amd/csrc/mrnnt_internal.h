@@ -22,6 +22,7 @@ struct DevProblem {
     const int *S;               // [B]
     const int64_t *row_off;     // [B+1] (workspace, built by the setup kernel)
     const int64_t *col_off;     // [B+1]
+    const int *col_b;           // [cols] utterance of each lattice column (setup kernel)
     const int *min_s;           // [cols] alignment band (nullptr = unrestricted)
     const int *max_s;           // [cols]
     int B, V, blank;
@@ -85,7 +86,8 @@ Tuning &tuning();
 enum KernelId { K_BAND = 0, K_SOFTMAX = 1, K_DP = 2, K_GRAD = 3, K_SETUP = 4, K_JOINT_FWD = 5, K_JOINT_BWD = 6,
                 K_JOINT_RED = 7, K_COUNT = 8 };
 
-hipError_t launch_setup(const int *T, const int *S, int B, int64_t *row_off, int64_t *col_off, hipStream_t stream);
+hipError_t launch_setup(const int *T, const int *S, int B, int64_t *row_off, int64_t *col_off, int *col_b,
+                        hipStream_t stream);
 hipError_t launch_align(const DevProblem &p, const int *alignment, int64_t align_stride, int align_blank,
                         int max_shift, int *mtmp, int *min_s, int *max_s, hipStream_t stream);
 hipError_t launch_softmax(const DevProblem &p, int elem, int grid, hipStream_t stream);

@@ -52,9 +52,7 @@ __global__ __launch_bounds__(256) void row_list_kernel(DevProblem p, int mode, i
     const int lane = threadIdx.x & 63;
     const int64_t col = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (col >= p.num_cols) return;
-    Cursor cur;
-    cur.init(p.col_off, p.B, col);
-    const int b = cur.b;
+    const int b = p.col_b[col];
     const int T = p.T[b], S = p.S[b], W = S + 1;
     const int t = (int)(col - p.col_off[b]);
     const int64_t rowc = p.row_off[b] + (int64_t)t * W;
@@ -135,9 +133,7 @@ __device__ __forceinline__ RowPos row_pos(const DevProblem &p, const JointArgs &
     if (i >= j.n) return q;
     const int col = j.lcol[i];
     q.s = j.ls[i];
-    Cursor c;
-    c.init(p.col_off, p.B, col);
-    q.b = c.b;
+    q.b = p.col_b[col];
     q.t = (int)(col - p.col_off[q.b]);
     q.T = p.T[q.b];
     q.S = p.S[q.b];

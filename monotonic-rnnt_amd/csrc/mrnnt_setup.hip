@@ -108,8 +108,20 @@ __global__ __launch_bounds__(256) void synth_kernel(float *__restrict__ out, int
     }
 }
 
-hipError_t launch_setup(const int *T, const int *S, int B, int64_t *row_off, int64_t *col_off, hipStream_t stream) {
+// col_b[c] = utterance of lattice column c: one load instead of a binary search over col_off per workgroup
+__global__ __launch_bounds__(256) void col_map_kernel(const int *__restrict__ T, const int64_t *__restrict__ col_off,
+                                                      int *__restrict__ col_b) {
+    const int b = blockIdx.x;
+    const int64_t c0 = col_off[b];
+    for (int t = threadIdx.x; t < T[b]; t += blockDim.x) col_b[c0 + t] = b;
+}
+
+hipError_t launch_setup(const int *T, const int *S, int B, int64_t *row_off, int64_t *col_off, int *col_b,
+                        hipStream_t stream) {
     setup_kernel<<<1, 64, 0, stream>>>(T, S, B, row_off, col_off);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    col_map_kernel<<<B, 256, 0, stream>>>(T, col_off, col_b);
     return hipGetLastError();
 }
 

@@ -42,11 +42,8 @@ __global__ __launch_bounds__(64 * NW) void softmax_kernel(DevProblem p) {
     const int bj = blank / E, bc = blank % E, blane = bj & 63;
     const Vec ninf = splat<IO>(NEG_INF_F);
 
-    Cursor cur;
-    cur.init(p.col_off, p.B, blockIdx.x);
     for (int64_t c = blockIdx.x; c < p.num_cols; c += gridDim.x) {
-        cur.advance(p.col_off, c);
-        const int b = cur.b;
+        const int b = p.col_b[c];
         const int T = p.T[b], S = p.S[b];
         const int t = (int)(c - p.col_off[b]);
         const int64_t rowc = p.row_off[b] + (int64_t)t * (S + 1);
@@ -128,11 +125,8 @@ __global__ __launch_bounds__(256) void softmax_scalar_kernel(DevProblem p) {
     const int V = p.V;
     const int blank = p.blank;
     const Sc *__restrict__ acts = reinterpret_cast<const Sc *>(p.acts);
-    Cursor cur;
-    cur.init(p.col_off, p.B, blockIdx.x);
     for (int64_t c = blockIdx.x; c < p.num_cols; c += gridDim.x) {
-        cur.advance(p.col_off, c);
-        const int b = cur.b;
+        const int b = p.col_b[c];
         const int T = p.T[b], S = p.S[b];
         const int t = (int)(c - p.col_off[b]);
         const int64_t rowc = p.row_off[b] + (int64_t)t * (S + 1);
@@ -184,8 +178,10 @@ static void launch_vec(const DevProblem &p, int grid, hipStream_t stream) {
             case 7: softmax_kernel<IO, 2, 4, NTL><<<grid, 256, 0, stream>>>(p); break;
             default: softmax_kernel<IO, 4, 2, NTL><<<grid, 256, 0, stream>>>(p); break;
         }
-    } else if (VL >= 96) {
-        softmax_kernel<IO, 2, 2, NTL><<<grid, 256, 0, stream>>>(p);
+    } else if (VL >= 96) {  // e.g. V = 1024 in bf16: 2 KiB rows
+        if (v == 4) softmax_kernel<IO, 2, 4, NTL><<<grid, 256, 0, stream>>>(p);
+        else if (v == 3) softmax_kernel<IO, 2, 3, NTL><<<grid, 256, 0, stream>>>(p);
+        else softmax_kernel<IO, 2, 2, NTL><<<grid, 256, 0, stream>>>(p);
     } else {
         softmax_kernel<IO, 1, 4, NTL><<<grid, 256, 0, stream>>>(p);
     }
