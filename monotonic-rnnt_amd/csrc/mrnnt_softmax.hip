@@ -30,8 +30,8 @@ __device__ __forceinline__ void write_row(const DevProblem &p, int64_t row, floa
 
 // Vector path: V % E == 0, 16-byte aligned rows. U = vector loads per lane per chunk (a chunk covers
 // 64*U*E elements), R = rows a wave reduces at once (U*R vector loads in flight per lane).
-template <class IO, int U, int R, bool NTL, int NW = 4>
-__global__ __launch_bounds__(64 * NW) void softmax_kernel(DevProblem p) {
+template <class IO, int U, int R, bool NTL, int NW = 4, int OCC = 1>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(OCC))) void softmax_kernel(DevProblem p) {
     constexpr int E = IO::E;
     typedef typename IO::V Vec;
     const int lane = threadIdx.x & 63;
@@ -176,12 +176,17 @@ static void launch_vec(const DevProblem &p, int grid, hipStream_t stream) {
             case 5: softmax_kernel<IO, 4, 2, NTL, 8><<<grid, 512, 0, stream>>>(p); break;
             case 6: softmax_kernel<IO, 4, 1, NTL, 8><<<grid, 512, 0, stream>>>(p); break;
             case 7: softmax_kernel<IO, 2, 4, NTL><<<grid, 256, 0, stream>>>(p); break;
+            case 8: softmax_kernel<IO, 4, 1, NTL, 4, 8><<<grid, 256, 0, stream>>>(p); break;
+            case 9: softmax_kernel<IO, 4, 2, NTL, 4, 6><<<grid, 256, 0, stream>>>(p); break;
+            case 10: softmax_kernel<IO, 2, 2, NTL, 4, 8><<<grid, 256, 0, stream>>>(p); break;
             default: softmax_kernel<IO, 4, 2, NTL><<<grid, 256, 0, stream>>>(p); break;
         }
     } else if (VL >= 96) {  // e.g. V = 1024 in bf16: 2 KiB rows
+        // default: one row per wave at 8 waves per SIMD (bf16 V = 1024: 3 % over two rows at 4 waves)
         if (v == 4) softmax_kernel<IO, 2, 4, NTL><<<grid, 256, 0, stream>>>(p);
         else if (v == 3) softmax_kernel<IO, 2, 3, NTL><<<grid, 256, 0, stream>>>(p);
-        else softmax_kernel<IO, 2, 2, NTL><<<grid, 256, 0, stream>>>(p);
+        else if (v == 0) softmax_kernel<IO, 2, 2, NTL><<<grid, 256, 0, stream>>>(p);
+        else softmax_kernel<IO, 2, 1, NTL, 4, 8><<<grid, 256, 0, stream>>>(p);
     } else {
         softmax_kernel<IO, 1, 4, NTL><<<grid, 256, 0, stream>>>(p);
     }
