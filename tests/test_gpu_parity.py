@@ -118,7 +118,7 @@ def test_out_of_band_rows_are_exact_zero(op, dev):
 # ---------------------------------------------------------------------------------------------
 # random problems vs the oracle
 
-@pytest.mark.parametrize("V", [3, 15, 16, 64, 100, 256, 1000, 1001, 1024, 2052])
+@pytest.mark.parametrize("V", [3, 15, 16, 64, 100, 256, 512, 600, 1000, 1001, 1024, 2052])
 def test_random_ragged_vs_oracle(op, dev, V):
     rng = np.random.default_rng(V)
     acts, labels, T, S = random_problem(rng, 5, (1, 40), 12, V, force={0: (1, 0), 1: (9, 9), 2: (17, 0)})
