@@ -34,7 +34,9 @@ __device__ __forceinline__ typename IO::V grad_vec(const typename IO::V &xv, con
 
 // Column-walking kernel (grad_variant 0 / 2): workgroups walk lattice columns, the four waves take rows
 // s (R at a time), lanes take 16-byte vectors of the row, U per lane per chunk.
-template <class IO, int U, int R, bool NTL, bool NTS>
+// MODE 0: every row of the column; 1: only the rows whose gradient is zero (out of band or dead: a pure write
+// stream); 2: only the live rows (a copy-shaped stream). grad_variant 4 runs 1 then 2.
+template <class IO, int U, int R, bool NTL, bool NTS, int MODE = 0>
 __global__ __launch_bounds__(256) void grad_kernel(DevProblem p, const float *__restrict__ scale,
                                                        void *__restrict__ grads) {
     typedef typename IO::V Vec;
@@ -69,7 +71,11 @@ __global__ __launch_bounds__(256) void grad_kernel(DevProblem p, const float *__
                 const int sr = s + r;
                 ok[r] = sr <= S;
                 inb[r] = ok[r] && sr >= lo && sr <= hi;
-                if (inb[r]) {
+                if (MODE == 1) {  // liveness only
+                    if (inb[r]) inb[r] = !p.occ_skip || row_live(alpha_prev(p, t, sr, rowc + sr, S + 1) - ll +
+                                                                 p.beta[rowc + sr]);
+                    rc[r] = RowCoef{0.0f, 0.0f, 0.0f, -1, false};
+                } else if (inb[r]) {
                     rc[r] = row_coef(p, t, T, S, sr, rowc + sr, ll, lab_b);
                     inb[r] = rc[r].live;  // dead rows are stored like out-of-band rows
                 } else {
@@ -83,7 +89,7 @@ __global__ __launch_bounds__(256) void grad_kernel(DevProblem p, const float *__
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
                         const int j = base + lane + 64 * u;
-                        if (inb[r] && j < VL) x[r][u] = vload<NTL>(&av[(arow + s + r) * (int64_t)VL + j]);
+                        if (MODE != 1 && inb[r] && j < VL) x[r][u] = vload<NTL>(&av[(arow + s + r) * (int64_t)VL + j]);
                     }
 #pragma unroll
                 for (int r = 0; r < R; ++r)
@@ -91,7 +97,8 @@ __global__ __launch_bounds__(256) void grad_kernel(DevProblem p, const float *__
                     for (int u = 0; u < U; ++u) {
                         const int j = base + lane + 64 * u;
                         if (!ok[r] || j >= VL) continue;
-                        const Vec g = inb[r] ? grad_vec<IO>(x[r][u], rc[r], j, blank, sc) : zv;
+                        if ((MODE == 1 && inb[r]) || (MODE == 2 && !inb[r])) continue;
+                        const Vec g = (MODE != 1 && inb[r]) ? grad_vec<IO>(x[r][u], rc[r], j, blank, sc) : zv;
                         vstore<NTS>(&gv[(arow + s + r) * (int64_t)VL + j], g);
                     }
             }
@@ -273,7 +280,10 @@ template <class IO, bool NTL, bool NTS>
 static void launch_vec(const DevProblem &p, const float *scale, void *grads, int grid, hipStream_t stream) {
     const int VL = p.V / IO::E;
     const int variant = tuning().grad_variant;
-    if (variant == 3 && p.pad_S1 == 0 && VL >= 192)
+    if (variant == 4 && VL >= 192) {
+        grad_kernel<IO, 4, 1, NTL, NTS, 1><<<grid, 256, 0, stream>>>(p, scale, grads);
+        grad_kernel<IO, 4, 1, NTL, NTS, 2><<<grid, 256, 0, stream>>>(p, scale, grads);
+    } else if (variant == 3 && p.pad_S1 == 0 && VL >= 192)
         grad_rows_kernel<IO, 4, NTL, NTS><<<grid, 256, 0, stream>>>(p, scale, grads);
     else if (VL >= 192 && variant == 2)
         grad_kernel<IO, 4, 2, NTL, NTS><<<grid, 256, 0, stream>>>(p, scale, grads);

@@ -258,23 +258,21 @@ __device__ __forceinline__ float tree_pick(const f2 (&x)[8], int i) {
     return __uint_as_float(bsel(m3, c0, c1));
 }
 
-// z = acc + bias as 8 packed pairs (pair k = registers 2k, 2k+1: vocabulary 32c + (2k&3) + 8(k>>1) + 4 half + {0,1}),
-// -inf past V (only the last chunk can reach past it)
-__device__ __forceinline__ void logits2(const f32x16 &acc, const float *bias_lds, int c, int half, int V, f2 (&z)[8]) {
+// z = acc + bias as 8 packed pairs (pair k = registers 2k, 2k+1: vocabulary 32c + (2k&3) + 8(k>>1) + 4 half + {0,1});
+// entries past V come out -inf through the padded bias
+__device__ __forceinline__ void logits2(const f32x16 &acc, const float *bias_lds, int c, int half, f2 (&z)[8]) {
 #pragma unroll
     for (int q4 = 0; q4 < 4; ++q4) {
         const f4 bv = *reinterpret_cast<const f4 *>(bias_lds + 32 * c + 8 * q4 + 4 * half);
         z[2 * q4] = (f2){acc[4 * q4], acc[4 * q4 + 1]} + (f2){bv.x, bv.y};
         z[2 * q4 + 1] = (f2){acc[4 * q4 + 2], acc[4 * q4 + 3]} + (f2){bv.z, bv.w};
     }
-    if (32 * c + 32 > V) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int v = 32 * c + ((2 * k) & 3) + 8 * (k >> 1) + 4 * half;
-            if (v >= V) z[k].x = NEG_INF_F;
-            if (v + 1 >= V) z[k].y = NEG_INF_F;
-        }
-    }
+}
+
+__device__ __forceinline__ float max3(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
 }
 
 // Chunk loop: a workgroup of NW waves (NW = 8: two waves per SIMD, 256 rows) shares each W chunk; NB LDS buffers
@@ -313,7 +311,8 @@ template <int KS, int NB>
 __device__ __forceinline__ float *load_bias(const JointArgs &j, int V, unsigned short *wsh) {
     float *bl = reinterpret_cast<float *>(wsh + NB * WTile<KS>::ELEMS);
     const int nb = (V + 31) / 32 * 32;
-    for (int v = threadIdx.x; v < nb; v += blockDim.x) bl[v] = (v < V && j.bias) ? j.bias[v] : 0.0f;
+    // past V: -inf, so z = acc + bias masks the tail chunk without a compare (the clamped W rows are finite)
+    for (int v = threadIdx.x; v < nb; v += blockDim.x) bl[v] = v < V ? (j.bias ? j.bias[v] : 0.0f) : NEG_INF_F;
     return bl;
 }
 
@@ -336,10 +335,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     bool fb = false, fe = false;
     chunk_loop<KS, NB, NW>(j, V, wsh, bfr, lane, 0, [&](const f32x16 &acc, int c) {
         f2 z[8];
-        logits2(acc, bias, c, half, V, z);
+        logits2(acc, bias, c, half, z);
         float cm = fmaxf(z[0].x, z[0].y);
 #pragma unroll
-        for (int k = 1; k < 8; ++k) cm = fmaxf(cm, fmaxf(z[k].x, z[k].y));
+        for (int k = 1; k < 8; ++k) cm = max3(cm, z[k].x, z[k].y);
         const float mn = fmaxf(m, cm);
         const float mr = (mn == NEG_INF_F) ? 0.0f : mn;
         const f2 nb = {-mr * kLog2e, -mr * kLog2e};
@@ -415,7 +414,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const f2 l2e = {kLog2e, kLog2e}, c2 = {rc.c2, rc.c2}, sc2 = {sc, sc};
     chunk_loop<KS, NB, NW>(j, V, wsh, bfr, lane, leave ? 4 : -1, [&](const f32x16 &acc, int c) {
         f2 g[8];
-        logits2(acc, bias, c, half, V, g);
+        logits2(acc, bias, c, half, g);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const f2 t = g[k] * l2e + c2;  // v_pk_fma_f32
