@@ -436,3 +436,23 @@ def test_occupancy_skip_is_bit_identical(op, dev, grad_variant):
     finally:
         L.tune("occ_skip", saved_skip)
         L.tune("grad_variant", saved_var)
+
+
+@pytest.mark.parametrize("B,T,S,V", [(1, 150, 20, 50), (1, 150, 20, 5000), (16, 150, 20, 50), (16, 150, 20, 5000),
+                                     (2, 391, 300, 79)])
+def test_reference_size_cases_vs_oracle(op, dev, B, T, S, V):
+    """The shape list of the reference's size tests (tensorflow_binding/test.py:159-176: uniform [0,1) acts like
+    tests/random.cpp:4-20, labels U[1, V-1] with a forced repeat at S/2 like tests/random.cpp:22-37), here
+    checked against the oracle rather than only for inf/NaN."""
+    rng = np.random.default_rng(B * 1000 + S)
+    Tn = np.full(B, T, np.int32)
+    Sn = np.full(B, S, np.int32)
+    rows = int(np.sum(Tn * (Sn + 1)))
+    acts = rng.random((rows, V), dtype=np.float32)
+    labels = rng.integers(1, V, (B, S)).astype(np.int32)
+    labels[:, S // 2] = labels[:, S // 2 - 1]
+    c, g = run_gpu(op, dev, acts, labels, Tn, Sn)
+    assert np.all(np.isfinite(c)) and np.all(np.isfinite(g))
+    cr, gr = O.oracle_rnnt(acts, labels, Tn, Sn, num_threads=8)
+    assert_costs(c, cr)
+    assert_grads(g, gr)
