@@ -197,6 +197,8 @@ def main():
         except Exception:
             traffic = None
 
+    copy_gbps = box_copy_gbps(dev)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_sample > 0 and args.acts_dtype == "f32":
         cpu = cpu_baseline(lib, L, acts, labels, T, S, V, args.cpu_sample, stream, args.cpu_threads)
@@ -227,7 +229,9 @@ def main():
                          "avg_launch_ms": round(g_ms, 4) if g_ms else None,
                          "live_rows": live, "inband_rows": n_band,
                          "formula_bytes_per_launch": formula_grad_bytes,
-                         "formula_gbps": round(formula_grad_bytes / (g_ms * 1e-3) / 1e9, 1) if g_ms else None},
+                         "formula_gbps": round(formula_grad_bytes / (g_ms * 1e-3) / 1e9, 1) if g_ms else None,
+                         "box_copy_gbps": copy_gbps,
+                         "frac_of_box_copy": round(achieved / copy_gbps, 4) if achieved and copy_gbps else None},
             "kernels": {
                 "log_softmax": {"avg_ms": round(s_ms, 4) if s_ms else None,
                                 "gbps": round(softmax_bytes / (s_ms * 1e-3) / 1e9, 1) if s_ms else None},
@@ -242,6 +246,28 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def box_copy_gbps(dev, gib=4, reps=5):
+    """Device-to-device copy rate of this box (torch copy_, read + write bytes / time): HBM rates differ by up
+    to ~15 % between MI355X boxes of the pool (profiles/r01/membench_ceilings*.json), so the gradient kernel's
+    rate is also reported against what a plain copy reaches on the same card. None if memory is short."""
+    n = gib << 30
+    if torch.cuda.mem_get_info(dev)[0] < 2 * n + (4 << 30):
+        return None
+    src = torch.empty(n, dtype=torch.uint8, device=dev)
+    dst = torch.empty_like(src)
+    dst.copy_(src)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        dst.copy_(src)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    del src, dst
+    torch.cuda.empty_cache()
+    return round(2 * n / (ms * 1e-3) / 1e9, 1)
 
 
 def live_rows(op, L, acts, labels, T, S, dev):
@@ -283,10 +309,9 @@ def cpu_baseline(lib, L, acts, labels, T, S, V, n_sample, stream, max_threads=16
         finite = finite and bool(np.all(np.isfinite(costs)))
     dt = time.perf_counter() - t0
     n = g * reps
-    groups = [None] * reps
     return {"value": round(n / dt, 4), "unit": "utt/s", "cores": threads, "kind": kind,
             "sample": f"{n} utterances of the same workload (T={int(T[0])}, S={int(S[0])}, V={V}): "
-                      f"{len(groups)} call(s) of {g}, cost_and_grad at fp32, OpenMP over utterances "
+                      f"{reps} call(s) of {g}, cost_and_grad at fp32, OpenMP over utterances "
                       f"({threads} threads), {dt:.2f} s",
             "finite": finite}
 
