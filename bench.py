@@ -197,7 +197,7 @@ def main():
         except Exception:
             traffic = None
 
-    copy_gbps = box_copy_gbps(dev)
+    copy_gbps = box_copy_gbps(lib, L, dev)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_sample > 0 and args.acts_dtype == "f32":
@@ -248,21 +248,26 @@ def main():
         dist.destroy_process_group()
 
 
-def box_copy_gbps(dev, gib=4, reps=5):
-    """Device-to-device copy rate of this box (torch copy_, read + write bytes / time): HBM rates differ by up
-    to ~15 % between MI355X boxes of the pool (profiles/r01/membench_ceilings*.json), so the gradient kernel's
-    rate is also reported against what a plain copy reaches on the same card. None if memory is short."""
+def box_copy_gbps(lib, L, dev, gib=4, reps=5):
+    """This card's device-copy rate (mrnnt_copy_probe: the gradient pass's access pattern, read + write bytes /
+    time, HIP events on the stream it runs on): HBM rates differ by up to ~15 % between MI355X boxes of the
+    pool (profiles/r01/membench_ceilings*.json), so the gradient kernel's rate is also reported against what a
+    plain copy reaches on the same card. None if memory is short."""
     n = gib << 30
     if torch.cuda.mem_get_info(dev)[0] < 2 * n + (4 << 30):
         return None
-    src = torch.empty(n, dtype=torch.uint8, device=dev)
+    src = torch.zeros(n, dtype=torch.uint8, device=dev)
     dst = torch.empty_like(src)
-    dst.copy_(src)
+    stream = torch.cuda.current_stream(dev)
+    sp = ctypes.c_void_p(stream.cuda_stream)
+    run = lambda: L.check(lib.mrnnt_copy_probe(ctypes.c_void_p(dst.data_ptr()), ctypes.c_void_p(src.data_ptr()),  # noqa: E731
+                                               n, sp), "copy_probe")
+    run()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
+    e0.record(stream)
     for _ in range(reps):
-        dst.copy_(src)
-    e1.record()
+        run()
+    e1.record(stream)
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
     del src, dst

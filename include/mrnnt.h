@@ -154,7 +154,8 @@ int mrnnt_version(void);
 /* Kernel-time accounting over HIP events recorded around each launch on its stream.
  * enable=1 starts recording (clearing previous records). mrnnt_profile_read synchronises the
  * recorded events and returns per-kernel totals in ms and launch counts for
- *   [0] band, [1] log-softmax row reduce, [2] alpha/beta DP, [3] logit gradient, [4] setup. */
+ *   [0] band, [1] log-softmax row reduce, [2] alpha/beta DP, [3] logit gradient, [4] setup,
+ *   [5] joint forward, [6] joint backward, [7] joint reduce. */
 void mrnnt_profile_enable(int enable);
 int mrnnt_profile_read(double *total_ms, int64_t *launches, int n);
 
@@ -172,6 +173,12 @@ int mrnnt_tune(const char *key, int value);
  * host twin in oracle/rnnt_oracle.c): element i gets hash(seed, begin + i) as N(0,1)-like
  * (normal=1) or U[0,1) (normal=0). */
 RNNTStatus mrnnt_synth_acts(float *out, int64_t begin, int64_t count, uint64_t seed, int normal, hipStream_t stream);
+
+/* Bench helper (not part of the reference interface): copy `bytes` (a multiple of 16, 16-byte aligned
+ * pointers) from src to dst on the device in the gradient pass's access pattern (contiguous slabs per
+ * workgroup, nontemporal loads and stores), so a bench can report this card's own copy rate next to the
+ * kernels' rates. */
+RNNTStatus mrnnt_copy_probe(void *dst, const void *src, size_t bytes, hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -586,6 +586,14 @@ RNNTStatus mrnnt_synth_acts(float *out, int64_t begin, int64_t count, uint64_t s
     return RNNT_STATUS_SUCCESS;
 }
 
+RNNTStatus mrnnt_copy_probe(void *dst, const void *src, size_t bytes, hipStream_t stream) {
+    if ((bytes & 15) || (reinterpret_cast<uintptr_t>(dst) & 15) || (reinterpret_cast<uintptr_t>(src) & 15))
+        return fail(RNNT_STATUS_INVALID_VALUE, "copy_probe: bytes and pointers must be 16-byte aligned");
+    const hipError_t e = launch_copy_probe(dst, src, bytes, stream);
+    if (e != hipSuccess) return fail_hip(e, "copy probe kernel");
+    return RNNT_STATUS_SUCCESS;
+}
+
 }  // extern "C"
 
 // =================================================================================================

@@ -95,6 +95,7 @@ hipError_t launch_dp(const DevProblem &p, int S_max, int with_beta, float *costs
 hipError_t launch_grad(const DevProblem &p, int elem, const float *scale, void *grads, int grid, hipStream_t stream);
 hipError_t launch_count_live(const DevProblem &p, unsigned long long *count, hipStream_t stream);
 hipError_t launch_pad_zero(const DevProblem &p, int elem, void *grads, hipStream_t stream);
+hipError_t launch_copy_probe(void *dst, const void *src, size_t bytes, hipStream_t stream);
 hipError_t launch_synth(float *out, int64_t begin, int64_t count, uint64_t seed, int normal, hipStream_t stream);
 
 // A lattice row (t, s) with alpha(t-1, s) + beta(t, s) - ll < kDeadLogOcc has occupancy below e^-110 =

@@ -11,10 +11,10 @@
 //              g = dL/dz (bf16) and the joint activation tanh(enc + pred) (bf16), so that dW = G^T Hact,
 //              dH = G W and dbias = sum G are plain GEMMs / reductions over live rows only.
 //
-// Tiling: a workgroup of 4 waves owns 128 consecutive rows of a row list; a wave owns 32 rows and keeps their
-// activations as the MFMA B operand in registers (lane l: row l&31, k = 16 ks + 8 (l>>5) + [0,8)), built
-// once from enc/pred with a fast tanh. W streams through LDS in 32-vocabulary chunks (double-buffered,
-// padded rows against bank conflicts) shared by the 4 waves; each chunk is one 32x32 output tile per wave,
+// Tiling: a workgroup of 8 waves (two per SIMD) owns 256 consecutive rows of a row list; a wave owns 32 rows and
+// keeps their activations as the MFMA B operand in registers (lane l: row l&31, k = 16 ks + 8 (l>>5) + [0,8)),
+// built once from enc/pred with a fast tanh. W streams through LDS in 32-vocabulary chunks (LDS-DMA, double-
+// buffered, XOR-swizzled against bank conflicts) shared by the 8 waves; each chunk is one 32x32 output tile per wave,
 // D[vocab][row] = sum_k W[vocab][k] h[row][k]: the accumulator holds 16 vocabulary entries of ONE row per
 // lane (vocab = (i&3) + 8 (i>>2) + 4 (l>>5)), so the per-row online softmax is register-local and the two
 // lane halves merge once at the end.
@@ -28,13 +28,26 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f2 __attribute__((ext_vector_type(2)));
 
+// scalar f32 in the MFMA loop's epilogue: a packed v_pk_fma/add_f32 beside MFMAs costs more issue time than the
+// two scalar ops it replaces (MI355X_MICROARCH.md, per-instruction constants; the joint file is built with
+// -fno-slp-vectorize so these stay scalar -- measured 2 % faster forward and backward than packed)
+__device__ __forceinline__ f2 add2(f2 a, f2 b) { return (f2){a.x + b.x, a.y + b.y}; }
+__device__ __forceinline__ f2 mul2(f2 a, f2 b) { return (f2){a.x * b.x, a.y * b.y}; }
+__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return (f2){fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y)}; }
+
 __device__ __forceinline__ float bf16_lo(unsigned u) { return __uint_as_float(u << 16); }
 __device__ __forceinline__ float bf16_hi(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
 
-// tanh(x) = sign(x) (1 - e) / (1 + e), e = exp(-2|x|): v_exp_f32 + v_rcp_f32, |error| ~ 1e-7
-__device__ __forceinline__ float fast_tanh(float x) {
-    const float e = fast_exp2(-2.0f * kLog2e * fabsf(x));
-    return copysignf((1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e), x);
+
+// tanh(x) = sign(x) (1 - e) / (1 + e), e = exp(-2|x|) (v_exp_f32 + v_rcp_f32, |error| ~ 1e-7), two at a time on
+// packed f32 (v_pk_*): build_act runs before the MFMA loop, where packing halves its VALU
+__device__ __forceinline__ f2 fast_tanh2(f2 x) {
+    const f2 ax = {fabsf(x.x), fabsf(x.y)};
+    const f2 t = ax * (f2){-2.0f * kLog2e, -2.0f * kLog2e};
+    const f2 e = {fast_exp2(t.x), fast_exp2(t.y)};
+    const f2 num = (f2){1.0f, 1.0f} - e, den = (f2){1.0f, 1.0f} + e;
+    const f2 y = num * (f2){__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+    return (f2){copysignf(y.x, x.x), copysignf(y.y, x.y)};
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -161,8 +174,10 @@ __device__ __forceinline__ void build_act(const JointArgs &j, const RowPos &q, i
         bf16x8 h;
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
-            h[2 * w] = (__bf16)(keep * fast_tanh(bf16_lo(ev[w]) + bf16_lo(pv[w])));
-            h[2 * w + 1] = (__bf16)(keep * fast_tanh(bf16_hi(ev[w]) + bf16_hi(pv[w])));
+            const f2 y = fast_tanh2((f2){bf16_lo(ev[w]), bf16_hi(ev[w])} + (f2){bf16_lo(pv[w]), bf16_hi(pv[w])}) *
+                         (f2){keep, keep};
+            h[2 * w] = (__bf16)y.x;
+            h[2 * w + 1] = (__bf16)y.y;
         }
         if (STORE && v) *reinterpret_cast<bf16x8 *>(j.Hact + i * H + 16 * ks + 8 * half) = h;
         bfr[ks] = h;
@@ -264,8 +279,8 @@ __device__ __forceinline__ void logits2(const f32x16 &acc, const float *bias_lds
 #pragma unroll
     for (int q4 = 0; q4 < 4; ++q4) {
         const f4 bv = *reinterpret_cast<const f4 *>(bias_lds + 32 * c + 8 * q4 + 4 * half);
-        z[2 * q4] = (f2){acc[4 * q4], acc[4 * q4 + 1]} + (f2){bv.x, bv.y};
-        z[2 * q4 + 1] = (f2){acc[4 * q4 + 2], acc[4 * q4 + 3]} + (f2){bv.z, bv.w};
+        z[2 * q4] = add2((f2){acc[4 * q4], acc[4 * q4 + 1]}, (f2){bv.x, bv.y});
+        z[2 * q4 + 1] = add2((f2){acc[4 * q4 + 2], acc[4 * q4 + 3]}, (f2){bv.z, bv.w});
     }
 }
 
@@ -345,8 +360,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
         f2 s2 = {0.0f, 0.0f};
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const f2 t = z[k] * l2e + nb;  // v_pk_fma_f32
-            s2 += (f2){fast_exp2(t.x), fast_exp2(t.y)};
+            const f2 t = fma2(z[k], l2e, nb);
+            s2 = add2(s2, (f2){fast_exp2(t.x), fast_exp2(t.y)});
         }
         sum = sum * fast_exp2((m - mr) * kLog2e) + (s2.x + s2.y);
         m = mn;
@@ -417,7 +432,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
         logits2(acc, bias, c, half, g);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const f2 t = g[k] * l2e + c2;  // v_pk_fma_f32
+            const f2 t = fma2(g[k], l2e, c2);
             g[k] = (f2){fast_exp2(t.x), fast_exp2(t.y)};
         }
         // the <= 2 corrected entries of the row are rewritten by a second (2-byte) store after the vector store
@@ -430,7 +445,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
         if (rb >= 0) gb = tree_pick(g, rb);
         if (__ballot(mine)) gl = tree_pick(g, rl);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) g[k] = g[k] * sc2;  // v_pk_mul_f32
+        for (int k = 0; k < 8; ++k) g[k] = mul2(g[k], sc2);
         if (q.valid) {
 #pragma unroll
             for (int qd = 0; qd < 4; ++qd) {

@@ -134,6 +134,36 @@ hipError_t launch_align(const DevProblem &p, const int *alignment, int64_t align
     return hipGetLastError();
 }
 
+// bandwidth probe: a device copy in the gradient pass's access pattern -- each workgroup streams its own
+// contiguous slab of 16-byte elements, 4 loads in flight per lane, nontemporal loads and stores
+__global__ __launch_bounds__(256) void copy_probe_kernel(const u4 *__restrict__ a, u4 *__restrict__ b, int64_t n,
+                                                         int64_t slab) {
+    for (int64_t c0 = (int64_t)blockIdx.x * slab; c0 < n; c0 += (int64_t)gridDim.x * slab) {
+        const int64_t end = min(c0 + slab, n);
+        for (int64_t i = c0 + threadIdx.x; i < end; i += 256 * 4) {
+            u4 x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i + 256 * u < end) x[u] = __builtin_nontemporal_load(&a[i + 256 * u]);
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i + 256 * u < end) __builtin_nontemporal_store(x[u], &b[i + 256 * u]);
+        }
+    }
+}
+
+hipError_t launch_copy_probe(void *dst, const void *src, size_t bytes, hipStream_t stream) {
+    const int64_t n = (int64_t)(bytes / 16);
+    if (n <= 0) return hipSuccess;
+    int dev = 0, cus = 256;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int64_t slab = 50 * 1024;  // 800 KiB per workgroup pass
+    const int64_t blocks = std::min<int64_t>((n + slab - 1) / slab, (int64_t)32 * cus);
+    copy_probe_kernel<<<(int)blocks, 256, 0, stream>>>(static_cast<const u4 *>(src), static_cast<u4 *>(dst), n, slab);
+    return hipGetLastError();
+}
+
 hipError_t launch_synth(float *out, int64_t begin, int64_t count, uint64_t seed, int normal, hipStream_t stream) {
     if (count <= 0) return hipSuccess;
     int64_t blocks = (count + 255) / 256;

@@ -1,7 +1,8 @@
 """ctypes binding of libmonotonic_rnnt_amd.so (the flat C ABI in include/mrnnt.h).
 
 There is no fallback: if the HIP library is missing or fails to load, importing this module raises.
-Build it with `python __graft_entry__.py` (or `make -C monotonic-rnnt_amd`).
+Build it with `python __graft_entry__.py` (or `make -C monotonic-rnnt_amd`). MRNNT_LIB=<path> loads another
+build of the same ABI instead (A/B measurements of compile-time variants, tools/).
 """
 from __future__ import annotations
 
@@ -10,7 +11,7 @@ import os
 import threading
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "libmonotonic_rnnt_amd.so")
+LIB_PATH = os.environ.get("MRNNT_LIB") or os.path.join(PKG_DIR, "libmonotonic_rnnt_amd.so")
 
 RNNT_STATUS_SUCCESS = 0
 RNNT_STATUS_MEMOPS_FAILED = 1
@@ -119,6 +120,7 @@ def load() -> ctypes.CDLL:
             "mrnnt_profile_enable": (None, [i]),
             "mrnnt_profile_read": (i, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64), i]),
             "mrnnt_synth_acts": (i, [vp, i64, i64, ctypes.c_uint64, i, vp]),
+            "mrnnt_copy_probe": (i, [vp, vp, sz, vp]),
             "mrnnt_tune": (i, [ctypes.c_char_p, i]),
         }
         for name, (res, args) in sig.items():
