@@ -164,7 +164,8 @@ int mrnnt_profile_read(double *total_ms, int64_t *launches, int n);
  * sweep for the packed layout), "softmax_grid_per_cu" / "grad_grid_per_cu" (persistent workgroups per
  * CU, 0 = one workgroup per lattice column; "grid_per_cu" sets both), "nt_store" / "nt_load" (0/1:
  * nontemporal grads stores / acts loads), "occ_skip" (0/1: skip the acts read of rows
- * whose gradient is exactly zero, see mrnnt_grad_live_rows).
+ * whose gradient is exactly zero, see mrnnt_grad_live_rows), "joint_nbuf" (2/3 LDS weight buffers of
+ * the fused joint kernels).
  * Sets `key` to `value` (value < 0: query only) and returns the previous value, or -1 for an unknown key.
  * Process-global; not thread-safe against concurrent launches. */
 int mrnnt_tune(const char *key, int value);

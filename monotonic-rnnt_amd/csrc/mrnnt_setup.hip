@@ -156,8 +156,9 @@ hipError_t launch_copy_probe(void *dst, const void *src, size_t bytes, hipStream
     const int64_t n = (int64_t)(bytes / 16);
     if (n <= 0) return hipSuccess;
     int dev = 0, cus = 256;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return e;
     const int64_t slab = 50 * 1024;  // 800 KiB per workgroup pass
     const int64_t blocks = std::min<int64_t>((n + slab - 1) / slab, (int64_t)32 * cus);
     copy_probe_kernel<<<(int)blocks, 256, 0, stream>>>(static_cast<const u4 *>(src), static_cast<u4 *>(dst), n, slab);

@@ -2,7 +2,8 @@
 
 There is no fallback: if the HIP library is missing or fails to load, importing this module raises.
 Build it with `python __graft_entry__.py` (or `make -C monotonic-rnnt_amd`). MRNNT_LIB=<path> loads another
-build of the same ABI instead (A/B measurements of compile-time variants, tools/).
+build of the same ABI instead (A/B measurements of compile-time variants, tools/); MRNNT_TUNE="key=value,..."
+sets launch knobs (mrnnt_tune) at load.
 """
 from __future__ import annotations
 
@@ -130,6 +131,10 @@ def load() -> ctypes.CDLL:
         if lib.mrnnt_version() < 2:
             raise ImportError(f"{LIB_PATH} is a stale build (ABI version {lib.mrnnt_version()} < 2); "
                               "rebuild with `make -C monotonic-rnnt_amd`")
+        for kv in filter(None, os.environ.get("MRNNT_TUNE", "").split(",")):
+            k, v = kv.split("=")
+            if lib.mrnnt_tune(k.strip().encode(), int(v)) < 0:
+                raise ValueError(f"MRNNT_TUNE: unknown knob {k!r}")
         _lib = lib
         return lib
 
