@@ -191,8 +191,10 @@ def main():
         try:
             pm = json.load(open(pmc_path))
             # only a measurement of this config and of the kernel this run launches counts
-            if pm.get("config") == args.config and pm.get("kernel", "").startswith(
-                    "grad_rows_kernel" if L.tune("grad_variant") == 3 else "grad_kernel<IoF32"):
+            gv = L.tune("grad_variant")
+            fam = {3: "grad_rows_kernel", 5: "grad_staged_kernel", 6: "grad_staged_kernel"}.get(gv, "grad_kernel")
+            elem = {"f32": "IoF32", "bf16": "IoBF16", "f16": "IoF16"}[args.acts_dtype]
+            if pm.get("config") == args.config and pm.get("kernel", "").startswith(f"{fam}<{elem}"):
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -222,7 +224,7 @@ def main():
                        "parallelism": f"dp{world} (batch-sharded, one 4-byte "
                                       f"{'gloo (rehearsal)' if gloo else 'RCCL'} loss all-reduce)"},
             "achieved_hbm_gbps_step": round(step_bytes * total_utts / B * args.steps / elapsed / 1e9, 1),
-            "roofline": {"kernel": "grad_kernel (logit gradient)", "bound": "hbm",
+            "roofline": {"kernel": "logit gradient (grad_variant %d)" % L.tune("grad_variant"), "bound": "hbm",
                          "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4) if achieved else None,
                          "traffic": traffic, "algorithmic_bytes_per_launch": grad_bytes,
@@ -248,7 +250,7 @@ def main():
         dist.destroy_process_group()
 
 
-def box_copy_gbps(lib, L, dev, gib=4, reps=5):
+def box_copy_gbps(lib, L, dev, gib=8, reps=5):
     """This card's device-copy rate (mrnnt_copy_probe: the gradient pass's access pattern, read + write bytes /
     time, HIP events on the stream it runs on): HBM rates differ by up to ~15 % between MI355X boxes of the
     pool (profiles/r01/membench_ceilings*.json), so the gradient kernel's rate is also reported against what a

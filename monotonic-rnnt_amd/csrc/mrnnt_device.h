@@ -51,6 +51,35 @@ __device__ __forceinline__ void wave_reduce_max_sum(float &m, float &s) {
     }
 }
 
+// DPP wave64 reductions with a wave-uniform result (read from lane 63 into an SGPR): quad xor 1, xor 2,
+// half-row mirror, row mirror (every row of 16 holds its total), then row_bcast:15 / row_bcast:31 carry the
+// row totals up to lane 63. Six DPP-fed VALU ops and one v_readlane, no LDS (cf. ds_bpermute butterflies).
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ float dpp_f(float old, float src) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(src), CTRL, ROW_MASK, 0xf,
+                                                      false));
+}
+
+__device__ __forceinline__ float wave_max_uniform(float v) {
+    v = fmaxf(v, dpp_f<0xB1>(v, v));        // quad_perm [1,0,3,2]
+    v = fmaxf(v, dpp_f<0x4E>(v, v));        // quad_perm [2,3,0,1]
+    v = fmaxf(v, dpp_f<0x141>(v, v));       // row_half_mirror
+    v = fmaxf(v, dpp_f<0x140>(v, v));       // row_mirror
+    v = fmaxf(v, dpp_f<0x142, 0xa>(v, v));  // row_bcast:15 into rows 1, 3
+    v = fmaxf(v, dpp_f<0x143, 0xc>(v, v));  // row_bcast:31 into rows 2, 3
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
+__device__ __forceinline__ float wave_sum_uniform(float v) {
+    v += dpp_f<0xB1>(0.0f, v);
+    v += dpp_f<0x4E>(0.0f, v);
+    v += dpp_f<0x141>(0.0f, v);
+    v += dpp_f<0x140>(0.0f, v);
+    v += dpp_f<0x142, 0xa>(0.0f, v);  // rows 0, 2 add the old value 0
+    v += dpp_f<0x143, 0xc>(0.0f, v);
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
 // Monotone utterance cursor over a prefix-offset array (col_off or row_off), for a workgroup/wave that
 // walks indices in increasing order: one binary search at start, then amortised O(1) advances.
 struct Cursor {
@@ -168,8 +197,10 @@ __device__ __forceinline__ RowCoef row_coef(const DevProblem &p, int t, int T, i
     RowCoef rc;
     rc.live = !p.occ_skip || row_live(base + b0);
     rc.c2 = (float)(((double)p.den[row] + base + b0) * kLog2eD);
-    rc.cb = (float)exp(p.lpb[row] + base + b1);
-    rc.ce = (s < S) ? (float)exp(p.lpe[row] + base + b2) : 0.0f;
+    // the exponents are O(10) after the fp64 cancellation of alpha + beta - ll: fp32 v_exp_f32 on the
+    // rounded exponent (relative error ~1e-6 of a coefficient <= 1)
+    rc.cb = fast_exp2((float)((p.lpb[row] + base + b1) * kLog2eD));
+    rc.ce = (s < S) ? fast_exp2((float)((p.lpe[row] + base + b2) * kLog2eD)) : 0.0f;
     const int lab = (s < S) ? lab_b[s] : -1;
     rc.lab = (lab == p.blank) ? -1 : lab;
     return rc;

@@ -106,6 +106,93 @@ __global__ __launch_bounds__(256) void grad_kernel(DevProblem p, const float *__
     }
 }
 
+// Staged-coefficient kernel (grad_variant 5/6: R = 1 / 2 rows per wave). Work unit = a segment of up to 256
+// rows of one lattice column. Phase A: one row per thread, the row's coefficients (row_coef: alpha/beta/den/lp
+// read as coalesced vectors along s, the two fp64 exps lane-parallel) go to an LDS slot {c2, cb, ce, label|dead}.
+// Phase B: the waves stream the segment's rows; a row's acts loads wait only for one broadcast LDS read, not for
+// a chain of dependent scalar loads and fp64 math, so every wave keeps its row(s) of acts in flight. Two LDS
+// buffers alternate between work units: one barrier per unit.
+template <class IO, int U, int R, bool NTL, bool NTS>
+__global__ __launch_bounds__(256) void grad_staged_kernel(DevProblem p, const float *__restrict__ scale,
+                                                          void *__restrict__ grads) {
+    typedef typename IO::V Vec;
+    constexpr int SEG = 256;
+    constexpr int DEAD = -2;  // label slot of a row whose gradient is exactly zero (out of band or dead)
+    __shared__ float4 coef[2][SEG];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int VL = p.V / IO::E;
+    const int blank = p.blank;
+    const Vec *__restrict__ av = reinterpret_cast<const Vec *>(p.acts);
+    Vec *__restrict__ gv = reinterpret_cast<Vec *>(grads);
+
+    Cursor cur;
+    cur.b = blockIdx.x < p.num_cols ? p.col_b[blockIdx.x] : 0;
+    int buf = 0;
+    for (int64_t c = blockIdx.x; c < p.num_cols; c += gridDim.x) {
+        cur.advance(p.col_off, c);
+        const int b = cur.b;
+        const int T = p.T[b], S = p.S[b];
+        const int t = (int)(c - p.col_off[b]);
+        const int64_t rowc = p.row_off[b] + (int64_t)t * (S + 1);
+        const int64_t arow = acts_col_base(p, b, t, rowc);
+        const int lo = max(0, t - (T - S));
+        const int hi = min(t, S);
+        const double ll = p.ll[b];
+        const float sc = scale ? scale[b] : 1.0f;
+        const Vec zv = splat<IO>(0.0f * sc);
+        const int *__restrict__ lab_b = p.labels + (int64_t)b * p.label_stride;
+
+        for (int seg = 0; seg <= S; seg += SEG, buf ^= 1) {
+            {  // phase A
+                const int s = seg + tid;
+                float4 cf = make_float4(0.0f, 0.0f, 0.0f, __int_as_float(DEAD));
+                if (s >= lo && s <= hi) {
+                    const RowCoef rc = row_coef(p, t, T, S, s, rowc + s, ll, lab_b);
+                    if (rc.live) cf = make_float4(rc.c2, rc.cb, rc.ce, __int_as_float(rc.lab));
+                }
+                if (s <= S) coef[buf][tid] = cf;
+            }
+            __syncthreads();
+            const int n = min(SEG, S + 1 - seg);
+            for (int i = wave * R; i < n; i += 4 * R) {
+                float4 cf[R];
+                bool live[R], ok[R];
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    ok[r] = i + r < n;
+                    cf[r] = coef[buf][ok[r] ? i + r : i];
+                    live[r] = ok[r] && __float_as_int(cf[r].w) != DEAD;
+                }
+                for (int base = 0; base < VL; base += 64 * U) {
+                    Vec x[R][U];
+#pragma unroll
+                    for (int r = 0; r < R; ++r)
+#pragma unroll
+                        for (int u = 0; u < U; ++u) {
+                            const int j = base + lane + 64 * u;
+                            if (live[r] && j < VL)
+                                x[r][u] = vload<NTL>(&av[(arow + seg + i + r) * (int64_t)VL + j]);
+                        }
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        if (!ok[r]) continue;
+                        const RowCoef rc{cf[r].x, cf[r].y, cf[r].z, __float_as_int(cf[r].w), true};
+#pragma unroll
+                        for (int u = 0; u < U; ++u) {
+                            const int j = base + lane + 64 * u;
+                            if (j >= VL) continue;
+                            const Vec g = live[r] ? grad_vec<IO>(x[r][u], rc, j, blank, sc) : zv;
+                            vstore<NTS>(&gv[(arow + seg + i + r) * (int64_t)VL + j], g);
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
 // Row-stride kernel (grad_variant 3, packed layout only): every wave of the grid sweeps lattice rows in
 // memory order (wave w takes rows w, w + nwaves, ...), so the grid streams one contiguous window of acts
 // and grads like a grid-stride copy; (b, t, s) of a row come from a per-wave monotone cursor over row_off
@@ -280,7 +367,16 @@ template <class IO, bool NTL, bool NTS>
 static void launch_vec(const DevProblem &p, const float *scale, void *grads, int grid, hipStream_t stream) {
     const int VL = p.V / IO::E;
     const int variant = tuning().grad_variant;
-    if (variant == 4 && VL >= 192) {
+    if ((variant == 5 || variant == 6) && VL >= 96) {
+        const bool big = VL >= 192;
+        if (variant == 6) {
+            if (big) grad_staged_kernel<IO, 4, 2, NTL, NTS><<<grid, 256, 0, stream>>>(p, scale, grads);
+            else grad_staged_kernel<IO, 2, 2, NTL, NTS><<<grid, 256, 0, stream>>>(p, scale, grads);
+        } else {
+            if (big) grad_staged_kernel<IO, 4, 1, NTL, NTS><<<grid, 256, 0, stream>>>(p, scale, grads);
+            else grad_staged_kernel<IO, 2, 1, NTL, NTS><<<grid, 256, 0, stream>>>(p, scale, grads);
+        }
+    } else if (variant == 4 && VL >= 192) {
         grad_kernel<IO, 4, 1, NTL, NTS, 1><<<grid, 256, 0, stream>>>(p, scale, grads);
         grad_kernel<IO, 4, 1, NTL, NTS, 2><<<grid, 256, 0, stream>>>(p, scale, grads);
     } else if (variant == 3 && p.pad_S1 == 0 && VL >= 192)

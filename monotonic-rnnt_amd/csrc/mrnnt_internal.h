@@ -71,8 +71,12 @@ hipError_t launch_zero(void *ptr, size_t bytes, hipStream_t stream);
 
 // Launch-shape knobs (experiment hook: mrnnt_tune in mrnnt_capi.cpp). Defaults are the tuned values.
 struct Tuning {
-    int softmax_variant = 2;      // rows per wave of the log-softmax kernel: 0 -> 1 row, 2 -> 2 rows (large V)
-    int grad_variant = 0;         // 0 -> 1 row per wave, 2 -> 2 rows per wave, 3 -> row-stride sweep (packed)
+    int softmax_variant = 13;     // log-softmax kernel: 13/14/15 -> lean kernel with 2/1/4 rows per wave (rows of
+                                  // >= 96 vectors); 0/2/3.. -> first kernel (shuffle butterflies) with 1/2/3.. rows;
+                                  // 11/12 -> row-stride sweep (packed)
+    int grad_variant = 5;         // gradient kernel: 5/6 -> staged coefficients, 1/2 rows per wave (rows of >= 96
+                                  // vectors); 0/2 -> per-row coefficients, 1/2 rows; 3 -> row-stride sweep (packed);
+                                  // 4 -> zero rows then live rows
     int softmax_grid_per_cu = 0;  // workgroups (of 4 waves) per CU; 0 = one workgroup per lattice column
     int grad_grid_per_cu = 32;    // same for the gradient kernel
     int nt_store = 1;             // nontemporal stores of grads

@@ -159,8 +159,11 @@ hipError_t launch_copy_probe(void *dst, const void *src, size_t bytes, hipStream
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e != hipSuccess) return e;
-    const int64_t slab = 50 * 1024;  // 800 KiB per workgroup pass
-    const int64_t blocks = std::min<int64_t>((n + slab - 1) / slab, (int64_t)32 * cus);
+    // 32 workgroups per CU, each streaming >= 8 slabs in turn (a single pass of one slab per workgroup
+    // measures the launch tail, not the memory); slabs of 16 KiB .. 800 KiB, whole 4 KiB workgroup steps
+    const int64_t blocks_max = (int64_t)32 * cus;
+    const int64_t slab = std::min<int64_t>(50 * 1024, std::max<int64_t>(1024, n / (blocks_max * 8) / 1024 * 1024));
+    const int64_t blocks = std::min<int64_t>((n + slab - 1) / slab, blocks_max);
     copy_probe_kernel<<<(int)blocks, 256, 0, stream>>>(static_cast<const u4 *>(src), static_cast<u4 *>(dst), n, slab);
     return hipGetLastError();
 }

@@ -116,6 +116,226 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(OCC))) 
     }
 }
 
+// Element v of a lane's slice of the row (x[u][i], vector j = v / E in lane j % 64, u = j / 64 % U) into
+// every lane (wave-uniform u, i: one indexed register move), then v_readlane from the owning lane.
+template <int N>
+__device__ __forceinline__ float lane_pick(const float (&x)[N], int k) {
+    typedef float VN __attribute__((ext_vector_type(N)));
+    VN v;
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = x[i];
+    return v[k];
+}
+
+// Lean variant (softmax_variant 2 default for rows of >= 192 vectors; 13/14 select R = 1 / 4): the same
+// column walk and online per-lane (max, sum) as softmax_kernel, with the per-row overhead taken off the
+// vector pipe -- (max, sum) merged by DPP reductions into wave-uniform scalars (no ds_bpermute butterfly, one
+// exp per lane instead of two per step), blank / label logits read with a uniform indexed move + v_readlane
+// (no LDS spill of the row slice), and den / lpb / lpe of the R rows formed in parallel by lanes 0..R-1
+// (one fp64 log per R rows). FULL: V is a multiple of 64*U*E (no per-load bounds checks).
+template <class IO, int U, int R, bool NTL, bool FULL>
+__global__ __launch_bounds__(256) void softmax_lean_kernel(DevProblem p) {
+    constexpr int E = IO::E;
+    constexpr int CH = 64 * U;  // vectors per chunk
+    typedef typename IO::V Vec;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int VL = p.V / E;
+    const Vec *__restrict__ av = reinterpret_cast<const Vec *>(p.acts);
+    const int blank = p.blank;
+    const Vec ninf = splat<IO>(NEG_INF_F);
+
+    for (int64_t c = blockIdx.x; c < p.num_cols; c += gridDim.x) {
+        const int b = p.col_b[c];
+        const int T = p.T[b], S = p.S[b];
+        const int t = (int)(c - p.col_off[b]);
+        const int64_t rowc = p.row_off[b] + (int64_t)t * (S + 1);
+        const int64_t arow = acts_col_base(p, b, t, rowc);
+        const int lo = max(0, t - (T - S));
+        const int hi = min(t, S);
+        const int *__restrict__ lab_b = p.labels + (int64_t)b * p.label_stride;
+        zero_fill_outside_band(p, rowc, S, lo, hi);
+
+        for (int s = lo + wave * R; s <= hi; s += 4 * R) {
+            const int nrow = __builtin_amdgcn_readfirstlane(min(R, hi - s + 1));
+            float m[R], sum[R], zb[R], ze[R];
+            int lab[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                lab[r] = (r < nrow && s + r < S) ? __builtin_amdgcn_readfirstlane(lab_b[s + r]) : -1;
+                m[r] = NEG_INF_F;
+                sum[r] = 0.0f;
+                zb[r] = 0.0f;
+                ze[r] = 0.0f;
+            }
+            for (int base = 0; base < VL; base += CH) {
+                Vec x[R][U];
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    if (r < nrow) {
+#pragma unroll
+                        for (int u = 0; u < U; ++u) {
+                            const int j = base + lane + 64 * u;
+                            x[r][u] = (FULL || j < VL) ? vload<NTL>(&av[(arow + s + r) * (int64_t)VL + j]) : ninf;
+                        }
+                    } else {
+#pragma unroll
+                        for (int u = 0; u < U; ++u) x[r][u] = ninf;
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    float xf[U * E];
+                    float cm = NEG_INF_F;
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        float t4[E];
+                        IO::unpack(x[r][u], t4);
+#pragma unroll
+                        for (int i = 0; i < E; ++i) {
+                            xf[u * E + i] = t4[i];
+                            cm = fmaxf(cm, t4[i]);
+                        }
+                    }
+                    // blank / label logits: uniform position inside this chunk -> indexed move + readlane
+                    const int jb = blank / E - base;
+                    if (jb >= 0 && jb < CH) {
+                        const float v = lane_pick<U * E>(xf, (jb >> 6) * E + blank % E);
+                        zb[r] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), jb & 63));
+                    }
+                    const int je = lab[r] >= 0 ? lab[r] / E - base : -1;
+                    if (je >= 0 && je < CH) {
+                        const float v = lane_pick<U * E>(xf, (je >> 6) * E + lab[r] % E);
+                        ze[r] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), je & 63));
+                    }
+                    const float mn = fmaxf(m[r], cm);
+                    const float mr = (mn == NEG_INF_F) ? 0.0f : mn;
+                    const float off = -mr * kLog2e;
+                    float acc = sum[r] * fast_exp2(fmaf(m[r], kLog2e, off));
+#pragma unroll
+                    for (int k = 0; k < U * E; ++k) acc += fast_exp2(fmaf(xf[k], kLog2e, off));
+                    sum[r] = acc;
+                    m[r] = mn;
+                }
+            }
+            // merge the lanes: wave max, rescale each lane's sum to it, wave sum (uniform results)
+            float em = 0.0f, es = 1.0f, ezb = 0.0f, eze = 0.0f;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                if (r >= nrow) break;
+                const float M = wave_max_uniform(m[r]);
+                const float Mr = (M == NEG_INF_F) ? 0.0f : M;
+                const float part = sum[r] * fast_exp2((m[r] - Mr) * kLog2e);
+                const float Ssum = wave_sum_uniform(part);
+                if (lane == r) {
+                    em = M;
+                    es = Ssum;
+                    ezb = zb[r];
+                    eze = ze[r];
+                }
+            }
+            if (lane < nrow) {
+                const int64_t row = rowc + s + lane;
+                const double den = -(double)em - log((double)es);
+                p.den[row] = (float)den;
+                p.lpb[row] = (double)ezb + den;
+                p.lpe[row] = (double)eze + den;
+            }
+        }
+    }
+}
+
+// Row-stride variant (softmax_variant 11, packed layout only): the waves of a persistent grid sweep lattice
+// rows in memory order (wave w takes rows [w*R, w*R+R), then w + nwaves, ...), so the whole grid reads one
+// moving window of acts like a grid-stride stream; (b, t, s) of each row from a per-wave monotone cursor.
+// Out-of-band rows are not read; their lp entries are zero-filled by the wave that owns the row.
+template <class IO, int U, int R, bool NTL>
+__global__ __launch_bounds__(256) void softmax_rows_kernel(DevProblem p) {
+    constexpr int E = IO::E;
+    typedef typename IO::V Vec;
+    const int lane = threadIdx.x & 63;
+    const int64_t gw = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    const int VL = p.V / E;
+    const Vec *__restrict__ av = reinterpret_cast<const Vec *>(p.acts);
+    const int blank = p.blank;
+    const int bj = blank / E, bc = blank % E, blane = bj & 63;
+    const Vec ninf = splat<IO>(NEG_INF_F);
+    Cursor cur;
+    cur.init(p.row_off, p.B, gw * R < p.num_rows ? gw * R : 0);
+    for (int64_t r0 = gw * R; r0 < p.num_rows; r0 += nw * R) {
+        float m[R], sum[R], zb[R], ze[R];
+        int lab[R];
+        bool ok[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int64_t row = r0 + r;
+            ok[r] = false;
+            lab[r] = -1;
+            if (row < p.num_rows) {
+                cur.advance(p.row_off, row);
+                const int b = cur.b;
+                const int T = p.T[b], S = p.S[b];
+                const unsigned loc = (unsigned)(row - p.row_off[b]);
+                const int t = (int)(loc / (unsigned)(S + 1));
+                const int s = (int)(loc - (unsigned)t * (unsigned)(S + 1));
+                ok[r] = s <= t && (S - s) <= (T - t);
+                if (ok[r] && s < S) lab[r] = p.labels[(int64_t)b * p.label_stride + s];
+                if (!ok[r] && lane == 0) {
+                    p.lpb[row] = 0.0;
+                    p.lpe[row] = 0.0;
+                }
+            }
+            m[r] = NEG_INF_F;
+            sum[r] = 0.0f;
+            zb[r] = 0.0f;
+            ze[r] = 0.0f;
+        }
+        for (int base = 0; base < VL; base += 64 * U) {
+            Vec x[R][U];
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int j = base + lane + 64 * u;
+                    x[r][u] = (ok[r] && j < VL) ? vload<NTL>(&av[(r0 + r) * (int64_t)VL + j]) : ninf;
+                }
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                float xf[U][E];
+                float cm = NEG_INF_F;
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int j = base + lane + 64 * u;
+                    IO::unpack(x[r][u], xf[u]);
+#pragma unroll
+                    for (int i = 0; i < E; ++i) cm = fmaxf(cm, xf[u][i]);
+                    if (j == bj) zb[r] = pick<E>(xf[u], bc);
+                    if (lab[r] >= 0 && j == lab[r] / E) ze[r] = pick<E>(xf[u], lab[r] % E);
+                }
+                const float mn = fmaxf(m[r], cm);
+                const float mr = (mn == NEG_INF_F) ? 0.0f : mn;
+                float acc = sum[r] * fast_exp2((m[r] - mr) * kLog2e);
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+#pragma unroll
+                    for (int i = 0; i < E; ++i) acc += fast_exp2((xf[u][i] - mr) * kLog2e);
+                sum[r] = acc;
+                m[r] = mn;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) wave_reduce_max_sum(m[r], sum[r]);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (!ok[r]) continue;
+            const float zbv = __shfl(zb[r], blane);
+            const float zev = lab[r] >= 0 ? __shfl(ze[r], (lab[r] / E) & 63) : 0.0f;
+            if (lane == 0) write_row(p, r0 + r, m[r], sum[r], zbv, zev);
+        }
+    }
+}
+
 // Scalar path (any V, any alignment, any element type): one row per wave, lanes stride over v.
 template <class IO>
 __global__ __launch_bounds__(256) void softmax_scalar_kernel(DevProblem p) {
@@ -168,7 +388,26 @@ template <class IO, bool NTL>
 static void launch_vec(const DevProblem &p, int grid, hipStream_t stream) {
     const int VL = p.V / IO::E;
     const int v = tuning().softmax_variant;
-    if (VL >= 192) {
+    if (v >= 13 && v <= 15 && VL >= 96) {  // lean kernels: U vectors per lane per chunk, R = 2 / 1 / 4 rows
+        const int U = VL >= 192 ? 4 : 2;
+        const bool full = VL % (64 * U) == 0;
+#define MRNNT_LEAN(UU, RR)                                                                          \
+    (full ? softmax_lean_kernel<IO, UU, RR, NTL, true><<<grid, 256, 0, stream>>>(p)                \
+          : softmax_lean_kernel<IO, UU, RR, NTL, false><<<grid, 256, 0, stream>>>(p))
+        if (U == 4) {
+            if (v == 14) MRNNT_LEAN(4, 1);
+            else if (v == 15) MRNNT_LEAN(4, 4);
+            else MRNNT_LEAN(4, 2);
+        } else {
+            if (v == 14) MRNNT_LEAN(2, 1);
+            else if (v == 15) MRNNT_LEAN(2, 4);
+            else MRNNT_LEAN(2, 2);
+        }
+#undef MRNNT_LEAN
+    } else if (v >= 11 && p.pad_S1 == 0 && VL >= 192) {  // row-stride sweeps (persistent grid, see mrnnt_forward)
+        if (v == 12) softmax_rows_kernel<IO, 4, 1, NTL><<<grid, 256, 0, stream>>>(p);
+        else softmax_rows_kernel<IO, 4, 2, NTL><<<grid, 256, 0, stream>>>(p);
+    } else if (VL >= 192) {
         switch (v) {  // rows per wave (R) and waves per workgroup for a row of >= 192 vectors
             case 0: softmax_kernel<IO, 4, 1, NTL><<<grid, 256, 0, stream>>>(p); break;
             case 3: softmax_kernel<IO, 4, 3, NTL><<<grid, 256, 0, stream>>>(p); break;

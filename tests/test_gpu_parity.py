@@ -251,6 +251,13 @@ def test_config_c2_vs_oracle(op, dev):
     {"softmax_variant": 0, "grad_variant": 2, "nt_load": 0, "nt_store": 0},
     {"softmax_variant": 2, "grad_variant": 3, "softmax_grid_per_cu": 5, "grad_grid_per_cu": 7},
     {"softmax_variant": 0, "grad_variant": 3, "grid_per_cu": 16, "nt_store": 1, "nt_load": 0},
+    {"softmax_variant": 11, "grad_variant": 4, "softmax_grid_per_cu": 3, "grad_grid_per_cu": 5},
+    {"softmax_variant": 12, "grad_variant": 0, "softmax_grid_per_cu": 0, "nt_load": 0},
+    {"softmax_variant": 13},
+    {"softmax_variant": 14, "softmax_grid_per_cu": 2, "nt_load": 0},
+    {"softmax_variant": 15},
+    {"grad_variant": 5},
+    {"grad_variant": 6, "grad_grid_per_cu": 3, "nt_load": 0, "nt_store": 0},
 ])
 def test_every_kernel_variant_matches_oracle(op, dev, knobs):
     """All launch variants selectable through mrnnt_tune compute the same result (alignment included)."""
@@ -400,7 +407,7 @@ def _live_rows(op, dev, acts, labels, T, S, alignment=None, k=0):
     return int(cnt.item())
 
 
-@pytest.mark.parametrize("grad_variant", [0, 2, 3])
+@pytest.mark.parametrize("grad_variant", [0, 2, 3, 5, 6])
 def test_occupancy_skip_is_bit_identical(op, dev, grad_variant):
     """With occ_skip the gradient kernel does not read acts rows whose occupancy is < e^-110; their fp32
     gradient is exactly 0 either way, so grads must be bit-identical with the skip on and off (and match the

@@ -4,7 +4,7 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${TAG:-full}
 mkdir -p $O
 cd $R
-timeout -k 10 900 python -m pytest tests -m gpu -q -x -rs > $O/pytest_gpu.log 2>&1 && \
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rs --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 && \
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && \
 timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err
 echo rc=$?
