@@ -247,10 +247,7 @@ RNNTStatus mrnnt_forward(const mrnnt_problem *p, void *ws, size_t ws_bytes, floa
         });
         if (e != hipSuccess) return fail_hip(e, "alignment band kernels");
     }
-    // softmax_variant >= 11 sweeps rows (packed layout only) on a persistent grid, the others walk columns
-    const int grid = (tuning().softmax_variant >= 11 && tuning().softmax_variant <= 12 && pl.pad_S1 == 0)
-                         ? streaming_grid(pl.N, tuning().softmax_grid_per_cu > 0 ? tuning().softmax_grid_per_cu : 16)
-                         : streaming_grid(pl.cols, tuning().softmax_grid_per_cu);
+    const int grid = streaming_grid(pl.cols, tuning().softmax_grid_per_cu);
     e = timed(K_SOFTMAX, stream, [&] { return launch_softmax(d, pl.elem, grid, stream); });
     if (e != hipSuccess) return fail_hip(e, "log-softmax kernel");
     e = timed(K_DP, stream, [&] { return launch_dp(d, pl.S_max, with_beta ? 1 : 0, costs_dev, stream); });

@@ -72,8 +72,7 @@ hipError_t launch_zero(void *ptr, size_t bytes, hipStream_t stream);
 // Launch-shape knobs (experiment hook: mrnnt_tune in mrnnt_capi.cpp). Defaults are the tuned values.
 struct Tuning {
     int softmax_variant = 13;     // log-softmax kernel: 13/14/15 -> lean kernel with 2/1/4 rows per wave (rows of
-                                  // >= 96 vectors); 0/2/3.. -> first kernel (shuffle butterflies) with 1/2/3.. rows;
-                                  // 11/12 -> row-stride sweep (packed)
+                                  // >= 96 vectors); 0/2/3.. -> first kernel (shuffle butterflies) with 1/2/3.. rows
     int grad_variant = 5;         // gradient kernel: 5/6 -> staged coefficients, 1/2 rows per wave (rows of >= 96
                                   // vectors); 0/2 -> per-row coefficients, 1/2 rows; 3 -> row-stride sweep (packed);
                                   // 4 -> zero rows then live rows

@@ -4,7 +4,8 @@
 // One pass over the in-band rows of acts. Work decomposition: workgroups walk lattice columns (b, t)
 // (one workgroup per column by default, or a persistent grid with a monotone utterance cursor); inside a
 // column the four waves take rows s. Per row each lane keeps an online (max, sum-exp) over its 16-byte
-// vector loads, one wave64 butterfly merges the pairs, den = -max - log(sum) is formed in fp64, and the
+// vector loads, the lanes are merged (DPP reductions in softmax_lean_kernel, the default for rows of >= 96
+// vectors; a shuffle butterfly in softmax_kernel), den = -max - log(sum) is formed in fp64, and the
 // blank / label logits are captured from registers on the way, so the kernel also emits
 //   lpb[r] = z[r, blank] + den[r],   lpe[r] = z[r, label(s)] + den[r]
 // -- the only two log-probs the recursion reads. Rows outside the band are never read; their lp entries
@@ -245,97 +246,6 @@ __global__ __launch_bounds__(256) void softmax_lean_kernel(DevProblem p) {
     }
 }
 
-// Row-stride variant (softmax_variant 11, packed layout only): the waves of a persistent grid sweep lattice
-// rows in memory order (wave w takes rows [w*R, w*R+R), then w + nwaves, ...), so the whole grid reads one
-// moving window of acts like a grid-stride stream; (b, t, s) of each row from a per-wave monotone cursor.
-// Out-of-band rows are not read; their lp entries are zero-filled by the wave that owns the row.
-template <class IO, int U, int R, bool NTL>
-__global__ __launch_bounds__(256) void softmax_rows_kernel(DevProblem p) {
-    constexpr int E = IO::E;
-    typedef typename IO::V Vec;
-    const int lane = threadIdx.x & 63;
-    const int64_t gw = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t nw = (int64_t)gridDim.x * 4;
-    const int VL = p.V / E;
-    const Vec *__restrict__ av = reinterpret_cast<const Vec *>(p.acts);
-    const int blank = p.blank;
-    const int bj = blank / E, bc = blank % E, blane = bj & 63;
-    const Vec ninf = splat<IO>(NEG_INF_F);
-    Cursor cur;
-    cur.init(p.row_off, p.B, gw * R < p.num_rows ? gw * R : 0);
-    for (int64_t r0 = gw * R; r0 < p.num_rows; r0 += nw * R) {
-        float m[R], sum[R], zb[R], ze[R];
-        int lab[R];
-        bool ok[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int64_t row = r0 + r;
-            ok[r] = false;
-            lab[r] = -1;
-            if (row < p.num_rows) {
-                cur.advance(p.row_off, row);
-                const int b = cur.b;
-                const int T = p.T[b], S = p.S[b];
-                const unsigned loc = (unsigned)(row - p.row_off[b]);
-                const int t = (int)(loc / (unsigned)(S + 1));
-                const int s = (int)(loc - (unsigned)t * (unsigned)(S + 1));
-                ok[r] = s <= t && (S - s) <= (T - t);
-                if (ok[r] && s < S) lab[r] = p.labels[(int64_t)b * p.label_stride + s];
-                if (!ok[r] && lane == 0) {
-                    p.lpb[row] = 0.0;
-                    p.lpe[row] = 0.0;
-                }
-            }
-            m[r] = NEG_INF_F;
-            sum[r] = 0.0f;
-            zb[r] = 0.0f;
-            ze[r] = 0.0f;
-        }
-        for (int base = 0; base < VL; base += 64 * U) {
-            Vec x[R][U];
-#pragma unroll
-            for (int r = 0; r < R; ++r)
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int j = base + lane + 64 * u;
-                    x[r][u] = (ok[r] && j < VL) ? vload<NTL>(&av[(r0 + r) * (int64_t)VL + j]) : ninf;
-                }
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                float xf[U][E];
-                float cm = NEG_INF_F;
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int j = base + lane + 64 * u;
-                    IO::unpack(x[r][u], xf[u]);
-#pragma unroll
-                    for (int i = 0; i < E; ++i) cm = fmaxf(cm, xf[u][i]);
-                    if (j == bj) zb[r] = pick<E>(xf[u], bc);
-                    if (lab[r] >= 0 && j == lab[r] / E) ze[r] = pick<E>(xf[u], lab[r] % E);
-                }
-                const float mn = fmaxf(m[r], cm);
-                const float mr = (mn == NEG_INF_F) ? 0.0f : mn;
-                float acc = sum[r] * fast_exp2((m[r] - mr) * kLog2e);
-#pragma unroll
-                for (int u = 0; u < U; ++u)
-#pragma unroll
-                    for (int i = 0; i < E; ++i) acc += fast_exp2((xf[u][i] - mr) * kLog2e);
-                sum[r] = acc;
-                m[r] = mn;
-            }
-        }
-#pragma unroll
-        for (int r = 0; r < R; ++r) wave_reduce_max_sum(m[r], sum[r]);
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            if (!ok[r]) continue;
-            const float zbv = __shfl(zb[r], blane);
-            const float zev = lab[r] >= 0 ? __shfl(ze[r], (lab[r] / E) & 63) : 0.0f;
-            if (lane == 0) write_row(p, r0 + r, m[r], sum[r], zbv, zev);
-        }
-    }
-}
-
 // Scalar path (any V, any alignment, any element type): one row per wave, lanes stride over v.
 template <class IO>
 __global__ __launch_bounds__(256) void softmax_scalar_kernel(DevProblem p) {
@@ -404,9 +314,6 @@ static void launch_vec(const DevProblem &p, int grid, hipStream_t stream) {
             else MRNNT_LEAN(2, 2);
         }
 #undef MRNNT_LEAN
-    } else if (v >= 11 && p.pad_S1 == 0 && VL >= 192) {  // row-stride sweeps (persistent grid, see mrnnt_forward)
-        if (v == 12) softmax_rows_kernel<IO, 4, 1, NTL><<<grid, 256, 0, stream>>>(p);
-        else softmax_rows_kernel<IO, 4, 2, NTL><<<grid, 256, 0, stream>>>(p);
     } else if (VL >= 192) {
         switch (v) {  // rows per wave (R) and waves per workgroup for a row of >= 192 vectors
             case 0: softmax_kernel<IO, 4, 1, NTL><<<grid, 256, 0, stream>>>(p); break;

@@ -35,6 +35,10 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--variants", default=None)
     ap.add_argument("--rank", default="0/1", help="r/N: time rank r's slice of an N-way sharded config")
+    ap.add_argument("--fragment-gb", type=float, default=0.0,
+                    help="before allocating, map this many GB as --fragment-mib pieces and free every other one, "
+                         "so the big buffers are built from scattered physical memory (TLB / fragment-size study)")
+    ap.add_argument("--fragment-mib", type=int, default=2)
     ap.add_argument("--ws-first", action="store_true",
                     help="allocate the workspace before grads (the order the autograd surface produces)")
     args = ap.parse_args()
@@ -47,6 +51,13 @@ def main():
     DEFAULTS = {k: L.tune(k) for k in ("softmax_variant", "grad_variant", "softmax_grid_per_cu", "grad_grid_per_cu",
                                        "nt_store", "nt_load", "occ_skip")}
     dev = torch.device("cuda:0")
+    keep = []
+    if args.fragment_gb > 0:
+        piece = args.fragment_mib << 20
+        pieces = [torch.empty(piece, dtype=torch.uint8, device=dev) for _ in range(int(args.fragment_gb * 1e9 // piece))]
+        keep = pieces[::2]
+        del pieces
+        torch.cuda.empty_cache()
     rk, wd = (int(x) for x in args.rank.split("/"))
     T, S, V, workload = lengths_for(args.config, rk, wd)
     B = len(T)
@@ -55,7 +66,7 @@ def main():
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     acts = torch.empty((rows, V), dtype=torch.float32, device=dev)
     L.check(lib.mrnnt_synth_acts(ctypes.c_void_p(acts.data_ptr()), 0, rows * V, 0, 1, stream), "synth")
-    MAX_OFF_KB = 8192
+    MAX_OFF_KB = 1 << 20  # grads may be shifted by up to 1 GiB (variant knob "grads_offset_kb")
     if not args.ws_first:
         grads_store = torch.empty(rows * V + MAX_OFF_KB * 256, dtype=torch.float32, device=dev)
     labels = torch.from_numpy(np.random.default_rng(1).integers(1, V, (B, int(S.max()))).astype(np.int32)).to(dev)
@@ -108,7 +119,7 @@ def main():
                 continue  # warm-up round
             for k in times[i]:
                 times[i][k].append(prof[k][0])
-    out = {"alloc": out_alloc, "workload": workload, "rows": rows, "inband_rows": n_band, "V": V, "variants": []}
+    out = {"alloc": out_alloc, "fragment": {"gb": args.fragment_gb, "mib": args.fragment_mib, "held": len(keep)}, "workload": workload, "rows": rows, "inband_rows": n_band, "V": V, "variants": []}
     gb = (n_band + rows) * V * 4 / 1e9
     sb = n_band * V * 4 / 1e9
     for v, t in zip(variants, times):

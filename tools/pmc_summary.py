@@ -34,7 +34,7 @@ def short(name):
 def family(name):
     n = short(name)
     for fam in ("grad_staged_kernel", "grad_rows_kernel", "grad_kernel", "grad_scalar_kernel", "softmax_lean_kernel",
-                "softmax_rows_kernel", "softmax_kernel", "softmax_scalar_kernel", "recursion_kernel", "setup_kernel",
+                "softmax_kernel", "softmax_scalar_kernel", "recursion_kernel", "setup_kernel",
                 "synth_kernel", "pad_zero_kernel", "align_"):
         if n.startswith(fam):
             return fam
@@ -85,7 +85,7 @@ def main():
                "kernels": per}, open(os.path.join(out_dir, "pmc_per_launch.json"), "w"), indent=1)
 
     grad = [k for k in per if family(k) in ("grad_staged_kernel", "grad_kernel", "grad_rows_kernel")]
-    soft = [k for k in per if family(k) in ("softmax_lean_kernel", "softmax_kernel", "softmax_rows_kernel")]
+    soft = [k for k in per if family(k) in ("softmax_lean_kernel", "softmax_kernel")]
     assert grad and soft, per.keys()
     g, s = per[grad[0]], per[soft[0]]
     alg = bench["roofline"]["algorithmic_bytes_per_launch"]
