@@ -199,7 +199,7 @@ def main():
         except Exception:
             traffic = None
 
-    copy_gbps = box_copy_gbps(lib, L, dev)
+    copy_gbps = same_buffers_copy_gbps(lib, L, dev, acts.detach(), acts.grad)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_sample > 0 and args.acts_dtype == "f32":
@@ -232,8 +232,8 @@ def main():
                          "live_rows": live, "inband_rows": n_band,
                          "formula_bytes_per_launch": formula_grad_bytes,
                          "formula_gbps": round(formula_grad_bytes / (g_ms * 1e-3) / 1e9, 1) if g_ms else None,
-                         "box_copy_gbps": copy_gbps,
-                         "frac_of_box_copy": round(achieved / copy_gbps, 4) if achieved and copy_gbps else None},
+                         "copy_gbps_same_buffers": copy_gbps,
+                         "frac_of_copy_same_buffers": round(achieved / copy_gbps, 4) if achieved and copy_gbps else None},
             "kernels": {
                 "log_softmax": {"avg_ms": round(s_ms, 4) if s_ms else None,
                                 "gbps": round(softmax_bytes / (s_ms * 1e-3) / 1e9, 1) if s_ms else None},
@@ -250,19 +250,19 @@ def main():
         dist.destroy_process_group()
 
 
-def box_copy_gbps(lib, L, dev, gib=8, reps=5):
-    """This card's device-copy rate (mrnnt_copy_probe: the gradient pass's access pattern, read + write bytes /
-    time, HIP events on the stream it runs on): HBM rates differ by up to ~15 % between MI355X boxes of the
-    pool (profiles/r01/membench_ceilings*.json), so the gradient kernel's rate is also reported against what a
-    plain copy reaches on the same card. None if memory is short."""
-    n = gib << 30
-    if torch.cuda.mem_get_info(dev)[0] < 2 * n + (4 << 30):
+def same_buffers_copy_gbps(lib, L, dev, src_t, dst_t, gib=8, reps=5):
+    """Device-copy rate on THIS run's own buffers (mrnnt_copy_probe: the gradient pass's access pattern,
+    nontemporal, read + write bytes / time, HIP events on the stream it runs on), acts -> grads, after the timed
+    region. HBM streaming rates depend on where a buffer sits physically: two 52 GB buffers of one process can
+    differ by ~20 % for writes and ~10 % for reads (profiles/r01/grad_placement_study.json), so the gradient
+    kernel is compared with a plain copy between the same two buffers. None if the buffers are too small."""
+    n = min(gib << 30, src_t.numel() * src_t.element_size(), dst_t.numel() * dst_t.element_size())
+    n -= n % 16
+    if n < (1 << 30):
         return None
-    src = torch.zeros(n, dtype=torch.uint8, device=dev)
-    dst = torch.empty_like(src)
     stream = torch.cuda.current_stream(dev)
     sp = ctypes.c_void_p(stream.cuda_stream)
-    run = lambda: L.check(lib.mrnnt_copy_probe(ctypes.c_void_p(dst.data_ptr()), ctypes.c_void_p(src.data_ptr()),  # noqa: E731
+    run = lambda: L.check(lib.mrnnt_copy_probe(ctypes.c_void_p(dst_t.data_ptr()), ctypes.c_void_p(src_t.data_ptr()),  # noqa: E731
                                                n, sp), "copy_probe")
     run()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -272,8 +272,6 @@ def box_copy_gbps(lib, L, dev, gib=8, reps=5):
     e1.record(stream)
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
-    del src, dst
-    torch.cuda.empty_cache()
     return round(2 * n / (ms * 1e-3) / 1e9, 1)
 
 

@@ -119,6 +119,17 @@ RNNTStatus make_plan(const mrnnt_problem *p, Plan *pl) {
     return RNNT_STATUS_SUCCESS;
 }
 
+// A multiplier spreading consecutive column indices over the whole lattice: the first prime >= 0.618 cols
+// that does not divide cols (so i -> i * m mod cols is a permutation).
+int64_t scatter_mul(int64_t cols) {
+    if (cols < 3) return 0;
+    for (int64_t m = std::max<int64_t>(2, (int64_t)(0.6180339887 * (double)cols));; ++m) {
+        bool prime = true;
+        for (int64_t f = 2; f * f <= m && prime; ++f) prime = (m % f) != 0;
+        if (prime && cols % m != 0) return m;
+    }
+}
+
 DevProblem make_dev(const mrnnt_problem *p, const Plan &pl, const void *ws) {
     char *w = static_cast<char *>(const_cast<void *>(ws));
     DevProblem d;
@@ -140,6 +151,7 @@ DevProblem make_dev(const mrnnt_problem *p, const Plan &pl, const void *ws) {
     d.num_rows = pl.N;
     d.pad_T = pl.pad_T;
     d.pad_S1 = pl.pad_S1;
+    d.col_mul = 0;  // set per pass by mrnnt_forward / mrnnt_backward (tuning().col_scatter)
     d.den = reinterpret_cast<float *>(w + pl.off_den);
     d.lpb = reinterpret_cast<double *>(w + pl.off_lpb) + kLpPad;
     d.lpe = reinterpret_cast<double *>(w + pl.off_lpe) + kLpPad;
@@ -248,6 +260,7 @@ RNNTStatus mrnnt_forward(const mrnnt_problem *p, void *ws, size_t ws_bytes, floa
         if (e != hipSuccess) return fail_hip(e, "alignment band kernels");
     }
     const int grid = streaming_grid(pl.cols, tuning().softmax_grid_per_cu);
+    d.col_mul = (tuning().col_scatter & 1) ? scatter_mul(pl.cols) : 0;
     e = timed(K_SOFTMAX, stream, [&] { return launch_softmax(d, pl.elem, grid, stream); });
     if (e != hipSuccess) return fail_hip(e, "log-softmax kernel");
     e = timed(K_DP, stream, [&] { return launch_dp(d, pl.S_max, with_beta ? 1 : 0, costs_dev, stream); });
@@ -264,6 +277,7 @@ RNNTStatus mrnnt_backward(const mrnnt_problem *p, const void *ws, const float *g
     if (!ws) return fail(RNNT_STATUS_INVALID_VALUE, "workspace is null");
     if (!grads) return fail(RNNT_STATUS_INVALID_VALUE, "grads is null");
     DevProblem d = make_dev(p, pl, ws);
+    d.col_mul = (tuning().col_scatter & 2) ? scatter_mul(pl.cols) : 0;
     // grad_variant 3 sweeps rows (packed layout only), the others walk lattice columns
     const int grid = (tuning().grad_variant == 3 && pl.pad_S1 == 0)
                          ? streaming_grid(pl.N, std::max(1, tuning().grad_grid_per_cu))
@@ -563,6 +577,7 @@ int mrnnt_tune(const char *key, int value) {
     Tuning &t = tuning();
     if (!std::strcmp(key, "softmax_variant")) slot = &t.softmax_variant;
     else if (!std::strcmp(key, "grad_variant")) slot = &t.grad_variant;
+    else if (!std::strcmp(key, "col_scatter")) slot = &t.col_scatter;
     else if (!std::strcmp(key, "softmax_grid_per_cu")) slot = &t.softmax_grid_per_cu;
     else if (!std::strcmp(key, "grad_grid_per_cu")) slot = &t.grad_grid_per_cu;
     else if (!std::strcmp(key, "grid_per_cu")) {  // both streaming kernels

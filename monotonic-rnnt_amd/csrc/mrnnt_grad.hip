@@ -130,8 +130,10 @@ __global__ __launch_bounds__(256) void grad_staged_kernel(DevProblem p, const fl
     Cursor cur;
     cur.b = blockIdx.x < p.num_cols ? p.col_b[blockIdx.x] : 0;
     int buf = 0;
-    for (int64_t c = blockIdx.x; c < p.num_cols; c += gridDim.x) {
-        cur.advance(p.col_off, c);
+    for (int64_t ci = blockIdx.x; ci < p.num_cols; ci += gridDim.x) {
+        const int64_t c = p.col_mul ? (ci * p.col_mul) % p.num_cols : ci;
+        if (p.col_mul) cur.b = p.col_b[c];
+        else cur.advance(p.col_off, c);
         const int b = cur.b;
         const int T = p.T[b], S = p.S[b];
         const int t = (int)(c - p.col_off[b]);

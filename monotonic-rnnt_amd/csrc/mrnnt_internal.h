@@ -30,6 +30,8 @@ struct DevProblem {
     int64_t num_cols;           // sum_b T_b
     int64_t num_rows;           // N = sum_b T_b (S_b + 1)
     int64_t pad_T, pad_S1;      // padded acts layout (pad_S1 == 0: packed)
+    int64_t col_mul;            // column visiting order of the streaming kernels: the i-th column visited is
+                                // (i * col_mul) % num_cols (0 = in order; col_mul coprime with num_cols)
     float *den;                 // [N]  log-softmax denominator  -max - log sum exp(z - max)
     double *lpb;                // [N]  z[r, blank] + den[r]
     double *lpe;                // [N]  z[r, label(s)] + den[r]   (s < S)
@@ -82,6 +84,8 @@ struct Tuning {
     int nt_load = 1;              // nontemporal loads of acts (both streaming kernels)
     int occ_skip = 1;             // gradient: no acts read for rows with log-occupancy < kDeadLogOcc
     int joint_nbuf = 2;           // fused joint kernels: LDS buffers for the weight chunks (2 or 3)
+    int col_scatter = 2;          // visit columns in a scattered order (DevProblem::col_mul): bit 0 log-softmax,
+                                  // bit 1 gradient
 };
 Tuning &tuning();
 

@@ -29,8 +29,10 @@ import torch
 
 try:
     from . import _mrnnt_lib as _L
+    from .monotonic_rnnt_op import _lengths_on_device
 except ImportError:
     import _mrnnt_lib as _L
+    from monotonic_rnnt_op import _lengths_on_device
 
 _L.load()
 
@@ -69,8 +71,7 @@ class _JointPrepared:
             raise RuntimeError(f"monotonic_rnnt_joint: expected {B} input/label lengths")
         if B and (self.T_host.max() > enc.size(1) or self.S_host.max() + 1 > pred.size(1)):
             raise RuntimeError("monotonic_rnnt_joint: enc/pred have fewer frames/label positions than the lengths")
-        self.T_dev = input_lengths.detach().to(dev, torch.int32).contiguous()
-        self.S_dev = label_lengths.detach().to(dev, torch.int32).contiguous()
+        self.T_dev, self.S_dev = _lengths_on_device(input_lengths, label_lengths, self.T_host, self.S_host, dev)
         lab = labels.detach().to(dev, torch.int32)
         if lab.dim() == 1:
             lab = lab.view(B, -1)

@@ -47,6 +47,16 @@ def _ptr(t: Optional[torch.Tensor]):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
+def _lengths_on_device(input_lengths, label_lengths, T_host, S_host, dev):
+    """Device int32 copies of the lengths: device inputs are converted in place on the GPU; host inputs go up
+    as one pinned, non-blocking copy (stream-ordered before the kernels, no host wait)."""
+    if input_lengths.is_cuda or label_lengths.is_cuda:
+        return (input_lengths.detach().to(dev, torch.int32).contiguous().view(-1),
+                label_lengths.detach().to(dev, torch.int32).contiguous().view(-1))
+    ts = torch.from_numpy(np.stack([T_host, S_host])).pin_memory().to(dev, non_blocking=True)
+    return ts[0], ts[1]
+
+
 class _Prepared:
     """Device/host views of one call's inputs plus the filled mrnnt_problem."""
 
@@ -63,13 +73,15 @@ class _Prepared:
         dev = acts.device
         self.acts = acts.contiguous()
         B = labels.size(0)
+        # The plan (sizes, validation) needs the lengths on the host and the kernels need them on the device.
+        # Device lengths are read back (a sync, as the reference's cudaMemcpy, gpu_workspace_manager.h:63-69);
+        # host lengths go up in one pinned, non-blocking copy, so the call never waits for the GPU.
         self.T_host = np.ascontiguousarray(input_lengths.detach().to("cpu", torch.int32).numpy()).reshape(-1)
         self.S_host = np.ascontiguousarray(label_lengths.detach().to("cpu", torch.int32).numpy()).reshape(-1)
         if self.T_host.size != B or self.S_host.size != B:
             raise RuntimeError(f"monotonic_rnnt: expected {B} input/label lengths, "
                                f"got {self.T_host.size}/{self.S_host.size}")
-        self.T_dev = input_lengths.detach().to(dev, torch.int32).contiguous()
-        self.S_dev = label_lengths.detach().to(dev, torch.int32).contiguous()
+        self.T_dev, self.S_dev = _lengths_on_device(input_lengths, label_lengths, self.T_host, self.S_host, dev)
         lab = labels.detach().to(dev, torch.int32)
         if lab.dim() == 1:
             lab = lab.view(B, -1)

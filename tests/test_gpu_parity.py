@@ -255,6 +255,9 @@ def test_config_c2_vs_oracle(op, dev):
     {"softmax_variant": 13},
     {"softmax_variant": 14, "softmax_grid_per_cu": 2, "nt_load": 0},
     {"softmax_variant": 15},
+    {"col_scatter": 3},
+    {"col_scatter": 0, "grad_variant": 6},
+    {"col_scatter": 3, "grad_grid_per_cu": 0, "softmax_grid_per_cu": 4},
     {"grad_variant": 5},
     {"grad_variant": 6, "grad_grid_per_cu": 3, "nt_load": 0, "nt_store": 0},
 ])
@@ -262,7 +265,7 @@ def test_every_kernel_variant_matches_oracle(op, dev, knobs):
     """All launch variants selectable through mrnnt_tune compute the same result (alignment included)."""
     import _mrnnt_lib as L
     saved = {k: L.tune(k) for k in ("softmax_variant", "grad_variant", "softmax_grid_per_cu",
-                                    "grad_grid_per_cu", "nt_store", "nt_load")}
+                                    "grad_grid_per_cu", "nt_store", "nt_load", "col_scatter")}
     try:
         for k, v in knobs.items():
             assert L.tune(k, v) >= 0

@@ -39,6 +39,9 @@ def main():
                     help="before allocating, map this many GB as --fragment-mib pieces and free every other one, "
                          "so the big buffers are built from scattered physical memory (TLB / fragment-size study)")
     ap.add_argument("--fragment-mib", type=int, default=2)
+    ap.add_argument("--buffers", type=int, default=1,
+                    help="allocate this many acts and grads buffers (variant knobs acts_buf / grads_buf pick one): "
+                         "does the gradient kernel's speed depend on where a buffer sits?")
     ap.add_argument("--ws-first", action="store_true",
                     help="allocate the workspace before grads (the order the autograd surface produces)")
     args = ap.parse_args()
@@ -49,7 +52,7 @@ def main():
 
     lib = L.load()
     DEFAULTS = {k: L.tune(k) for k in ("softmax_variant", "grad_variant", "softmax_grid_per_cu", "grad_grid_per_cu",
-                                       "nt_store", "nt_load", "occ_skip")}
+                                       "nt_store", "nt_load", "occ_skip", "col_scatter")}
     dev = torch.device("cuda:0")
     keep = []
     if args.fragment_gb > 0:
@@ -85,6 +88,10 @@ def main():
     if args.ws_first:
         grads_store = torch.empty(rows * V + MAX_OFF_KB * 256, dtype=torch.float32, device=dev)
     grads_holder = {"t": grads_store[: rows * V].view(rows, V)}
+    acts_list, grads_list = [acts], [grads_store]
+    for _ in range(args.buffers - 1):
+        acts_list.append(acts.clone())
+        grads_list.append(torch.empty(rows * V, dtype=torch.float32, device=dev))
     out_alloc = {"acts": acts.data_ptr(), "grads": grads_store.data_ptr(), "ws": ws.data_ptr()}
 
     def run_once():
@@ -99,14 +106,18 @@ def main():
         for i, v in enumerate(variants):
             for k, val in DEFAULTS.items():
                 L.tune(k, val)
+            gb_i, ab_i = int(v.get("grads_buf", 0)), int(v.get("acts_buf", 0))
+            p.acts = acts_list[ab_i].data_ptr()
             for k, val in v.items():
+                if k in ("grads_buf", "acts_buf"):
+                    continue
                 if k == "grads_offset_kb":
                     o = int(val) * 256
                     grads_holder["t"] = grads_store[o: o + rows * V].view(rows, V)
                     continue
                 assert L.tune(k, val) >= 0, k
             if "grads_offset_kb" not in v:
-                grads_holder["t"] = grads_store[: rows * V].view(rows, V)
+                grads_holder["t"] = grads_list[gb_i][: rows * V].view(rows, V)
             L.profile_enable(True)
             run_once()
             prof = L.profile_read()
@@ -119,6 +130,8 @@ def main():
                 continue  # warm-up round
             for k in times[i]:
                 times[i][k].append(prof[k][0])
+    out_alloc["acts_bufs"] = [t.data_ptr() for t in acts_list]
+    out_alloc["grads_bufs"] = [t.data_ptr() for t in grads_list]
     out = {"alloc": out_alloc, "fragment": {"gb": args.fragment_gb, "mib": args.fragment_mib, "held": len(keep)}, "workload": workload, "rows": rows, "inband_rows": n_band, "V": V, "variants": []}
     gb = (n_band + rows) * V * 4 / 1e9
     sb = n_band * V * 4 / 1e9
