@@ -73,11 +73,11 @@ hipError_t launch_zero(void *ptr, size_t bytes, hipStream_t stream);
 
 // Launch-shape knobs (experiment hook: mrnnt_tune in mrnnt_capi.cpp). Defaults are the tuned values.
 struct Tuning {
-    int softmax_variant = 13;     // log-softmax kernel: 13/14/15 -> lean kernel with 2/1/4 rows per wave (rows of
-                                  // >= 96 vectors); 0/2/3.. -> first kernel (shuffle butterflies) with 1/2/3.. rows
-    int grad_variant = 5;         // gradient kernel: 5/6 -> staged coefficients, 1/2 rows per wave (rows of >= 96
-                                  // vectors); 0/2 -> per-row coefficients, 1/2 rows; 3 -> row-stride sweep (packed);
-                                  // 4 -> zero rows then live rows
+    int softmax_variant = 13;     // log-softmax kernel: 13/14/15 -> lean kernel with 2 (4 for rows of < 96
+                                  // vectors) / 1 / 4 rows per wave; 0/2 -> first kernel (shuffle butterflies), 1/2 rows
+    int grad_variant = 5;         // gradient kernel: 5 -> staged coefficients (1 / 2 rows per wave for rows of
+                                  // >= 192 / >= 96 vectors; shorter rows: per-row kernel, 4 rows), 6 -> staged, 2 rows;
+                                  // 0 / 2 -> per-row coefficients, default / 2 rows; 3 -> row-stride sweep (packed)
     int softmax_grid_per_cu = 0;  // workgroups (of 4 waves) per CU; 0 = one workgroup per lattice column
     int grad_grid_per_cu = 32;    // same for the gradient kernel
     int nt_store = 1;             // nontemporal stores of grads

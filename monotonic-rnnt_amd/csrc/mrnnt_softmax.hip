@@ -31,8 +31,9 @@ __device__ __forceinline__ void write_row(const DevProblem &p, int64_t row, floa
 
 // Vector path: V % E == 0, 16-byte aligned rows. U = vector loads per lane per chunk (a chunk covers
 // 64*U*E elements), R = rows a wave reduces at once (U*R vector loads in flight per lane).
-template <class IO, int U, int R, bool NTL, int NW = 4, int OCC = 1>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(OCC))) void softmax_kernel(DevProblem p) {
+template <class IO, int U, int R, bool NTL>
+__global__ __launch_bounds__(256) void softmax_kernel(DevProblem p) {
+    constexpr int NW = 4;
     constexpr int E = IO::E;
     typedef typename IO::V Vec;
     const int lane = threadIdx.x & 63;
@@ -295,48 +296,34 @@ __global__ __launch_bounds__(256) void softmax_scalar_kernel(DevProblem p) {
     }
 }
 
+template <class IO, bool NTL, int U>
+static void launch_u(const DevProblem &p, int grid, hipStream_t stream) {
+    const int VL = p.V / IO::E;
+    const int v = tuning().softmax_variant;
+    const bool full = VL % (64 * U) == 0;
+    if (v == 0 || v == 2) {  // first kernel (shuffle butterflies), 1 or 2 rows per wave
+        if (v == 0) softmax_kernel<IO, U, 1, NTL><<<grid, 256, 0, stream>>>(p);
+        else softmax_kernel<IO, U, 2, NTL><<<grid, 256, 0, stream>>>(p);
+        return;
+    }
+    // lean kernel: 13 -> 2 rows per wave (4 for rows of < 96 vectors), 14 -> 1, 15 -> 4
+    const int R = v == 14 ? 1 : (v == 15 || (v == 13 && U == 1)) ? 4 : 2;
+#define MRNNT_LEAN(RR)                                                                              \
+    (full ? softmax_lean_kernel<IO, U, RR, NTL, true><<<grid, 256, 0, stream>>>(p)                 \
+          : softmax_lean_kernel<IO, U, RR, NTL, false><<<grid, 256, 0, stream>>>(p))
+    if (R == 1) MRNNT_LEAN(1);
+    else if (R == 4) MRNNT_LEAN(4);
+    else MRNNT_LEAN(2);
+#undef MRNNT_LEAN
+}
+
+// U = 16-byte loads per lane per chunk: a 4 KiB chunk for rows of >= 192 vectors, 2 KiB for >= 96, else 1 KiB
 template <class IO, bool NTL>
 static void launch_vec(const DevProblem &p, int grid, hipStream_t stream) {
     const int VL = p.V / IO::E;
-    const int v = tuning().softmax_variant;
-    if (v >= 13 && v <= 15 && VL >= 96) {  // lean kernels: U vectors per lane per chunk, R = 2 / 1 / 4 rows
-        const int U = VL >= 192 ? 4 : 2;
-        const bool full = VL % (64 * U) == 0;
-#define MRNNT_LEAN(UU, RR)                                                                          \
-    (full ? softmax_lean_kernel<IO, UU, RR, NTL, true><<<grid, 256, 0, stream>>>(p)                \
-          : softmax_lean_kernel<IO, UU, RR, NTL, false><<<grid, 256, 0, stream>>>(p))
-        if (U == 4) {
-            if (v == 14) MRNNT_LEAN(4, 1);
-            else if (v == 15) MRNNT_LEAN(4, 4);
-            else MRNNT_LEAN(4, 2);
-        } else {
-            if (v == 14) MRNNT_LEAN(2, 1);
-            else if (v == 15) MRNNT_LEAN(2, 4);
-            else MRNNT_LEAN(2, 2);
-        }
-#undef MRNNT_LEAN
-    } else if (VL >= 192) {
-        switch (v) {  // rows per wave (R) and waves per workgroup for a row of >= 192 vectors
-            case 0: softmax_kernel<IO, 4, 1, NTL><<<grid, 256, 0, stream>>>(p); break;
-            case 3: softmax_kernel<IO, 4, 3, NTL><<<grid, 256, 0, stream>>>(p); break;
-            case 4: softmax_kernel<IO, 4, 4, NTL><<<grid, 256, 0, stream>>>(p); break;
-            case 5: softmax_kernel<IO, 4, 2, NTL, 8><<<grid, 512, 0, stream>>>(p); break;
-            case 6: softmax_kernel<IO, 4, 1, NTL, 8><<<grid, 512, 0, stream>>>(p); break;
-            case 7: softmax_kernel<IO, 2, 4, NTL><<<grid, 256, 0, stream>>>(p); break;
-            case 8: softmax_kernel<IO, 4, 1, NTL, 4, 8><<<grid, 256, 0, stream>>>(p); break;
-            case 9: softmax_kernel<IO, 4, 2, NTL, 4, 6><<<grid, 256, 0, stream>>>(p); break;
-            case 10: softmax_kernel<IO, 2, 2, NTL, 4, 8><<<grid, 256, 0, stream>>>(p); break;
-            default: softmax_kernel<IO, 4, 2, NTL><<<grid, 256, 0, stream>>>(p); break;
-        }
-    } else if (VL >= 96) {  // e.g. V = 1024 in bf16: 2 KiB rows
-        // default: one row per wave at 8 waves per SIMD (bf16 V = 1024: 3 % over two rows at 4 waves)
-        if (v == 4) softmax_kernel<IO, 2, 4, NTL><<<grid, 256, 0, stream>>>(p);
-        else if (v == 3) softmax_kernel<IO, 2, 3, NTL><<<grid, 256, 0, stream>>>(p);
-        else if (v == 0) softmax_kernel<IO, 2, 2, NTL><<<grid, 256, 0, stream>>>(p);
-        else softmax_kernel<IO, 2, 1, NTL, 4, 8><<<grid, 256, 0, stream>>>(p);
-    } else {
-        softmax_kernel<IO, 1, 4, NTL><<<grid, 256, 0, stream>>>(p);
-    }
+    if (VL >= 192) launch_u<IO, NTL, 4>(p, grid, stream);
+    else if (VL >= 96) launch_u<IO, NTL, 2>(p, grid, stream);
+    else launch_u<IO, NTL, 1>(p, grid, stream);
 }
 
 template <class IO>

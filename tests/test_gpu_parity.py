@@ -251,7 +251,7 @@ def test_config_c2_vs_oracle(op, dev):
     {"softmax_variant": 0, "grad_variant": 2, "nt_load": 0, "nt_store": 0},
     {"softmax_variant": 2, "grad_variant": 3, "softmax_grid_per_cu": 5, "grad_grid_per_cu": 7},
     {"softmax_variant": 0, "grad_variant": 3, "grid_per_cu": 16, "nt_store": 1, "nt_load": 0},
-    {"softmax_variant": 2, "grad_variant": 4, "softmax_grid_per_cu": 3, "grad_grid_per_cu": 5},
+    {"softmax_variant": 2, "grad_variant": 6, "softmax_grid_per_cu": 3, "grad_grid_per_cu": 5},
     {"softmax_variant": 13},
     {"softmax_variant": 14, "softmax_grid_per_cu": 2, "nt_load": 0},
     {"softmax_variant": 15},
