@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <algorithm>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 typedef float f4 __attribute__((ext_vector_type(4)));
@@ -159,7 +160,50 @@ static float time_ms(F f, int reps) {
     return ts[ts.size() / 2];
 }
 
+// --buffers K GIB SUB: K buffers of GIB GiB each; per buffer the streaming read / write rates of the whole buffer
+// and the nontemporal write rate of every SUB-GiB sub-range (does a buffer's speed depend on where it sits, and
+// is a slow buffer slow everywhere?)
+static int buffers_mode(int K, double gib, double sub) {
+    const int64_t n = (int64_t)(gib * (1 << 30)) / 16;
+    const int64_t ns = (int64_t)(sub * (1 << 30)) / 16;
+    int cus = 0;
+    CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    const int grid = cus * 32;
+    std::vector<f4 *> buf(K);
+    float *out;
+    CHECK(hipMalloc(&out, 16));
+    for (int k = 0; k < K; ++k) {
+        CHECK(hipMalloc(&buf[k], n * 16));
+        k_fill<<<4096, 256>>>(buf[k], n);
+    }
+    CHECK(hipDeviceSynchronize());
+    const double bytes = (double)n * 16;
+    std::printf("{\"gib\": %.1f, \"sub_gib\": %.1f, \"buffers\": [\n", gib, sub);
+    for (int k = 0; k < K; ++k) {
+        f4 *a = buf[k];
+        const float r_nt = time_ms([&] { k_read_nt<8><<<grid, 256>>>(a, n, out); }, 3);
+        const float r_pl = time_ms([&] { k_read<8><<<grid, 256>>>(a, n, out); }, 3);
+        const float w_nt = time_ms([&] { k_write<1><<<grid, 256>>>(a, n); }, 3);
+        const float w_pl = time_ms([&] { k_write_plain<1><<<grid, 256>>>(a, n); }, 3);
+        const float c_nt = time_ms([&] { k_copy<4, true><<<grid, 256>>>(buf[(k + 1) % K], a, n); }, 3);
+        std::printf("%s {\"ptr\": \"%p\", \"read_nt\": %.1f, \"read\": %.1f, \"write_nt\": %.1f, \"write\": %.1f, "
+                    "\"copy_in_nt\": %.1f, \"sub_write_nt\": [",
+                    k ? ",\n" : "", (void *)a, bytes / (r_nt * 1e-3) / 1e9, bytes / (r_pl * 1e-3) / 1e9,
+                    bytes / (w_nt * 1e-3) / 1e9, bytes / (w_pl * 1e-3) / 1e9, 2 * bytes / (c_nt * 1e-3) / 1e9);
+        for (int64_t o = 0; o + ns <= n; o += ns) {
+            const float ms = time_ms([&] { k_write<1><<<grid, 256>>>(a + o, ns); }, 3);
+            std::printf("%s%.0f", o ? ", " : "", (double)ns * 16 / (ms * 1e-3) / 1e9);
+        }
+        std::printf("]}");
+    }
+    std::printf("\n]}\n");
+    return 0;
+}
+
 int main(int argc, char **argv) {
+    if (argc > 1 && std::string(argv[1]) == "--buffers")
+        return buffers_mode(argc > 2 ? std::atoi(argv[2]) : 4, argc > 3 ? std::atof(argv[3]) : 48.0,
+                            argc > 4 ? std::atof(argv[4]) : 4.0);
     const double gib = argc > 1 ? std::atof(argv[1]) : 16.0;
     const int64_t n = (int64_t)(gib * (1 << 30)) / 16;
     int cus = 0;
