@@ -242,6 +242,26 @@ def test_config_c2_vs_oracle(op, dev):
     assert_grads(g, gr)
 
 
+def test_accuracy_against_reference_fp32_noise(op, dev):
+    """configs[1] shape: distance of this path and of cpu_rnnt.h<float> (its restatement, pinned bit-exact) to the
+    fp64 golden. The HIP path (fp64 recursion state) must be at least as close as the reference's own
+    fp32 CPU computation."""
+    B, Tn, Sn, V = 16, 200, 40, 256
+    T = np.full(B, Tn, np.int32)
+    S = np.full(B, Sn, np.int32)
+    rows = int(np.sum(T * (S + 1)))
+    acts = O.synth_acts(0, rows * V, seed=0).reshape(rows, V)
+    labels = np.random.default_rng(1).integers(1, V, (B, Sn)).astype(np.int32)
+    c, g = run_gpu(op, dev, acts, labels, T, S)
+    c64, g64 = O.oracle_rnnt(acts, labels, T, S, num_threads=16)
+    c32, g32 = O.oracle_rnnt(acts, labels, T, S, precision="f32", num_threads=16)
+    ours = (float(np.max(np.abs(c - c64) / np.abs(c64))), float(np.max(np.abs(g - g64))))
+    ref32 = (float(np.max(np.abs(c32 - c64) / np.abs(c64))), float(np.max(np.abs(g32 - g64))))
+    print(f"\naccuracy vs cpu_rnnt.h<double>: HIP path costs rel {ours[0]:.3e} grads abs {ours[1]:.3e}; "
+          f"cpu_rnnt.h<float> costs rel {ref32[0]:.3e} grads abs {ref32[1]:.3e}")
+    assert ours[0] <= max(ref32[0], 1e-6) and ours[1] <= max(ref32[1], 1e-6), (ours, ref32)
+
+
 @pytest.mark.parametrize("knobs", [
     {"softmax_variant": 0, "grad_variant": 0, "grid_per_cu": 8, "nt_store": 1},
     {"softmax_variant": 2, "grad_variant": 2, "grid_per_cu": 0, "nt_store": 0},

@@ -160,10 +160,44 @@ static float time_ms(F f, int reps) {
     return ts[ts.size() / 2];
 }
 
-// --buffers K GIB SUB: K buffers of GIB GiB each; per buffer the streaming read / write rates of the whole buffer
+// write patterns for the buffer study: each wave writes whole 4 KiB rows (the gradient kernel's store shape);
+// rows visited in order (grid-stride over rows) or with the row index multiplied by an odd constant mod rows
+// (scattered); and 2 MiB pages visited in a scattered order, each page written by one workgroup
+__global__ __launch_bounds__(256) void k_write_rows(f4 *__restrict__ b, int64_t rows, int64_t mul) {
+    const int lane = threadIdx.x & 63;
+    const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (int64_t)gridDim.x * 4;
+    const f4 z = (f4){0.f, 0.f, 0.f, 0.f};
+    for (int64_t r = gw; r < rows; r += nw) {
+        const int64_t row = mul ? (r * mul) % rows : r;
+        f4 *o = b + row * 256;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) __builtin_nontemporal_store(z, o + lane + 64 * u);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_write_pages(f4 *__restrict__ b, int64_t pages, int64_t mul) {
+    const f4 z = (f4){0.f, 0.f, 0.f, 0.f};
+    for (int64_t pg = blockIdx.x; pg < pages; pg += gridDim.x) {
+        f4 *o = b + ((pg * mul) % pages) * (int64_t)(2 << 20) / 16;
+        for (int i = threadIdx.x; i < (2 << 20) / 16; i += 256) __builtin_nontemporal_store(z, o + i);
+    }
+}
+
+// --buffers K GIB SUB [FRAG]: K buffers of GIB GiB each; per buffer the streaming read / write rates of the whole buffer
 // and the nontemporal write rate of every SUB-GiB sub-range (does a buffer's speed depend on where it sits, and
 // is a slow buffer slow everywhere?)
-static int buffers_mode(int K, double gib, double sub) {
+static int buffers_mode(int K, double gib, double sub, double frag_gib) {
+    // optional: map frag_gib GiB as 2 MiB pieces and free every other one first, so the buffers are built from
+    // scattered 2 MiB physical pieces
+    std::vector<void *> keep;
+    if (frag_gib > 0) {
+        std::vector<void *> pieces((size_t)(frag_gib * 512));
+        for (auto &q : pieces) CHECK(hipMalloc(&q, 2 << 20));
+        for (size_t i = 0; i < pieces.size(); ++i) {
+            if (i & 1) CHECK(hipFree(pieces[i]));
+            else keep.push_back(pieces[i]);
+        }
+    }
     const int64_t n = (int64_t)(gib * (1 << 30)) / 16;
     const int64_t ns = (int64_t)(sub * (1 << 30)) / 16;
     int cus = 0;
@@ -186,10 +220,16 @@ static int buffers_mode(int K, double gib, double sub) {
         const float w_nt = time_ms([&] { k_write<1><<<grid, 256>>>(a, n); }, 3);
         const float w_pl = time_ms([&] { k_write_plain<1><<<grid, 256>>>(a, n); }, 3);
         const float c_nt = time_ms([&] { k_copy<4, true><<<grid, 256>>>(buf[(k + 1) % K], a, n); }, 3);
+        const int64_t rows = n / 256, pages = n * 16 / (2 << 20);
+        const float w_rows = time_ms([&] { k_write_rows<<<grid, 256>>>(a, rows, 0); }, 3);
+        const float w_rows_sc = time_ms([&] { k_write_rows<<<grid, 256>>>(a, rows, 7919); }, 3);
+        const float w_pages_sc = time_ms([&] { k_write_pages<<<cus * 8, 256>>>(a, pages, 4093); }, 3);
         std::printf("%s {\"ptr\": \"%p\", \"read_nt\": %.1f, \"read\": %.1f, \"write_nt\": %.1f, \"write\": %.1f, "
-                    "\"copy_in_nt\": %.1f, \"sub_write_nt\": [",
+                    "\"copy_in_nt\": %.1f, \"write_rows\": %.1f, \"write_rows_scattered\": %.1f, "
+                    "\"write_pages_scattered\": %.1f, \"sub_write_nt\": [",
                     k ? ",\n" : "", (void *)a, bytes / (r_nt * 1e-3) / 1e9, bytes / (r_pl * 1e-3) / 1e9,
-                    bytes / (w_nt * 1e-3) / 1e9, bytes / (w_pl * 1e-3) / 1e9, 2 * bytes / (c_nt * 1e-3) / 1e9);
+                    bytes / (w_nt * 1e-3) / 1e9, bytes / (w_pl * 1e-3) / 1e9, 2 * bytes / (c_nt * 1e-3) / 1e9,
+                    bytes / (w_rows * 1e-3) / 1e9, bytes / (w_rows_sc * 1e-3) / 1e9, bytes / (w_pages_sc * 1e-3) / 1e9);
         for (int64_t o = 0; o + ns <= n; o += ns) {
             const float ms = time_ms([&] { k_write<1><<<grid, 256>>>(a + o, ns); }, 3);
             std::printf("%s%.0f", o ? ", " : "", (double)ns * 16 / (ms * 1e-3) / 1e9);
@@ -203,7 +243,7 @@ static int buffers_mode(int K, double gib, double sub) {
 int main(int argc, char **argv) {
     if (argc > 1 && std::string(argv[1]) == "--buffers")
         return buffers_mode(argc > 2 ? std::atoi(argv[2]) : 4, argc > 3 ? std::atof(argv[3]) : 48.0,
-                            argc > 4 ? std::atof(argv[4]) : 4.0);
+                            argc > 4 ? std::atof(argv[4]) : 4.0, argc > 5 ? std::atof(argv[5]) : 0.0);
     const double gib = argc > 1 ? std::atof(argv[1]) : 16.0;
     const int64_t n = (int64_t)(gib * (1 << 30)) / 16;
     int cus = 0;
