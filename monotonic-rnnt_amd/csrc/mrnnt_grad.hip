@@ -99,7 +99,7 @@ __global__ __launch_bounds__(256) void grad_kernel(DevProblem p, const float *__
     }
 }
 
-// Staged-coefficient kernel (grad_variant 5/6: R = 1 / 2 rows per wave). Work unit = a segment of up to 256
+// Staged-coefficient kernel (grad_variant 5, the default, and 6: 2 rows per wave). Work unit = a segment of up to 256
 // rows of one lattice column. Phase A: one row per thread, the row's coefficients (row_coef: alpha/beta/den/lp
 // read as coalesced vectors along s, the two fp64 exps lane-parallel) go to an LDS slot {c2, cb, ce, label|dead}.
 // Phase B: the waves stream the segment's rows; a row's acts loads wait only for one broadcast LDS read, not for

@@ -129,7 +129,7 @@ __device__ __forceinline__ float lane_pick(const float (&x)[N], int k) {
     return v[k];
 }
 
-// Lean variant (softmax_variant 2 default for rows of >= 192 vectors; 13/14 select R = 1 / 4): the same
+// Lean kernel (softmax_variant 13, the default; 14 / 15 select R = 1 / 4 rows per wave): the same
 // column walk and online per-lane (max, sum) as softmax_kernel, with the per-row overhead taken off the
 // vector pipe -- (max, sum) merged by DPP reductions into wave-uniform scalars (no ds_bpermute butterfly, one
 // exp per lane instead of two per step), blank / label logits read with a uniform indexed move + v_readlane
