@@ -198,6 +198,181 @@ __global__ __launch_bounds__(64 * NW) void recursion_kernel(DevProblem p, int wi
 }
 
 
+// Halo recursion (64 < S+1 <= 8 * (64 - HL)): NW waves, one cell per lane, and no per-step barrier. Wave w
+// owns C = 64 - HL consecutive cells and its remaining HL lanes recompute the HL cells next to them that the
+// neighbouring wave owns (alpha: the cells below, beta: the cells above). Those halo lanes lose one valid lane
+// per step (their outer neighbour is not in the wave), so the own cells stay exact for HL steps; then the
+// neighbour's HL boundary cells are copied in through LDS (one barrier per HL steps instead of one per step).
+template <int D, int NW, int HL, bool BAND>
+__device__ __forceinline__ void alpha_pass_halo(const DevProblem &p, int b, float *__restrict__ costs,
+                                                double (*xh)[8][HL > 0 ? HL : 1]) {
+    static_assert((HL == 0 ? NW == 1 : D % HL == 0) && NW <= 8,
+                  "halo refreshes at prefetch-block positions (HL = 0: one wave, no halo); xh sized for <= 8 waves");
+    constexpr int C = 64 - HL;
+    constexpr int HLD = HL > 0 ? HL : 1;  // divisor for the (compiled-out when HL == 0) refresh logic
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int T = p.T[b], S = p.S[b], W = S + 1;
+    const int64_t r0 = p.row_off[b], c0 = p.col_off[b];
+    const int s0 = wave * C - HL + lane;  // negative for the halo lanes of wave 0 (always out of band)
+    const bool own = lane >= HL && s0 < W;
+
+    double a = (s0 == 0) ? 0.0 : NEG_INF_D;
+    double pb[D], pe[D];
+    int mn[D], mx[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        const int tt = min(d, T - 1);
+        pb[d] = p.lpb[r0 + (int64_t)tt * W + s0];
+        pe[d] = p.lpe[r0 + (int64_t)tt * W + s0 - 1];
+        mn[d] = BAND ? p.min_s[c0 + tt] : 0;
+        mx[d] = BAND ? p.max_s[c0 + tt] : S;
+    }
+    auto step = [&](int t, int d) {
+        const int lo = max(max(t - (T - 1 - S), mn[d]), 0);
+        const int hi = min(min(t + 1, S), mx[d]);
+        double carry = dpp_shr1(a);  // lane 0: garbage that only ever feeds halo lanes ...
+        if (HL == 0 && lane == 0) carry = NEG_INF_D;  // ... or, with no halo, alpha(t-1, -1)
+        const double v = lse2(a + pb[d], carry + pe[d]);
+        a = (s0 >= lo && s0 <= hi) ? v : NEG_INF_D;
+        if (own) p.alpha[r0 + (int64_t)t * W + s0] = a;
+        const int tn = min(t + D, T - 1);
+        pb[d] = p.lpb[r0 + (int64_t)tn * W + s0];
+        pe[d] = p.lpe[r0 + (int64_t)tn * W + s0 - 1];
+        mn[d] = BAND ? p.min_s[c0 + tn] : 0;
+        mx[d] = BAND ? p.max_s[c0 + tn] : S;
+    };
+    // whole blocks of D == HL steps (no early exit inside: the vmcnt waits stay D steps deep), a halo refresh from
+    // the wave below (its top HL own cells) after each, then the tail
+    int t0 = 0;
+    for (; t0 + D <= T; t0 += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            step(t0 + d, d);
+            if (HL > 0 && (d + 1) % HLD == 0 && (d + 1 < D || t0 + D < T)) {
+                const int par = ((t0 + d) / HLD) & 1;
+                if (lane >= C) xh[par][wave][lane - C] = a;
+                __syncthreads();
+                if (wave > 0 && lane < HL) a = xh[par][wave - 1][lane];
+            }
+        }
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        if (t0 + d >= T) break;
+        step(t0 + d, d);
+        if (HL > 0 && (d + 1) % HLD == 0 && t0 + d + 1 < T) {
+            const int par = ((t0 + d) / HLD) & 1;
+            if (lane >= C) xh[par][wave][lane - C] = a;
+            __syncthreads();
+            if (wave > 0 && lane < HL) a = xh[par][wave - 1][lane];
+        }
+    }
+    if (own && s0 == S) {
+        p.ll[b] = a;
+        if (costs) costs[b] = (float)(-a);
+    }
+}
+
+template <int D, int NW, int HL, bool BAND>
+__device__ __forceinline__ void beta_pass_halo(const DevProblem &p, int b, double (*xh)[8][HL > 0 ? HL : 1]) {
+    static_assert((HL == 0 ? NW == 1 : D % HL == 0) && NW <= 8,
+                  "halo refreshes at prefetch-block positions (HL = 0: one wave, no halo); xh sized for <= 8 waves");
+    constexpr int C = 64 - HL;
+    constexpr int HLD = HL > 0 ? HL : 1;  // divisor for the (compiled-out when HL == 0) refresh logic
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int T = p.T[b], S = p.S[b], W = S + 1;
+    const int64_t r0 = p.row_off[b], c0 = p.col_off[b];
+    const int s0 = wave * C + lane;  // lanes >= C: halo, the first HL cells of the wave above
+    const bool own = lane < C && s0 < W;
+
+    double bn = (s0 == S) ? 0.0 : NEG_INF_D;  // beta(T, s)
+    double pb[D], pe[D];
+    int mn[D], mx[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        const int tt = max(T - 1 - d, 0);
+        pb[d] = p.lpb[r0 + (int64_t)tt * W + s0];
+        pe[d] = p.lpe[r0 + (int64_t)tt * W + s0];
+        mn[d] = (BAND && tt > 0) ? p.min_s[c0 + tt - 1] : 0;
+        mx[d] = (BAND && tt > 0) ? p.max_s[c0 + tt - 1] : S;
+    }
+    auto step = [&](int t, int d) {
+        int lo, hi;
+        if (t == 0) {
+            lo = 0;
+            hi = 0;
+        } else {
+            lo = max(max(t - (T - S), mn[d]), 0);
+            hi = min(min(t, S), mx[d]);
+        }
+        double carry = dpp_shl1(bn);  // lane 63: garbage that only ever feeds halo lanes ...
+        if (HL == 0 && lane == 63) carry = NEG_INF_D;  // ... or, with no halo, beta(t+1, 64) (S + 1 <= 64)
+        const double v = lse2(bn + pb[d], carry + pe[d]);
+        bn = (s0 >= lo && s0 <= hi) ? v : NEG_INF_D;
+        if (own) p.beta[r0 + (int64_t)t * W + s0] = bn;
+        const int tn = max(t - D, 0);
+        pb[d] = p.lpb[r0 + (int64_t)tn * W + s0];
+        pe[d] = p.lpe[r0 + (int64_t)tn * W + s0];
+        mn[d] = (BAND && tn > 0) ? p.min_s[c0 + tn - 1] : 0;
+        mx[d] = (BAND && tn > 0) ? p.max_s[c0 + tn - 1] : S;
+    };
+    int t0 = T - 1;
+    for (; t0 - D + 1 >= 0; t0 -= D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            step(t0 - d, d);
+            if (HL > 0 && (d + 1) % HLD == 0 && (d + 1 < D || t0 - D >= 0)) {  // refresh from the wave above
+                const int par = ((T - 1 - t0 + d) / HLD) & 1;
+                if (lane < HL) xh[par][wave][lane] = bn;
+                __syncthreads();
+                if (wave < NW - 1 && lane >= C) bn = xh[par][wave + 1][lane - C];
+            }
+        }
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        if (t0 - d < 0) break;
+        step(t0 - d, d);
+        if (HL > 0 && (d + 1) % HLD == 0 && t0 - d - 1 >= 0) {
+            const int par = ((T - 1 - t0 + d) / HLD) & 1;
+            if (lane < HL) xh[par][wave][lane] = bn;
+            __syncthreads();
+            if (wave < NW - 1 && lane >= C) bn = xh[par][wave + 1][lane - C];
+        }
+    }
+    if (threadIdx.x == 0) p.llb[b] = bn;
+}
+
+template <int D, int NW, int HL, bool BAND>
+__global__ __launch_bounds__(64 * NW) void recursion_halo_kernel(DevProblem p, int with_beta,
+                                                                 float *__restrict__ costs) {
+    __shared__ double xh[2][8][HL > 0 ? HL : 1];
+    const int b = with_beta ? (int)(blockIdx.x >> 1) : (int)blockIdx.x;
+    const bool bwd = with_beta && (blockIdx.x & 1);
+    if (bwd)
+        beta_pass_halo<D, NW, HL, BAND>(p, b, xh);
+    else
+        alpha_pass_halo<D, NW, HL, BAND>(p, b, costs, xh);
+}
+
+template <int NW, int HL = 8>
+static void launch_halo(const DevProblem &p, int with_beta, float *costs, hipStream_t stream) {
+    const int blocks = with_beta ? 2 * p.B : p.B;
+    if (tuning().dp_halo == 2) {  // 16-step prefetch blocks
+        if (p.min_s)
+            recursion_halo_kernel<16, NW, HL, true><<<blocks, 64 * NW, 0, stream>>>(p, with_beta, costs);
+        else
+            recursion_halo_kernel<16, NW, HL, false><<<blocks, 64 * NW, 0, stream>>>(p, with_beta, costs);
+        return;
+    }
+    if (p.min_s)
+        recursion_halo_kernel<8, NW, HL, true><<<blocks, 64 * NW, 0, stream>>>(p, with_beta, costs);
+    else
+        recursion_halo_kernel<8, NW, HL, false><<<blocks, 64 * NW, 0, stream>>>(p, with_beta, costs);
+}
+
 template <int K, int NW>
 static void launch_k(const DevProblem &p, int with_beta, float *costs, hipStream_t stream) {
     // D = rows of lp prefetched ahead (register ring), shallower where K cells per lane use the registers
@@ -213,6 +388,22 @@ static void launch_k(const DevProblem &p, int with_beta, float *costs, hipStream
 // LSE chain of K cells plus (NW > 1) one barrier, so small S runs on one wave with no barrier at all.
 hipError_t launch_dp(const DevProblem &p, int S_max, int with_beta, float *costs, hipStream_t stream) {
     const int W = S_max + 1;
+    if (tuning().dp_halo && W <= 64) {  // one wave, one cell per lane, no halo
+        launch_halo<1, 0>(p, with_beta, costs, stream);
+        return hipGetLastError();
+    }
+    if (tuning().dp_halo && W <= 8 * 56) {  // halo recursion: 56 own cells per wave
+        switch ((W + 55) / 56) {
+            case 2: launch_halo<2>(p, with_beta, costs, stream); break;
+            case 3: launch_halo<3>(p, with_beta, costs, stream); break;
+            case 4: launch_halo<4>(p, with_beta, costs, stream); break;
+            case 5: launch_halo<5>(p, with_beta, costs, stream); break;
+            case 6: launch_halo<6>(p, with_beta, costs, stream); break;
+            case 7: launch_halo<7>(p, with_beta, costs, stream); break;
+            default: launch_halo<8>(p, with_beta, costs, stream); break;
+        }
+        return hipGetLastError();
+    }
     if (W <= 64) launch_k<1, 1>(p, with_beta, costs, stream);
     else if (W <= 128) launch_k<1, 2>(p, with_beta, costs, stream);
     else if (W <= 256) launch_k<1, 4>(p, with_beta, costs, stream);

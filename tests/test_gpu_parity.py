@@ -276,6 +276,8 @@ def test_accuracy_against_reference_fp32_noise(op, dev):
     {"softmax_variant": 14, "softmax_grid_per_cu": 2, "nt_load": 0},
     {"softmax_variant": 15},
     {"col_scatter": 3},
+    {"dp_halo": 0},
+    {"dp_halo": 1},
     {"col_scatter": 0, "grad_variant": 6},
     {"col_scatter": 3, "grad_grid_per_cu": 0, "softmax_grid_per_cu": 4},
     {"grad_variant": 5},
@@ -285,7 +287,7 @@ def test_every_kernel_variant_matches_oracle(op, dev, knobs):
     """All launch variants selectable through mrnnt_tune compute the same result (alignment included)."""
     import _mrnnt_lib as L
     saved = {k: L.tune(k) for k in ("softmax_variant", "grad_variant", "softmax_grid_per_cu",
-                                    "grad_grid_per_cu", "nt_store", "nt_load", "col_scatter")}
+                                    "grad_grid_per_cu", "nt_store", "nt_load", "col_scatter", "dp_halo")}
     try:
         for k, v in knobs.items():
             assert L.tune(k, v) >= 0
@@ -296,14 +298,15 @@ def test_every_kernel_variant_matches_oracle(op, dev, knobs):
             cr, gr = O.oracle_rnnt(acts, labels, T, S)
             assert_costs(c, cr)
             assert_grads(g, gr)
-        acts, labels, T, S = random_problem(rng, 3, (20, 60), 10, 128)
-        al = np.zeros((3, int(T.max())), np.int32)
-        for b in range(3):
-            al[b, np.sort(rng.choice(T[b], S[b], replace=False))] = labels[b, : S[b]]
-        c, g = run_gpu(op, dev, acts, labels, T, S, alignment=al, k=2)
-        cr, gr = O.oracle_rnnt(acts, labels, T, S, alignment=al, max_shift=2)
-        assert_costs(c, cr)
-        assert_grads(g, gr)
+        for Tr, S_max, V, k in (((20, 60), 10, 128, 2), ((160, 220), 150, 32, 5)):  # 1 wave / halo recursion
+            acts, labels, T, S = random_problem(rng, 3, Tr, S_max, V, force={0: (Tr[1], S_max)})
+            al = np.zeros((3, int(T.max())), np.int32)
+            for b in range(3):
+                al[b, np.sort(rng.choice(T[b], S[b], replace=False))] = labels[b, : S[b]]
+            c, g = run_gpu(op, dev, acts, labels, T, S, alignment=al, k=k)
+            cr, gr = O.oracle_rnnt(acts, labels, T, S, alignment=al, max_shift=k)
+            assert_costs(c, cr)
+            assert_grads(g, gr)
     finally:
         for k, v in saved.items():
             L.tune(k, v)

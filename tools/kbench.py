@@ -52,7 +52,7 @@ def main():
 
     lib = L.load()
     DEFAULTS = {k: L.tune(k) for k in ("softmax_variant", "grad_variant", "softmax_grid_per_cu", "grad_grid_per_cu",
-                                       "nt_store", "nt_load", "occ_skip", "col_scatter")}
+                                       "nt_store", "nt_load", "occ_skip", "col_scatter", "dp_halo")}
     dev = torch.device("cuda:0")
     keep = []
     if args.fragment_gb > 0:
