@@ -76,6 +76,9 @@ def main():
                     help="element type of acts/grads (extension; the headline metric is f32, the reference's type)")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
                     help="launch knob for experiments (mrnnt_tune); the defaults are the tuned values")
+    ap.add_argument("--align-k", type=int, default=None,
+                    help="alignment-restricted loss (restrict_to_alignment, max_distance_from_alignment = K) on a "
+                         "synthetic alignment with the labels evenly spaced over the frames")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI, the real path) or gloo (rehearsal: several ranks may share one GPU)")
     args = ap.parse_args()
@@ -128,12 +131,17 @@ def main():
     labels = torch.from_numpy(rng.integers(1, V, (B, max(1, int(S.max())))).astype(np.int32)).to(dev)
     T_t = torch.from_numpy(T)
     S_t = torch.from_numpy(S)
+    align, n_window = None, None
+    if args.align_k is not None:
+        al_np, n_window = synthetic_alignment(labels.cpu().numpy(), T, S, args.align_k)
+        align = torch.from_numpy(al_np).to(dev)
+        workload += f", alignment-restricted (k={args.align_k}, labels evenly spaced)"
     acts.requires_grad_(True)
     torch.cuda.synchronize()
 
     def step():
         acts.grad = None
-        costs = op.monotonic_rnnt_loss(acts, labels, T_t, S_t, blank_label=0)
+        costs = op.monotonic_rnnt_loss(acts, labels, T_t, S_t, align, args.align_k or 0, blank_label=0)
         loss = costs.sum()
         loss.backward()
         if world > 1:
@@ -170,11 +178,12 @@ def main():
 
     # live rows: in-band rows whose gradient is not exactly zero in fp32 -- the only acts rows the gradient
     # kernel reads (occupancy skip); counted once after the timed region
-    live = live_rows(op, L, acts, labels, T_t, S_t, dev)
+    live = live_rows(op, L, acts, labels, T_t, S_t, dev, align, args.align_k or 0)
     grad_bytes = (live + rows) * V * elem  # algorithmic: read live acts rows once, write every grads row once
     formula_grad_bytes = (n_band + rows) * V * elem  # SURVEY.md §8d formula: every in-band row read
-    softmax_bytes = n_band * V * elem
-    step_bytes = (n_band + live + rows) * V * elem
+    n_read = n_band if n_window is None else n_window  # rows the log-softmax pass reads
+    softmax_bytes = n_read * V * elem
+    step_bytes = (n_read + live + rows) * V * elem
 
     def avg_ms(name):
         ms, n = prof[name]
@@ -221,6 +230,7 @@ def main():
             "data": "synthetic: counter-hash N(0,1)-like acts (seed 0), labels U[1,V-1] (seed 1+rank); inputs resident in HBM",
             "config": {"workload": workload, "utterances_per_gpu": B, "global_batch": total_utts,
                        "rows_per_gpu": rows, "inband_rows_per_gpu": n_band, "V": V,
+                       **({"window_rows_per_gpu": n_window} if n_window is not None else {}),
                        "parallelism": f"dp{world} (batch-sharded, one 4-byte "
                                       f"{'gloo (rehearsal)' if gloo else 'RCCL'} loss all-reduce)"},
             "achieved_hbm_gbps_step": round(step_bytes * total_utts / B * args.steps / elapsed / 1e9, 1),
@@ -275,9 +285,32 @@ def same_buffers_copy_gbps(lib, L, dev, src_t, dst_t, gib=8, reps=5):
     return round(2 * n / (ms * 1e-3) / 1e9, 1)
 
 
-def live_rows(op, L, acts, labels, T, S, dev):
+def synthetic_alignment(labels, T, S, k):
+    """[B, T_max] alignment with label i of utterance b at frame floor((i + 0.5) T_b / S_b) (blank = 0 elsewhere),
+    and the number of lattice rows the log-softmax pass reads under it (the alignment window of each column:
+    mrnnt_softmax.hip align_window, from the band of gpu_workspace_manager.h:191-219)."""
+    B = len(T)
+    al = np.zeros((B, int(T.max())), np.int32)
+    n_window = 0
+    for b in range(B):
+        Tb, Sb = int(T[b]), int(S[b])
+        fr = ((np.arange(Sb) + 0.5) * Tb / max(Sb, 1)).astype(np.int64)
+        al[b, fr] = labels[b, :Sb]
+        m = np.concatenate([[0], np.cumsum(al[b, :Tb] != 0)])
+        t = np.arange(Tb)
+        mn = m[np.clip(t + 1 - k, 0, Tb)]
+        mx = m[np.clip(t + 1 + k, 0, Tb)]
+        wlo = np.minimum(mn - 1, np.concatenate([[0], mn[:-1]]))
+        whi = np.maximum(mx, np.concatenate([[0], mx[:-1]]))
+        lo = np.maximum(np.maximum(0, t - (Tb - Sb)), wlo)
+        hi = np.minimum(np.minimum(t, Sb), whi)
+        n_window += int(np.maximum(hi - lo + 1, 0).sum())
+    return al, n_window
+
+
+def live_rows(op, L, acts, labels, T, S, dev, align=None, k=0):
     """In-band rows the gradient kernel reads on this workload (mrnnt_grad_live_rows after one forward)."""
-    prep = op._Prepared(acts.detach(), labels, T, S, None, 0, 0)
+    prep = op._Prepared(acts.detach(), labels, T, S, align, k, 0)
     _, ws = op._forward(prep, with_beta=True)
     cnt = torch.zeros(1, dtype=torch.int64, device=dev)
     L.check(L.load().mrnnt_grad_live_rows(ctypes.byref(prep.problem), ctypes.c_void_p(ws.data_ptr()),

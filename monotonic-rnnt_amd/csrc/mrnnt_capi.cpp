@@ -464,7 +464,8 @@ RNNTStatus mrnnt_joint_forward(const mrnnt_joint_problem *jp, void *ws, size_t w
                         reinterpret_cast<int *>(w + jl.off_ls), reinterpret_cast<unsigned long long *>(w + jl.off_total),
                         stream);
     if (e != hipSuccess) return fail_hip(e, "row list kernels");
-    const JointArgs j = joint_args(jp, jl, ws, jl.n_inband);
+    JointArgs j = joint_args(jp, jl, ws, jl.n_inband);
+    if (pl.align) j.n_dev = reinterpret_cast<const unsigned long long *>(w + jl.off_total);  // alignment windows
     e = timed(K_JOINT_FWD, stream, [&] { return launch_joint_forward(d, j, stream); });
     if (e != hipSuccess) return fail_hip(e, "joint log-softmax kernel");
     e = timed(K_DP, stream, [&] { return launch_dp(d, pl.S_max, with_beta ? 1 : 0, costs_dev, stream); });

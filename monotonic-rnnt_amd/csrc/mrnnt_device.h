@@ -103,6 +103,32 @@ __device__ __forceinline__ int64_t acts_col_base(const DevProblem &p, int b, int
     return p.pad_S1 ? ((int64_t)b * p.pad_T + t) * p.pad_S1 : rowc;
 }
 
+// Alignment-restricted calls (restrict_to_alignment, gpu_workspace_manager.h:191-219): only the rows the recursion
+// can use inside the alignment band need the log-softmax. alpha(t, s), s in [min_s(t), max_s(t)], reads rows s and
+// s-1 of column t; beta(t, s), s in [min_s(t-1), max_s(t-1)] (t > 0; beta(0, .) only s = 0), reads row s; every
+// other cell is -inf, so the other rows' lp only meet -inf and no gradient row outside the window is live. The
+// row reads of the pass drop from the whole band to a few rows per column.
+__device__ __forceinline__ void align_window(const DevProblem &p, int64_t c, int t, int &lo, int &hi) {
+    if (!p.min_s) return;
+    int wlo = p.min_s[c] - 1, whi = p.max_s[c];
+    if (t > 0) {
+        wlo = min(wlo, p.min_s[c - 1]);
+        whi = max(whi, p.max_s[c - 1]);
+    } else {
+        wlo = min(wlo, 0);
+        whi = max(whi, 0);
+    }
+    lo = max(lo, wlo);
+    hi = min(hi, whi);
+}
+
+__device__ __forceinline__ void write_row(const DevProblem &p, int64_t row, float m, float sum, float zb, float ze) {
+    const double den = -(double)m - log((double)sum);
+    p.den[row] = (float)den;
+    p.lpb[row] = (double)zb + den;
+    p.lpe[row] = (double)ze + den;
+}
+
 // ---- element-type traits of the acts / grads I/O (math is fp32 in registers) ----------------------
 
 struct IoF32 {

@@ -53,7 +53,8 @@ struct JointArgs {
     int H;
     const int *lcol;             // row list: lattice column and label position of entry i
     const int *ls;
-    int64_t n;                   // entries in the list
+    int64_t n;                   // entries in the list (an upper bound when n_dev is set)
+    const unsigned long long *n_dev;  // entries in the list, on the device (alignment windows), or nullptr
     // backward outputs, one row per list entry
     unsigned short *G;           // [n, V] bf16 dL/dz
     unsigned short *Hact;        // [n, H] bf16 tanh(enc + pred)

@@ -69,8 +69,8 @@ __global__ __launch_bounds__(256) void row_list_kernel(DevProblem p, int mode, i
     const int T = p.T[b], S = p.S[b], W = S + 1;
     const int t = (int)(col - p.col_off[b]);
     const int64_t rowc = p.row_off[b] + (int64_t)t * W;
-    const int lo = max(0, t - (T - S));
-    const int hi = min(t, S);
+    int lo = max(0, t - (T - S)), hi = min(t, S);
+    if (mode == 0) align_window(p, col, t, lo, hi);  // alignment-restricted: only the rows the recursion uses
     const double ll = mode ? p.ll[b] : 0.0;
     int64_t base = WRITE ? cnt[col] : 0;
     int n = 0;
@@ -141,9 +141,13 @@ struct RowPos {
     int64_t row;  // packed lattice row
 };
 
+__device__ __forceinline__ int64_t list_len(const JointArgs &j) {
+    return j.n_dev ? (int64_t)*j.n_dev : j.n;
+}
+
 __device__ __forceinline__ RowPos row_pos(const DevProblem &p, const JointArgs &j, int64_t i) {
     RowPos q{false, 0, 0, 0, 1, 0, -1, 0};
-    if (i >= j.n) return q;
+    if (i >= list_len(j)) return q;
     const int col = j.lcol[i];
     q.s = j.ls[i];
     q.b = p.col_b[col];
@@ -336,6 +340,7 @@ template <int KS, int NB, int NW>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2))) void joint_fwd_kernel(DevProblem p,
                                                                                              JointArgs j) {
     extern __shared__ __attribute__((aligned(16))) unsigned short wsh[];
+    if ((int64_t)blockIdx.x * (32 * NW) >= list_len(j)) return;  // whole workgroup past a shorter list
     const int lane = threadIdx.x & 63, half = lane >> 5;
     const int64_t i = (int64_t)blockIdx.x * (32 * NW) + (threadIdx.x >> 6) * 32 + (lane & 31);
     const RowPos q = row_pos(p, j, i);

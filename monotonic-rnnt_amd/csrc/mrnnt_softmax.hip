@@ -14,19 +14,15 @@
 
 namespace mrnnt {
 
+// rows of the column that are not reduced: finite lp (the recursion reads them, masked) and den (the gradient's
+// per-row coefficient of such a row meets alpha or beta = -inf and comes out exactly 0)
 __device__ __forceinline__ void zero_fill_outside_band(const DevProblem &p, int64_t rowc, int S, int lo, int hi) {
     for (int s = threadIdx.x; s <= S; s += blockDim.x)
         if (s < lo || s > hi) {
             p.lpb[rowc + s] = 0.0;
             p.lpe[rowc + s] = 0.0;
+            p.den[rowc + s] = 0.0f;
         }
-}
-
-__device__ __forceinline__ void write_row(const DevProblem &p, int64_t row, float m, float sum, float zb, float ze) {
-    const double den = -(double)m - log((double)sum);
-    p.den[row] = (float)den;
-    p.lpb[row] = (double)zb + den;
-    p.lpe[row] = (double)ze + den;
 }
 
 // Vector path: V % E == 0, 16-byte aligned rows. U = vector loads per lane per chunk (a chunk covers
@@ -50,8 +46,8 @@ __global__ __launch_bounds__(256) void softmax_kernel(DevProblem p) {
         const int t = (int)(c - p.col_off[b]);
         const int64_t rowc = p.row_off[b] + (int64_t)t * (S + 1);
         const int64_t arow = acts_col_base(p, b, t, rowc);
-        const int lo = max(0, t - (T - S));
-        const int hi = min(t, S);
+        int lo = max(0, t - (T - S)), hi = min(t, S);
+        align_window(p, c, t, lo, hi);
         const int *__restrict__ lab_b = p.labels + (int64_t)b * p.label_stride;
         zero_fill_outside_band(p, rowc, S, lo, hi);
 
@@ -154,8 +150,8 @@ __global__ __launch_bounds__(256) void softmax_lean_kernel(DevProblem p) {
         const int t = (int)(c - p.col_off[b]);
         const int64_t rowc = p.row_off[b] + (int64_t)t * (S + 1);
         const int64_t arow = acts_col_base(p, b, t, rowc);
-        const int lo = max(0, t - (T - S));
-        const int hi = min(t, S);
+        int lo = max(0, t - (T - S)), hi = min(t, S);
+        align_window(p, c, t, lo, hi);
         const int *__restrict__ lab_b = p.labels + (int64_t)b * p.label_stride;
         zero_fill_outside_band(p, rowc, S, lo, hi);
 
@@ -263,8 +259,8 @@ __global__ __launch_bounds__(256) void softmax_scalar_kernel(DevProblem p) {
         const int t = (int)(c - p.col_off[b]);
         const int64_t rowc = p.row_off[b] + (int64_t)t * (S + 1);
         const int64_t arow = acts_col_base(p, b, t, rowc);
-        const int lo = max(0, t - (T - S));
-        const int hi = min(t, S);
+        int lo = max(0, t - (T - S)), hi = min(t, S);
+        align_window(p, c, t, lo, hi);
         const int *__restrict__ lab_b = p.labels + (int64_t)b * p.label_stride;
         zero_fill_outside_band(p, rowc, S, lo, hi);
         for (int s = lo + wave; s <= hi; s += 4) {

@@ -1,0 +1,9 @@
+# alignment windows in the fused joint forward: joint tests, joint bench with and without alignment restriction
+set -o pipefail
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/s3z; mkdir -p $O; cd $R
+timeout -k 10 600 python -u -m pytest tests/test_gpu_joint.py tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 && \
+timeout -k 10 600 python tools/joint_bench.py --align-k 2 > $O/jb_k2.json 2> $O/jb_k2.err && \
+timeout -k 10 600 python tools/joint_bench.py > $O/jb.json 2> $O/jb.err
+echo rc=$?
+tail -n 2 $O/pytest.log
+cat $O/jb_k2.json $O/jb.json

@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-unfused", action="store_true")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE")
+    ap.add_argument("--align-k", type=int, default=None,
+                    help="alignment-restricted loss (max_distance_from_alignment = K) on bench.py's synthetic alignment")
     a = ap.parse_args()
     import _mrnnt_lib as L
     import monotonic_rnnt_joint as J
@@ -54,11 +56,17 @@ def main():
     Tl = torch.full((B,), T, dtype=torch.int32)
     Sl = torch.full((B,), S, dtype=torch.int32)
     n_band = B * ((S + 1) * (T - S + 1) - 1)
+    al, k = None, 0
+    if a.align_k is not None:
+        sys.path.insert(0, ROOT)
+        from bench import synthetic_alignment
+        al_np, n_band = synthetic_alignment(labels.cpu().numpy(), Tl.numpy(), Sl.numpy(), a.align_k)
+        al, k = torch.from_numpy(al_np).to(dev), a.align_k  # n_band: the rows the forward computes
 
     def fused():
         for x in (enc, pred, W, bias):
             x.grad = None
-        c = J.monotonic_rnnt_joint_loss(enc, pred, W, bias, labels, Tl, Sl)
+        c = J.monotonic_rnnt_joint_loss(enc, pred, W, bias, labels, Tl, Sl, alignment=al, max_distance_from_alignment=k)
         c.sum().backward()
         return c
 
@@ -67,7 +75,7 @@ def main():
             x.grad = None
         h = torch.tanh(enc[:, :, None, :] + pred[:, None, :, :])
         z = torch.nn.functional.linear(h, W, bias.to(torch.bfloat16))  # [B, T, S+1, V] bf16
-        c = op.monotonic_rnnt_loss(z, labels, Tl, Sl)
+        c = op.monotonic_rnnt_loss(z, labels, Tl, Sl, al, k)
         c.sum().backward()
         return c
 
@@ -87,11 +95,12 @@ def main():
             L.profile_enable(False)
         return dt, c.detach(), pr
 
-    out = {"config": {"B": B, "T": T, "S": S, "V": V, "H": H, "dtype": "bf16 operands, fp32 accumulate"},
+    out = {"config": {"B": B, "T": T, "S": S, "V": V, "H": H, "dtype": "bf16 operands, fp32 accumulate",
+                      "align_k": a.align_k},
            "tune": a.tune or None}
     dt, c_f, pr = timeit(fused, prof=True)
     # live rows of the backward pass (the gradient kernel's row count)
-    prep = J._JointPrepared(enc.detach(), pred.detach(), W.detach(), bias.detach(), labels, Tl, Sl, 0)
+    prep = J._JointPrepared(enc.detach(), pred.detach(), W.detach(), bias.detach(), labels, Tl, Sl, 0, al, k)
     _, ws = prep.forward(with_beta=True)
     G, _ = prep.backward_rows(ws, None)
     n_live = G.shape[0]
@@ -101,7 +110,7 @@ def main():
     f_bwd = 2.0 * n_live * V * H
     out["fused"] = {
         "ms_per_step": round(dt * 1e3, 3), "utt_per_s": round(B / dt, 1),
-        "inband_rows": n_band, "live_rows": n_live, "live_frac": round(n_live / n_band, 4),
+        "forward_rows": n_band, "live_rows": n_live, "live_frac": round(n_live / n_band, 4),
         "kernels_ms": {"joint_fwd": round(ms("joint_fwd"), 3), "alpha_beta": round(ms("alpha_beta"), 3),
                        "joint_bwd": round(ms("joint_bwd"), 3), "joint_reduce": round(ms("joint_reduce"), 3)},
         "joint_fwd_tflops": round(f_fwd / (ms("joint_fwd") * 1e-3) / 1e12, 1),
