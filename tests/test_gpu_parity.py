@@ -470,6 +470,42 @@ def test_occupancy_skip_is_bit_identical(op, dev, grad_variant):
         L.tune("grad_variant", saved_var)
 
 
+@pytest.mark.parametrize("grad_variant", [0, 5])
+def test_alignment_window_with_and_without_occupancy_skip(op, dev, grad_variant):
+    """Alignment-restricted calls reduce only the rows of each column's alignment window; rows outside it get
+    zero lp/den. With the occupancy skip off the gradient kernel reads those rows too: the result must still be
+    bit-identical to the skip-on run (every such row meets alpha or beta = -inf) and match the oracle."""
+    import _mrnnt_lib as L
+    rng = np.random.default_rng(707)
+    T = np.array([300, 220, 90], np.int32)
+    S = np.array([110, 60, 30], np.int32)
+    V = 48
+    rows = int(np.sum(T * (S + 1)))
+    acts = rng.standard_normal((rows, V)).astype(np.float32)
+    labels = rng.integers(1, V, (3, int(S.max()))).astype(np.int32)
+    al = np.zeros((3, int(T.max())), np.int32)
+    for b in range(3):
+        al[b, np.sort(rng.choice(T[b], S[b], replace=False))] = labels[b, : S[b]]
+    scale = np.array([1.0, -2.0, 0.5], np.float32)
+    k = 3
+    saved_skip, saved_var = L.tune("occ_skip"), L.tune("grad_variant")
+    try:
+        L.tune("grad_variant", grad_variant)
+        out = {}
+        for skip in (0, 1):
+            L.tune("occ_skip", skip)
+            out[skip] = run_gpu(op, dev, acts, labels, T, S, alignment=al, k=k, scale=scale)
+        assert np.array_equal(out[0][0], out[1][0])
+        assert np.array_equal(out[0][1].view(np.uint32), out[1][1].view(np.uint32))
+        cr, gr = O.oracle_rnnt(acts, labels, T, S, alignment=al, max_shift=k, num_threads=4)
+        gr = gr * np.repeat(scale.astype(np.float64), T * (S + 1))[:, None]
+        assert_costs(out[1][0], cr)
+        assert_grads(out[1][1], gr)
+    finally:
+        L.tune("occ_skip", saved_skip)
+        L.tune("grad_variant", saved_var)
+
+
 @pytest.mark.parametrize("B,T,S,V", [(1, 150, 20, 50), (1, 150, 20, 5000), (16, 150, 20, 50), (16, 150, 20, 5000),
                                      (2, 391, 300, 79)])
 def test_reference_size_cases_vs_oracle(op, dev, B, T, S, V):
