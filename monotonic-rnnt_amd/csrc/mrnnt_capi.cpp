@@ -580,6 +580,7 @@ int mrnnt_tune(const char *key, int value) {
     else if (!std::strcmp(key, "grad_variant")) slot = &t.grad_variant;
     else if (!std::strcmp(key, "col_scatter")) slot = &t.col_scatter;
     else if (!std::strcmp(key, "dp_halo")) slot = &t.dp_halo;
+    else if (!std::strcmp(key, "joint_reduce_sparse")) slot = &t.joint_reduce_sparse;
     else if (!std::strcmp(key, "softmax_grid_per_cu")) slot = &t.softmax_grid_per_cu;
     else if (!std::strcmp(key, "grad_grid_per_cu")) slot = &t.grad_grid_per_cu;
     else if (!std::strcmp(key, "grid_per_cu")) {  // both streaming kernels

@@ -85,6 +85,8 @@ struct Tuning {
     int nt_load = 1;              // nontemporal loads of acts (both streaming kernels)
     int occ_skip = 1;             // gradient: no acts read for rows with log-occupancy < kDeadLogOcc
     int joint_nbuf = 2;           // fused joint kernels: LDS buffers for the weight chunks (2 or 3)
+    int joint_reduce_sparse = 0;  // joint d_enc/d_pred reduce: 0 row-parallel kernel below 4 live rows per column,
+                                  // 1 always frame by frame, 2 always row-parallel
     int dp_halo = 2;              // alpha/beta: halo recursion (one barrier per 8 steps, 8 / 16-step prefetch
                                   // blocks: 1 / 2) for S+1 <= 448; 0: one barrier per step
     int col_scatter = 2;          // visit columns in a scattered order (DevProblem::col_mul): bit 0 log-softmax,

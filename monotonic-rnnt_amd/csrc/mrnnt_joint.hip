@@ -501,10 +501,29 @@ __global__ __launch_bounds__(256) void joint_reduce_kernel(DevProblem p, JointAr
     const int hl = (tid % TPR) * 4, rsub = tid / TPR;
     float *acc = lds;
     float *red = lds + (S + 1) * HS;
-    for (int i = tid; i < (S + 1) * HS; i += 256) acc[i] = 0.0f;
-    __syncthreads();
     const int64_t tslots = j.enc_sb / H, sslots = j.pred_sb / H;
     const int t1 = min(t0 + kReduceTT, T);
+    // label positions this block of frames touches: rows of a column are listed by ascending s, so the first and
+    // last row of each column bound them (a few labels under an alignment restriction, the band otherwise); only
+    // that slice of the d_pred accumulator is cleared and flushed
+    __shared__ int srange[2];
+    if (tid == 0) {
+        srange[0] = S + 1;
+        srange[1] = -1;
+    }
+    __syncthreads();
+    if (tid < t1 - t0) {
+        const int64_t col = p.col_off[b] + t0 + tid;
+        const int64_t r0 = off[col], r1 = off[col + 1];
+        if (r1 > r0) {
+            atomicMin(&srange[0], j.ls[r0]);
+            atomicMax(&srange[1], j.ls[r1 - 1]);
+        }
+    }
+    __syncthreads();
+    const int s_lo = srange[0], s_hi = srange[1];
+    for (int i = s_lo * HS + tid; i < (s_hi + 1) * HS; i += 256) acc[i] = 0.0f;
+    __syncthreads();
     for (int t = t0; t < t1; ++t) {
         const int64_t col = p.col_off[b] + t;
         const int64_t r0 = off[col], r1 = off[col + 1];
@@ -540,8 +559,76 @@ __global__ __launch_bounds__(256) void joint_reduce_kernel(DevProblem p, JointAr
         }
         __syncthreads();
     }
-    for (int i = tid; i < (S + 1) * HS; i += 256) {
+    for (int i = s_lo * HS + tid; i < (s_hi + 1) * HS; i += 256) {
         const float v = acc[i];
+        if (v != 0.0f) atomicAdd(&d_pred[((int64_t)b * sslots + i / HS) * H + h0 + i % HS], v);
+    }
+}
+
+// Sparse variant (few live rows per frame, e.g. alignment-restricted training): the rows of a block of frames are
+// processed all at once (TPR threads per row) instead of frame by frame, so a workgroup does not wait one
+// dependent load chain per frame; d_enc and d_pred partials meet in LDS through ds_add_f32.
+template <int HS>
+__global__ __launch_bounds__(256) void joint_reduce_sparse_kernel(DevProblem p, JointArgs j,
+                                                                  const int64_t *__restrict__ off,
+                                                                  const unsigned short *__restrict__ dH,
+                                                                  float *__restrict__ d_enc, float *__restrict__ d_pred,
+                                                                  int ntb) {
+    constexpr int TPR = HS / 4;
+    constexpr int RP = 256 / TPR;
+    extern __shared__ float lds[];  // acc_pred[(S_b+1) * HS] then acc_enc[kReduceTT * HS]
+    const int H = j.H;
+    const int nh = H / HS;
+    const int bx = blockIdx.x / nh;
+    const int h0 = (blockIdx.x % nh) * HS;
+    const int b = bx / ntb;
+    const int t0 = (bx % ntb) * kReduceTT;
+    const int T = p.T[b], S = p.S[b];
+    if (t0 >= T) return;
+    const int tid = threadIdx.x;
+    const int hl = (tid % TPR) * 4, rsub = tid / TPR;
+    const int t1 = min(t0 + kReduceTT, T);
+    float *accp = lds;
+    float *acce = lds + (S + 1) * HS;
+    const int64_t c0 = p.col_off[b];
+    const int64_t rb = off[c0 + t0], re = off[c0 + t1];
+    // the label range the rows touch: only that slice of the d_pred accumulator is cleared and flushed
+    __shared__ int srange[2];
+    if (tid == 0) {
+        srange[0] = S + 1;
+        srange[1] = -1;
+    }
+    for (int i = tid; i < kReduceTT * HS; i += 256) acce[i] = 0.0f;
+    __syncthreads();
+    for (int64_t r = rb + tid; r < re; r += 256) {
+        const int s = j.ls[r];
+        atomicMin(&srange[0], s);
+        atomicMax(&srange[1], s);
+    }
+    __syncthreads();
+    const int s_lo = srange[0], s_hi = srange[1];
+    for (int i = s_lo * HS + tid; i < (s_hi + 1) * HS; i += 256) accp[i] = 0.0f;
+    __syncthreads();
+    for (int64_t r = rb + rsub; r < re; r += RP) {
+        const int s = j.ls[r];
+        const int tt = (int)(j.lcol[r] - c0 - t0);
+        const uint2 dv = *reinterpret_cast<const uint2 *>(dH + r * H + h0 + hl);
+        const uint2 hv = *reinterpret_cast<const uint2 *>(j.Hact + r * H + h0 + hl);
+        const float h_0 = bf16_lo(hv.x), h_1 = bf16_hi(hv.x), h_2 = bf16_lo(hv.y), h_3 = bf16_hi(hv.y);
+        const float v[4] = {bf16_lo(dv.x) * (1.0f - h_0 * h_0), bf16_hi(dv.x) * (1.0f - h_1 * h_1),
+                            bf16_lo(dv.y) * (1.0f - h_2 * h_2), bf16_hi(dv.y) * (1.0f - h_3 * h_3)};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            atomicAdd(&acce[tt * HS + hl + q], v[q]);
+            atomicAdd(&accp[s * HS + hl + q], v[q]);
+        }
+    }
+    __syncthreads();
+    const int64_t tslots = j.enc_sb / H, sslots = j.pred_sb / H;
+    for (int i = tid; i < (t1 - t0) * HS; i += 256)  // rows (b, t < T_b) of d_enc are overwritten (ABI)
+        d_enc[((int64_t)b * tslots + t0 + i / HS) * H + h0 + i % HS] = acce[i];
+    for (int i = s_lo * HS + tid; i < (s_hi + 1) * HS; i += 256) {
+        const float v = accp[i];
         if (v != 0.0f) atomicAdd(&d_pred[((int64_t)b * sslots + i / HS) * H + h0 + i % HS], v);
     }
 }
@@ -550,8 +637,17 @@ hipError_t launch_joint_reduce(const DevProblem &p, const JointArgs &j, const in
                                const unsigned short *dH, float *d_enc, float *d_pred, hipStream_t stream) {
     const int ntb = (T_max + kReduceTT - 1) / kReduceTT;
     const int W = S_max + 1;
+    // fewer than 4 live rows per lattice column on average: the row-parallel sparse kernel
+    const int mode = tuning().joint_reduce_sparse;
+    const bool sparse = mode == 0 ? j.n < 4 * p.num_cols : mode == 2;
     auto go = [&](auto hs_tag) {
         constexpr int HS = decltype(hs_tag)::value;
+        if (sparse) {
+            const size_t lds = sizeof(float) * ((size_t)W * HS + (size_t)kReduceTT * HS);
+            joint_reduce_sparse_kernel<HS><<<p.B * ntb * (j.H / HS), 256, lds, stream>>>(p, j, off, dH, d_enc,
+                                                                                          d_pred, ntb);
+            return;
+        }
         const size_t lds = sizeof(float) * ((size_t)W * HS + 256 / (HS / 4) * HS);
         joint_reduce_kernel<HS><<<p.B * ntb * (j.H / HS), 256, lds, stream>>>(p, j, off, dH, d_enc, d_pred, ntb);
     };
