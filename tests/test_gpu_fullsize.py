@@ -154,3 +154,47 @@ def test_config_c5_large_vocab():
     cr, gr = O.oracle_rnnt(host, labels, T, S, precision="f64", num_threads=2)
     assert np.max(np.abs(c - cr) / np.abs(cr)) <= 1e-4
     assert np.abs(g.cpu().numpy() - gr).max() <= 1e-4
+
+
+def test_headline_alignment_restricted(headline):
+    """The headline shape alignment-restricted (labels evenly spaced over the frames, k = 2): the log-softmax pass
+    then reduces only each column's alignment window. Costs finite and >= the unrestricted costs (a subset of the
+    paths), every row outside the window exactly zero, row sums zero, and utterance 0 against the oracle."""
+    import monotonic_rnnt_op as op
+    dev = headline["acts"].device
+    labels = headline["labels"]
+    k = 2
+    al = np.zeros((B, T), np.int32)
+    frames = ((np.arange(S) + 0.5) * T / S).astype(np.int64)
+    al[:, frames] = labels[:, :S]
+    acts = headline["acts"]
+    acts.grad = None  # the fixture's gradient stays in headline["grads"]; do not accumulate into it
+    acts.requires_grad_(True)
+    costs = op.monotonic_rnnt_loss(acts, torch.from_numpy(labels).to(dev), torch.full((B,), T, dtype=torch.int32),
+                                   torch.full((B,), S, dtype=torch.int32), torch.from_numpy(al).to(dev), k, 0)
+    costs.sum().backward()
+    torch.cuda.synchronize()
+    g = acts.grad
+    acts.requires_grad_(False)
+    acts.grad = None
+    c = costs.detach().cpu().numpy().astype(np.float64)
+    assert np.all(np.isfinite(c)) and np.all(c >= headline["costs"] * (1 - 1e-6))
+    assert g.sum(dim=1, dtype=torch.float64).abs().max().item() < 1e-4
+    # rows outside the window [min(min_s(t) - 1, min_s(t-1)), max(max_s(t), max_s(t-1))] are exactly zero
+    m = np.concatenate([[0], np.cumsum(al[0] != 0)])
+    t = np.arange(T)
+    mn, mx = m[np.clip(t + 1 - k, 0, T)], m[np.clip(t + 1 + k, 0, T)]
+    wlo = np.minimum(mn - 1, np.concatenate([[0], mn[:-1]]))
+    whi = np.maximum(mx, np.concatenate([[0], mx[:-1]]))
+    s = np.arange(S + 1)
+    outside = (s[None, :] < wlo[:, None]) | (s[None, :] > whi[:, None])
+    rowmax = g.abs().amax(dim=1).view(B, T * (S + 1))  # per-row max |grad| ([N] floats, not a copy of g)
+    assert rowmax[:, torch.from_numpy(outside.reshape(-1)).to(dev)].max().item() == 0.0
+    rows_per = headline["rows_per"]
+    host_acts = O.synth_acts(0, rows_per * V, seed=0).reshape(rows_per, V)
+    cr, gr = O.oracle_rnnt(host_acts, labels[:1], [T], [S], alignment=al[:1], max_shift=k, precision="f64",
+                           num_threads=1)
+    assert abs(c[0] - cr[0]) <= 1e-4 * abs(cr[0])
+    assert np.abs(g[:rows_per].cpu().numpy() - gr).max() <= 1e-4
+    del g
+    torch.cuda.empty_cache()
