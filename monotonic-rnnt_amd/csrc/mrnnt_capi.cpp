@@ -248,7 +248,7 @@ RNNTStatus mrnnt_forward(const mrnnt_problem *p, void *ws, size_t ws_bytes, floa
     e = timed(K_SETUP, stream, [&] {
         return launch_setup(p->T_dev, p->S_dev, pl.B, reinterpret_cast<int64_t *>(w + pl.off_row),
                             reinterpret_cast<int64_t *>(w + pl.off_col),
-                            reinterpret_cast<int *>(w + pl.off_colb), stream);
+                            reinterpret_cast<int *>(w + pl.off_colb), d.lpb, d.lpe, pl.N, stream);
     });
     if (e != hipSuccess) return fail_hip(e, "setup kernel");
     if (pl.align) {
@@ -446,7 +446,7 @@ RNNTStatus mrnnt_joint_forward(const mrnnt_joint_problem *jp, void *ws, size_t w
     hipError_t e = timed(K_SETUP, stream, [&] {
         return launch_setup(jp->T_dev, jp->S_dev, pl.B, reinterpret_cast<int64_t *>(w + pl.off_row),
                             reinterpret_cast<int64_t *>(w + pl.off_col),
-                            reinterpret_cast<int *>(w + pl.off_colb), stream);
+                            reinterpret_cast<int *>(w + pl.off_colb), nullptr, nullptr, 0, stream);
     });
     if (e != hipSuccess) return fail_hip(e, "setup kernel");
     if (pl.align) {

@@ -98,8 +98,9 @@ Tuning &tuning();
 enum KernelId { K_BAND = 0, K_SOFTMAX = 1, K_DP = 2, K_GRAD = 3, K_SETUP = 4, K_JOINT_FWD = 5, K_JOINT_BWD = 6,
                 K_JOINT_RED = 7, K_COUNT = 8 };
 
+// lpb / lpe (may be null): zero their 64 pad entries either side of [0, n)
 hipError_t launch_setup(const int *T, const int *S, int B, int64_t *row_off, int64_t *col_off, int *col_b,
-                        hipStream_t stream);
+                        double *lpb, double *lpe, int64_t n, hipStream_t stream);
 hipError_t launch_align(const DevProblem &p, const int *alignment, int64_t align_stride, int align_blank,
                         int max_shift, int *mtmp, int *min_s, int *max_s, hipStream_t stream);
 hipError_t launch_softmax(const DevProblem &p, int elem, int grid, hipStream_t stream);

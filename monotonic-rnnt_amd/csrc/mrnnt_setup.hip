@@ -11,13 +11,23 @@ Tuning &tuning() {
 
 // row_off[b] = sum_{b'<b} T_b'(S_b'+1), col_off[b] = sum_{b'<b} T_b' -- one wave, any B (reference
 // gpu_workspace_manager.h:256-329 computes these on the host and copies them with blocking memcpys).
+// It also zeroes the 64 lp entries either side of the lp arrays: the recursion's in-band cell s = 0 of
+// utterance 0 adds lpe[-1] to its -inf predecessor, and a NaN / +inf left in the (reused) workspace there
+// would turn alpha(0, 0) into NaN (then -inf through fmax in the next LSE: an infinite cost).
 __global__ __launch_bounds__(64) void setup_kernel(const int *__restrict__ T, const int *__restrict__ S, int B,
-                                                   int64_t *__restrict__ row_off, int64_t *__restrict__ col_off) {
+                                                   int64_t *__restrict__ row_off, int64_t *__restrict__ col_off,
+                                                   double *__restrict__ lpb, double *__restrict__ lpe, int64_t n) {
     const int lane = threadIdx.x;
     int64_t carry_r = 0, carry_c = 0;
     if (lane == 0) {
         row_off[0] = 0;
         col_off[0] = 0;
+    }
+    if (lpb) {
+        lpb[lane - 64] = 0.0;
+        lpe[lane - 64] = 0.0;
+        lpb[n + lane] = 0.0;
+        lpe[n + lane] = 0.0;
     }
     for (int base = 0; base < B; base += 64) {
         const int b = base + lane;
@@ -117,8 +127,8 @@ __global__ __launch_bounds__(256) void col_map_kernel(const int *__restrict__ T,
 }
 
 hipError_t launch_setup(const int *T, const int *S, int B, int64_t *row_off, int64_t *col_off, int *col_b,
-                        hipStream_t stream) {
-    setup_kernel<<<1, 64, 0, stream>>>(T, S, B, row_off, col_off);
+                        double *lpb, double *lpe, int64_t n, hipStream_t stream) {
+    setup_kernel<<<1, 64, 0, stream>>>(T, S, B, row_off, col_off, lpb, lpe, n);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     col_map_kernel<<<B, 256, 0, stream>>>(T, col_off, col_b);

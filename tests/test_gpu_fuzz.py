@@ -1,0 +1,113 @@
+"""Seeded random sweep of the HIP path against the oracle (cpu_rnnt.h<double> restatement), across the shapes the
+kernel variants switch on: V (vector width, chunking, FULL / ragged rows, V < 4, odd V), S+1 (single-wave /
+halo / per-step-barrier recursion, gradient segments of 256 rows), blank anywhere in [0, V), labels that may equal
+the blank, alignment restriction with random k, per-utterance gradient scales (negative and zero included),
+packed and padded layouts, f32 / bf16 / f16 acts. Tolerances as tests/test_gpu_parity.py (reduced precision:
+the grads tolerance adds one rounding of the acts type).
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+N_CASES = 160
+
+
+@pytest.fixture(scope="module")
+def op():
+    import monotonic_rnnt_op
+    return monotonic_rnnt_op
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    return torch.device("cuda:0")
+
+
+def make_case(seed):
+    rng = np.random.default_rng(1000 + seed)
+    V = int(rng.choice([2, 3, 5, 16, 31, 64, 100, 255, 256, 257, 1000, 1024, 1030, 2048]))
+    B = int(rng.integers(1, 5))
+    # label lengths across the recursion's shapes: <= 63, halo (64 .. 447), per-step barrier (>= 448)
+    s_cap = int(rng.choice([8, 60, 130, 250, 460]))
+    if V >= 1000:
+        s_cap = min(s_cap, 130)  # keep the oracle's work small
+    T = rng.integers(1, s_cap + 40, B).astype(np.int32)
+    S = np.array([rng.integers(0, min(int(t), s_cap) + 1) for t in T], np.int32)
+    blank = int(rng.integers(0, V))
+    L = max(1, int(S.max()))
+    labels = rng.integers(0, V, (B, L)).astype(np.int32)
+    if rng.random() < 0.7:  # mostly labels != blank, as in training data
+        labels[labels == blank] = (blank + 1) % V if V > 1 else blank
+    rows = int(np.sum(T.astype(np.int64) * (S + 1)))
+    acts = (rng.standard_normal((rows, V)) * rng.choice([0.5, 1.0, 3.0])).astype(np.float32)
+    scale = rng.choice([1.0, -0.5, 0.0, 2.0, 0.25], B).astype(np.float32)
+    align, k = None, 0
+    if rng.random() < 0.3:
+        k = int(rng.integers(0, 6))
+        align = np.full((B, int(T.max())), blank, np.int32)
+        for b in range(B):
+            fr = np.sort(rng.choice(int(T[b]), int(S[b]), replace=False))
+            align[b, fr] = labels[b, : S[b]]
+            # the alignment's labels are parsed by != blank: keep them distinct from the blank
+            align[b, fr[align[b, fr] == blank]] = (blank + 1) % V
+    dtype = rng.choice(["f32"] * 6 + ["bf16", "f16"])
+    padded = bool(rng.random() < 0.25)
+    return dict(V=V, T=T, S=S, blank=blank, labels=labels, acts=acts, scale=scale, align=align, k=k,
+                dtype=str(dtype), padded=padded)
+
+
+def pad(acts, T, S, pad_T, pad_S1):
+    B, V = len(T), acts.shape[1]
+    out = np.full((B, pad_T, pad_S1, V), np.nan, np.float32)
+    r = 0
+    for b in range(B):
+        n = int(T[b]) * (int(S[b]) + 1)
+        out[b, : T[b], : S[b] + 1] = acts[r: r + n].reshape(T[b], S[b] + 1, V)
+        r += n
+    return out
+
+
+def unpad(x, T, S):
+    return np.concatenate([x[b, : T[b], : S[b] + 1].reshape(-1, x.shape[-1]) for b in range(len(T))])
+
+
+@pytest.mark.parametrize("seed", range(N_CASES))
+def test_random_case_vs_oracle(op, dev, seed):
+    c = make_case(seed)
+    T, S, V = c["T"], c["S"], c["V"]
+    tdt = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}[c["dtype"]]
+    a = torch.from_numpy(c["acts"]).to(tdt)
+    host = a.float().numpy()  # the exact values the kernels read
+    if c["padded"]:
+        a = torch.from_numpy(pad(host, T, S, int(T.max()) + 2, int(S.max()) + 3)).to(tdt)
+    a = a.to(dev).requires_grad_(True)
+    lab = torch.from_numpy(c["labels"]).to(dev)
+    al = None if c["align"] is None else torch.from_numpy(c["align"]).to(dev)
+    costs = op.monotonic_rnnt_loss(a, lab, torch.from_numpy(T), torch.from_numpy(S), al, c["k"], c["blank"])
+    (costs * torch.from_numpy(c["scale"]).to(dev)).sum().backward()
+    g = a.grad.float().cpu().numpy()
+    if c["padded"]:
+        pad_rows = np.ones(g.shape[:3], bool)
+        for b in range(len(T)):
+            pad_rows[b, : T[b], : S[b] + 1] = False
+        assert np.all(g[pad_rows] == 0.0)  # padding rows of the gradient are zero
+        g = unpad(g, T, S)
+    cr, gr = O.oracle_rnnt(host, c["labels"], T, S, blank=c["blank"], alignment=c["align"], max_shift=c["k"],
+                           num_threads=8)
+    gr = gr * np.repeat(c["scale"].astype(np.float64), T.astype(np.int64) * (S + 1))[:, None]
+    cc = costs.detach().float().cpu().numpy().astype(np.float64)
+    fin = np.isfinite(cr)
+    assert np.array_equal(np.isfinite(cc), fin), (cc, cr)
+    if fin.any():
+        err = np.abs(cc[fin] - cr[fin]) / np.maximum(1.0, np.abs(cr[fin]))
+        assert err.max() <= 1e-4, (err.max(), cc, cr)
+    gfin = np.isfinite(gr)
+    assert np.array_equal(np.isfinite(g), gfin)
+    rel = {"f32": 0.0, "bf16": 2.0 ** -8, "f16": 2.0 ** -11}[c["dtype"]]
+    tol = 1e-4 + rel * np.abs(gr[gfin])
+    assert np.all(np.abs(g[gfin] - gr[gfin]) <= tol), np.abs(g[gfin] - gr[gfin]).max()

@@ -190,6 +190,30 @@ def test_invalid_lengths_raise(op, dev):
                                torch.tensor([4], dtype=torch.int32), torch.tensor([2], dtype=torch.int32))
 
 
+@pytest.mark.parametrize("poison", ["nan", "inf", "huge"])
+def test_stale_workspace_contents_do_not_matter(op, dev, monkeypatch, poison):
+    """The workspace comes from torch's caching allocator holding earlier data (the NaN padding of a padded acts
+    tensor, say). Found by tests/test_gpu_fuzz.py: utterance 0's alpha(0, 0) read lpe[-1] from the lp pad."""
+    orig = op._Prepared.workspace
+    byte = {"nan": 0xFF, "huge": 0x7F}.get(poison)  # all-0xFF doubles are NaN, all-0x7F ones 1.4e306
+
+    def poisoned(self):
+        ws = orig(self)
+        if byte is not None:
+            ws.fill_(byte)
+        else:  # +inf doubles over the 8-byte-aligned part
+            ws[: ws.numel() // 8 * 8].view(torch.float64).fill_(float("inf"))
+        return ws
+    monkeypatch.setattr(op._Prepared, "workspace", poisoned)
+    rng = np.random.default_rng(5)
+    for Tr, Smax, V in (((20, 40), 7, 64), ((60, 90), 59, 33), ((150, 200), 120, 16)):  # 1 wave, 1 wave, halo
+        acts, labels, T, S = random_problem(rng, 3, Tr, Smax, V, force={0: (Tr[1], Smax)})
+        c, g = run_gpu(op, dev, acts, labels, T, S)
+        cr, gr = O.oracle_rnnt(acts, labels, T, S)
+        assert_costs(c, cr)
+        assert_grads(g, gr)
+
+
 def test_loglik_forward_equals_backward(op, dev):
     """beta(0,0) == alpha(T-1,S): the two recursions run independently (cpu_rnnt.h:257-259 check)."""
     import ctypes
