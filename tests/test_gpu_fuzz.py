@@ -2,8 +2,9 @@
 kernel variants switch on: V (vector width, chunking, FULL / ragged rows, V < 4, odd V), S+1 (single-wave /
 halo / per-step-barrier recursion, gradient segments of 256 rows), blank anywhere in [0, V), labels that may equal
 the blank, alignment restriction with random k, per-utterance gradient scales (negative and zero included),
-packed and padded layouts, f32 / bf16 / f16 acts. Tolerances as tests/test_gpu_parity.py (reduced precision:
-the grads tolerance adds one rounding of the acts type).
+packed and padded layouts, f32 / bf16 / f16 acts; then the same generator through the other launch variants.
+Tolerances as tests/test_gpu_parity.py (reduced precision: the grads tolerance adds one rounding of the acts type).
+The sweep found the stale-workspace bug pinned by test_gpu_parity.py::test_stale_workspace_contents_do_not_matter.
 """
 import numpy as np
 import pytest
@@ -78,7 +79,34 @@ def unpad(x, T, S):
 
 @pytest.mark.parametrize("seed", range(N_CASES))
 def test_random_case_vs_oracle(op, dev, seed):
-    c = make_case(seed)
+    check_case(op, dev, make_case(seed), cost_only_too=(seed % 4 == 0))
+
+
+KNOB_SETS = [
+    {"dp_halo": 0},                                  # per-step-barrier recursion at every S
+    {"softmax_variant": 0, "grad_variant": 2},       # first log-softmax, per-row gradient
+    {"grad_variant": 3, "nt_load": 0, "nt_store": 0},  # row-sweep gradient, plain loads / stores
+    {"softmax_variant": 14, "grad_variant": 6, "col_scatter": 0},
+    {"occ_skip": 0, "softmax_variant": 15},
+]
+
+
+@pytest.mark.parametrize("knobs", range(len(KNOB_SETS)))
+@pytest.mark.parametrize("seed", range(1000, 1024))
+def test_random_case_other_kernels(op, dev, knobs, seed):
+    """The same sweep through the other launch variants (mrnnt_tune), 24 cases each."""
+    import _mrnnt_lib as L
+    saved = {k: L.tune(k) for k in KNOB_SETS[knobs]}
+    try:
+        for k, v in KNOB_SETS[knobs].items():
+            assert L.tune(k, v) >= 0, k
+        check_case(op, dev, make_case(seed))
+    finally:
+        for k, v in saved.items():
+            L.tune(k, v)
+
+
+def check_case(op, dev, c, cost_only_too=False):
     T, S, V = c["T"], c["S"], c["V"]
     tdt = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}[c["dtype"]]
     a = torch.from_numpy(c["acts"]).to(tdt)
@@ -111,3 +139,6 @@ def test_random_case_vs_oracle(op, dev, seed):
     rel = {"f32": 0.0, "bf16": 2.0 ** -8, "f16": 2.0 ** -11}[c["dtype"]]
     tol = 1e-4 + rel * np.abs(gr[gfin])
     assert np.all(np.abs(g[gfin] - gr[gfin]) <= tol), np.abs(g[gfin] - gr[gfin]).max()
+    if cost_only_too:  # the cost-only forward (no beta pass) gives the same costs bit for bit
+        c2 = op.monotonic_rnnt_loss(a.detach(), lab, torch.from_numpy(T), torch.from_numpy(S), al, c["k"], c["blank"])
+        assert np.array_equal(c2.float().cpu().numpy().astype(np.float64), cc)

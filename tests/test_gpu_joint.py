@@ -88,14 +88,14 @@ def run_joint(jop, dev, enc, pred, w, bias, labels, T, S, blank=0, scale=None, a
     e = enc.to(dev).requires_grad_(True)
     p = pred.to(dev).requires_grad_(True)
     ww = w.to(dev).requires_grad_(True)
-    bb = bias.to(dev).requires_grad_(True)
+    bb = None if bias is None else bias.to(dev).requires_grad_(True)
     al = None if alignment is None else torch.from_numpy(alignment).to(dev)
     costs = jop.monotonic_rnnt_joint_loss(e, p, ww, bb, torch.from_numpy(labels).to(dev), torch.from_numpy(T),
                                           torch.from_numpy(S), blank, al, k)
     sc = torch.ones(len(T), device=dev) if scale is None else torch.tensor(scale, dtype=torch.float32, device=dev)
     (costs * sc).sum().backward()
     torch.cuda.synchronize()
-    return costs.detach().cpu().double().numpy(), e.grad, p.grad, ww.grad, bb.grad
+    return costs.detach().cpu().double().numpy(), e.grad, p.grad, ww.grad, None if bb is None else bb.grad
 
 
 @pytest.mark.parametrize("H,V", [(128, 64), (256, 100), (256, 1000), (512, 256), (384, 96), (640, 130)])
@@ -147,6 +147,51 @@ def test_joint_matches_materialised_acts_path(jop, dev):
     c_acts = op.monotonic_rnnt_loss(acts, torch.from_numpy(labels).to(dev), torch.from_numpy(T),
                                     torch.from_numpy(S)).cpu().double().numpy()
     assert np.all(np.abs(c_fused - c_acts) <= 1e-3 * np.maximum(1.0, np.abs(c_acts))), (c_fused, c_acts)
+
+
+@pytest.mark.parametrize("seed", range(32))
+def test_joint_random_cases(jop, dev, seed):
+    """Seeded sweep over the fused path's switches: every supported H, V with and without a tail chunk (V < 32
+    included), blank anywhere, labels that may equal the blank, no bias, ragged lengths with S = 0 and T = S,
+    alignment restriction, negative / zero gradient scales."""
+    rng = np.random.default_rng(7000 + seed)
+    H = int(rng.choice([128, 256, 384, 512, 640]))
+    V = int(rng.choice([2, 3, 17, 32, 64, 100, 130, 256, 1000, 1030]))
+    B = int(rng.integers(1, 5))
+    enc, pred, w, bias, labels, T, S = make_case(int(rng.integers(1 << 30)), B, (1, int(rng.choice([8, 30, 60]))),
+                                                 int(rng.choice([0, 4, 12, 30])), H, V,
+                                                 scale_in=float(rng.choice([0.5, 1.0, 2.0])))
+    if rng.random() < 0.3:  # T = S somewhere
+        T[0] = max(int(S[0]), 1)
+    blank = int(rng.integers(0, V))
+    labels = rng.integers(0, V, labels.shape).astype(np.int32)
+    if rng.random() < 0.7:
+        labels[labels == blank] = (blank + 1) % V
+    if rng.random() < 0.25:
+        bias = None
+    scale = rng.choice([1.0, -0.5, 0.0, 2.0], B).tolist()
+    al, k = None, 0
+    if rng.random() < 0.3:
+        k = int(rng.integers(0, 4))
+        al = np.full((B, int(T.max())), blank, np.int32)
+        for b in range(B):
+            fr = np.sort(rng.choice(int(T[b]), int(S[b]), replace=False))
+            al[b, fr] = np.where(labels[b, : S[b]] == blank, (blank + 1) % V, labels[b, : S[b]])
+    c, de, dp, dw, db = run_joint(jop, dev, enc, pred, w, bias, labels, T, S, blank=blank, scale=scale,
+                                  alignment=al, k=k)
+    bias_ref = torch.zeros(V) if bias is None else bias
+    cr, de_r, dp_r, dw_r, db_r = host_reference(enc, pred, w, bias_ref, labels, T, S, blank=blank, scale=scale,
+                                                alignment=al, k=k)
+    fin = np.isfinite(cr)
+    assert np.array_equal(np.isfinite(c), fin), (c, cr)
+    assert np.all(np.abs(c[fin] - cr[fin]) <= 1e-5 * np.maximum(1.0, np.abs(cr[fin]))), (c, cr)
+    close(de, de_r, name="d_enc")
+    close(dp, dp_r, name="d_pred")
+    close(dw, dw_r, name="d_weight")
+    if bias is not None:
+        close(db, db_r, name="d_bias")
+    for b in range(B):
+        assert torch.all(de[b, T[b]:] == 0) and torch.all(dp[b, S[b] + 1:] == 0)
 
 
 @pytest.mark.parametrize("k", [0, 2])
