@@ -195,17 +195,40 @@ struct ProfRec {
 std::mutex g_prof_mu;
 bool g_prof_on = false;
 std::vector<ProfRec> g_prof;
+// events are created ahead (mrnnt_profile_enable) and recycled, so a timed launch adds two event records and
+// no hipEventCreate to the host path it measures (that matters for 0.1 ms steps)
+std::vector<hipEvent_t> g_event_pool;
+constexpr size_t kEventPrealloc = 2048;
+
+// timing-only events: no system-scope fence at record (a cache writeback + invalidate between the timed kernels
+// would slow the launches being measured)
+hipError_t make_timing_event(hipEvent_t *e) { return hipEventCreateWithFlags(e, hipEventDisableSystemFence); }
+
+hipEvent_t pooled_event() {  // g_prof_mu held
+    if (!g_event_pool.empty()) {
+        const hipEvent_t e = g_event_pool.back();
+        g_event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    return make_timing_event(&e) == hipSuccess ? e : nullptr;
+}
 
 template <class F>
 hipError_t timed(int id, hipStream_t s, F &&launch) {
-    bool on;
+    ProfRec r{id, nullptr, nullptr};
     {
         std::lock_guard<std::mutex> lk(g_prof_mu);
-        on = g_prof_on;
+        if (!g_prof_on) return launch();
+        r.a = pooled_event();
+        r.b = pooled_event();
+        if (!r.a || !r.b) {
+            if (r.a) g_event_pool.push_back(r.a);
+            if (r.b) g_event_pool.push_back(r.b);
+            r.a = r.b = nullptr;
+        }
     }
-    if (!on) return launch();
-    ProfRec r{id, nullptr, nullptr};
-    if (hipEventCreate(&r.a) != hipSuccess || hipEventCreate(&r.b) != hipSuccess) return launch();
+    if (!r.a) return launch();
     (void)hipEventRecord(r.a, s);
     const hipError_t e = launch();
     (void)hipEventRecord(r.b, s);
@@ -539,12 +562,17 @@ RNNTStatus mrnnt_joint_reduce(const mrnnt_joint_problem *jp, void *ws, int64_t n
 
 void mrnnt_profile_enable(int enable) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
-    for (auto &r : g_prof) {
-        (void)hipEventDestroy(r.a);
-        (void)hipEventDestroy(r.b);
+    for (auto &r : g_prof) {  // recycled: a record still pending is complete before the event is recorded again
+        g_event_pool.push_back(r.a);
+        g_event_pool.push_back(r.b);
     }
     g_prof.clear();
     g_prof_on = enable != 0;
+    while (g_prof_on && g_event_pool.size() < kEventPrealloc) {
+        hipEvent_t e = nullptr;
+        if (make_timing_event(&e) != hipSuccess) break;
+        g_event_pool.push_back(e);
+    }
 }
 
 int mrnnt_profile_read(double *total_ms, int64_t *launches, int n) {
