@@ -95,6 +95,11 @@ def test_workspace_size_and_validation(lib):
     assert lib.mrnnt_workspace_size(ctypes.byref(p), ctypes.byref(n)) == L.RNNT_STATUS_INVALID_VALUE
     p, keep = _problem([4], [2], V=3, blank=3)  # blank out of range
     assert lib.mrnnt_workspace_size(ctypes.byref(p), ctypes.byref(n)) == L.RNNT_STATUS_INVALID_VALUE
+    p, keep = _problem([2100], [2047])  # the largest label length the recursion covers (S + 1 = 2048)
+    assert lib.mrnnt_workspace_size(ctypes.byref(p), ctypes.byref(n)) == L.RNNT_STATUS_SUCCESS
+    p, keep = _problem([2100], [2048])
+    assert lib.mrnnt_workspace_size(ctypes.byref(p), ctypes.byref(n)) == L.RNNT_STATUS_INVALID_VALUE
+    assert b"exceeds 2047" in lib.mrnnt_last_error()
 
 
 def test_forward_rejects_bad_arguments_without_touching_gpu(lib):

@@ -106,6 +106,22 @@ def test_random_case_other_kernels(op, dev, knobs, seed):
             L.tune(k, v)
 
 
+@pytest.mark.parametrize("B,V,dtype", [(300, 16, "f32"), (1000, 33, "f32"), (257, 64, "bf16")])
+def test_many_utterances(op, dev, B, V, dtype):
+    """Batches wider than the setup scan's 64-lane chunks, with T = 1 / S = 0 utterances among them."""
+    rng = np.random.default_rng(B)
+    T = rng.integers(1, 30, B).astype(np.int32)
+    T[:3] = 1
+    S = np.array([rng.integers(0, t + 1) for t in T], np.int32)
+    S[1] = 0
+    labels = rng.integers(1, V, (B, max(1, int(S.max())))).astype(np.int32)
+    rows = int(np.sum(T.astype(np.int64) * (S + 1)))
+    acts = rng.standard_normal((rows, V)).astype(np.float32)
+    c = dict(V=V, T=T, S=S, blank=0, labels=labels, acts=acts, scale=rng.choice([1.0, -0.5], B).astype(np.float32),
+             align=None, k=0, dtype=dtype, padded=False)
+    check_case(op, dev, c, cost_only_too=True)
+
+
 def check_case(op, dev, c, cost_only_too=False):
     T, S, V = c["T"], c["S"], c["V"]
     tdt = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}[c["dtype"]]

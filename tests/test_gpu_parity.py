@@ -336,7 +336,8 @@ def test_every_kernel_variant_matches_oracle(op, dev, knobs):
             L.tune(k, v)
 
 
-@pytest.mark.parametrize("S_len,T_len,V", [(1100, 1200, 16), (64, 64, 8), (128, 300, 12), (511, 530, 8)])
+@pytest.mark.parametrize("S_len,T_len,V", [(1100, 1200, 16), (64, 64, 8), (128, 300, 12), (511, 530, 8),
+                                           (2047, 2060, 4)])
 def test_long_label_sequences_vs_oracle(op, dev, S_len, T_len, V):
     """Label lengths across the recursion's wave/cell sizing boundaries (S+1 = 65, 129, 512, 1101)."""
     rng = np.random.default_rng(S_len)
