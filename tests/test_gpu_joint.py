@@ -11,6 +11,8 @@ Tolerances (floating-point extension on bf16 matrix cores, stated here):
   grads : max |dg| <= 1.5e-2 * max |g_ref| + 1e-5 per tensor (the logit gradient is stored as bf16, 2^-9 relative,
                                          and dH = G weight runs as a bf16 GEMM)
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -45,7 +47,7 @@ def make_case(seed, B, Trange, Smax, H, V, scale_in=1.0):
     return enc, pred, w, bias, labels, T, S
 
 
-def host_reference(enc, pred, w, bias, labels, T, S, blank=0, scale=None, alignment=None, k=0):
+def host_reference(enc, pred, w, bias, labels, T, S, blank=0, scale=None, alignment=None, k=0, extra=None):
     B = len(T)
     W64 = w.double()
     hs, rows = [], []
@@ -60,6 +62,8 @@ def host_reference(enc, pred, w, bias, labels, T, S, blank=0, scale=None, alignm
     if scale is not None:
         dz = dz * np.repeat(np.asarray(scale, np.float64), T * (S + 1))[:, None]
     dz = torch.from_numpy(dz)
+    if extra is not None:  # column sums of |dz|: what d_bias = sum_rows dz cancels from
+        extra["dz_abs_colsum"] = dz.abs().sum(0)
     d_enc = torch.zeros(enc.shape, dtype=torch.float64)
     d_pred = torch.zeros(pred.shape, dtype=torch.float64)
     d_w = torch.zeros(w.shape, dtype=torch.float64)
@@ -149,11 +153,7 @@ def test_joint_matches_materialised_acts_path(jop, dev):
     assert np.all(np.abs(c_fused - c_acts) <= 1e-3 * np.maximum(1.0, np.abs(c_acts))), (c_fused, c_acts)
 
 
-@pytest.mark.parametrize("seed", range(32))
-def test_joint_random_cases(jop, dev, seed):
-    """Seeded sweep over the fused path's switches: every supported H, V with and without a tail chunk (V < 32
-    included), blank anywhere, labels that may equal the blank, no bias, ragged lengths with S = 0 and T = S,
-    alignment restriction, negative / zero gradient scales."""
+def random_joint_case(seed):
     rng = np.random.default_rng(7000 + seed)
     H = int(rng.choice([128, 256, 384, 512, 640]))
     V = int(rng.choice([2, 3, 17, 32, 64, 100, 130, 256, 1000, 1030]))
@@ -177,11 +177,23 @@ def test_joint_random_cases(jop, dev, seed):
         for b in range(B):
             fr = np.sort(rng.choice(int(T[b]), int(S[b]), replace=False))
             al[b, fr] = np.where(labels[b, : S[b]] == blank, (blank + 1) % V, labels[b, : S[b]])
+    return enc, pred, w, bias, labels, T, S, blank, scale, al, k
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("MRNNT_FUZZ_FIRST", "0")),
+                                  int(os.environ.get("MRNNT_FUZZ_FIRST", "0")) + int(os.environ.get("MRNNT_JOINT_CASES", "32"))))
+def test_joint_random_cases(jop, dev, seed):
+    """Seeded sweep over the fused path's switches: every supported H, V with and without a tail chunk (V < 32
+    included), blank anywhere, labels that may equal the blank, no bias, ragged lengths with S = 0 and T = S,
+    alignment restriction, negative / zero gradient scales."""
+    enc, pred, w, bias, labels, T, S, blank, scale, al, k = random_joint_case(seed)
+    B, V = len(T), w.shape[0]
     c, de, dp, dw, db = run_joint(jop, dev, enc, pred, w, bias, labels, T, S, blank=blank, scale=scale,
                                   alignment=al, k=k)
     bias_ref = torch.zeros(V) if bias is None else bias
+    ex = {}
     cr, de_r, dp_r, dw_r, db_r = host_reference(enc, pred, w, bias_ref, labels, T, S, blank=blank, scale=scale,
-                                                alignment=al, k=k)
+                                                alignment=al, k=k, extra=ex)
     fin = np.isfinite(cr)
     assert np.array_equal(np.isfinite(c), fin), (c, cr)
     assert np.all(np.abs(c[fin] - cr[fin]) <= 1e-5 * np.maximum(1.0, np.abs(cr[fin]))), (c, cr)
@@ -189,7 +201,11 @@ def test_joint_random_cases(jop, dev, seed):
     close(dp, dp_r, name="d_pred")
     close(dw, dw_r, name="d_weight")
     if bias is not None:
-        close(db, db_r, name="d_bias")
+        # d_bias sums G (stored as bf16) over rows: with V = 2 or 3 it can cancel to ~1 % of sum |G|, so the bound
+        # adds two bf16 roundings of that sum (found by the 400-case sweep, seeds 223 / 334: V = 2)
+        lim = 1.5e-2 * db_r.abs().max().item() + 2.0 ** -8 * ex["dz_abs_colsum"].max().item() + 1e-5
+        err = (db.double().cpu() - db_r).abs().max().item()
+        assert err <= lim, ("d_bias", err, lim)
     for b in range(B):
         assert torch.all(de[b, T[b]:] == 0) and torch.all(dp[b, S[b] + 1:] == 0)
 
