@@ -209,6 +209,13 @@ __device__ __forceinline__ double alpha_prev(const DevProblem &p, int t, int s, 
     return (t == 0) ? (s == 0 ? 0.0 : NEG_INF_D) : p.alpha[row - W];
 }
 
+// Value of a row whose gradient is not computed (out of band, or dead), times the upstream gradient: the
+// reference forms every row as exp(... - ll) (cpu_rnnt.h:221-231), i.e. 0 for a finite log-likelihood and NaN
+// for ll = -inf (no path survives, e.g. an alignment band that excludes them all) or NaN.
+__device__ __forceinline__ float zero_row_value(double ll, float sc) {
+    return (ll > NEG_INF_D ? 0.0f : __builtin_nanf("")) * sc;
+}
+
 // The dead-row predicate (mrnnt_internal.h kDeadLogOcc); NaN state is live.
 __device__ __forceinline__ bool row_live(double log_occ) { return !(log_occ < kDeadLogOcc); }
 

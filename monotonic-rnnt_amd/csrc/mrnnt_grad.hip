@@ -6,8 +6,8 @@
 // times grad_scale[b]. Per row the three coefficients are formed in fp64 from the recursion state; per
 // element it is one fma + one v_exp_f32 (+ a select for the <= 2 special columns) in fp32 registers,
 // then one conversion to the output element type. Out-of-band lattice rows store 0 * grad_scale (the
-// reference's backward multiplies its zero rows by grad_output); padding rows of the padded layout
-// store 0 (launch_pad_zero).
+// reference's backward multiplies its zero rows by grad_output; NaN when ll = -inf, zero_row_value); padding
+// rows of the padded layout store 0 (launch_pad_zero).
 #include <algorithm>
 
 #include "mrnnt_device.h"
@@ -58,7 +58,7 @@ __global__ __launch_bounds__(256) void grad_kernel(DevProblem p, const float *__
         const int hi = min(t, S);
         const double ll = p.ll[b];
         const float sc = scale ? scale[b] : 1.0f;
-        const Vec zv = splat<IO>(0.0f * sc);
+        const Vec zv = splat<IO>(zero_row_value(ll, sc));
         const int *__restrict__ lab_b = p.labels + (int64_t)b * p.label_stride;
 
         for (int s = wave * R; s <= S; s += 4 * R) {
@@ -136,7 +136,7 @@ __global__ __launch_bounds__(256) void grad_staged_kernel(DevProblem p, const fl
         const int hi = min(t, S);
         const double ll = p.ll[b];
         const float sc = scale ? scale[b] : 1.0f;
-        const Vec zv = splat<IO>(0.0f * sc);
+        const Vec zv = splat<IO>(zero_row_value(ll, sc));
         const int *__restrict__ lab_b = p.labels + (int64_t)b * p.label_stride;
 
         for (int seg = 0; seg <= S; seg += SEG, buf ^= 1) {
@@ -220,7 +220,7 @@ __global__ __launch_bounds__(256) void grad_rows_kernel(DevProblem p, const floa
         RowCoef rc;
         if (inb) rc = row_coef(p, t, T, S, s, row, p.ll[b], p.labels + (int64_t)b * p.label_stride);
         if (!inb || !rc.live) {
-            const Vec zv = splat<IO>(0.0f * sc);
+            const Vec zv = splat<IO>(zero_row_value(p.ll[b], sc));
             for (int j = lane; j < VL; j += 64) vstore<NTS>(out + j, zv);
             continue;
         }
@@ -264,7 +264,7 @@ __global__ __launch_bounds__(256) void grad_scalar_kernel(DevProblem p, const fl
         const int hi = min(t, S);
         const double ll = p.ll[b];
         const float sc = scale ? scale[b] : 1.0f;
-        const Sc zs = IO::from_f(0.0f * sc);
+        const Sc zs = IO::from_f(zero_row_value(ll, sc));
         const int *__restrict__ lab_b = p.labels + (int64_t)b * p.label_stride;
         for (int s = wave; s <= S; s += 4) {
             Sc *__restrict__ g = gs + (arow + s) * (int64_t)V;

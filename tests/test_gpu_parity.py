@@ -145,6 +145,29 @@ def test_alignment_restricted_vs_oracle(op, dev, k):
     assert_grads(g, gr)
 
 
+@pytest.mark.parametrize("V", [1, 5, 64])
+def test_infeasible_alignment_matches_reference_inf_nan(op, dev, V):
+    """An alignment band that no path satisfies (fewer aligned labels than S, k = 0): the reference's cost is +inf
+    and every gradient element of that utterance is NaN/inf (exp(... - ll) with ll = -inf, cpu_rnnt.h:221-231),
+    out-of-band rows included; the other utterance is unaffected. V = 1: blank only, labels parse as blanks."""
+    rng = np.random.default_rng(V)
+    acts, labels, T, S = random_problem(rng, 2, (12, 20), 6, max(V, 2), force={0: (15, 5), 1: (14, 4)})
+    acts = np.ascontiguousarray(acts[:, :V])
+    labels = np.where(labels >= V, 0, labels).astype(np.int32) if V > 1 else np.zeros_like(labels)
+    if V > 1:
+        labels = np.where(labels == 0, 1, labels).astype(np.int32)
+    al = np.zeros((2, 15), np.int32)
+    al[0, [2, 7]] = 1 if V > 1 else 0           # 2 (or 0) aligned labels for S = 5: infeasible
+    al[1, np.sort(rng.choice(14, 4, replace=False))] = labels[1, :4] if V > 1 else 0
+    c, g = run_gpu(op, dev, acts, labels, T, S, alignment=al, k=0, scale=[1.0, -0.5])
+    cr, gr = O.oracle_rnnt(acts, labels, T, S, alignment=al, max_shift=0)
+    gr = gr * np.repeat(np.array([1.0, -0.5]), T * (S + 1))[:, None]
+    assert np.isinf(cr[0]) and np.isinf(c[0])
+    assert not np.isfinite(g[: 15 * 6]).any()
+    assert_costs(c, cr)
+    assert_grads(g, gr)
+
+
 def test_grad_output_scaling_fused(op, dev):
     rng = np.random.default_rng(5)
     acts, labels, T, S = random_problem(rng, 4, (5, 30), 8, 128)
