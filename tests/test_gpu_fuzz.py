@@ -19,6 +19,8 @@ pytestmark = pytest.mark.gpu
 N_CASES = int(os.environ.get("MRNNT_FUZZ_CASES", "160"))  # round-end suite: 160; long sweeps: set it higher
 FIRST = int(os.environ.get("MRNNT_FUZZ_FIRST", "0"))
 V_CHOICES = [int(v) for v in os.environ.get("MRNNT_FUZZ_V", "2,3,5,16,31,64,100,255,256,257,1000,1024,1030,2048").split(",")]
+ACT_SCALES = [float(v) for v in os.environ.get("MRNNT_FUZZ_SCALE", "0.5,1,3").split(",")]  # logit spread
+T_EXTRA = int(os.environ.get("MRNNT_FUZZ_T_EXTRA", "40"))  # frames beyond the label cap
 
 
 @pytest.fixture(scope="module")
@@ -43,7 +45,7 @@ def make_case(seed):
         s_cap = min(s_cap, 130)  # keep the oracle's work small
     if V >= 4000:
         s_cap = min(s_cap, 40)
-    T = rng.integers(1, s_cap + 40, B).astype(np.int32)
+    T = rng.integers(1, s_cap + T_EXTRA, B).astype(np.int32)
     S = np.array([rng.integers(0, min(int(t), s_cap) + 1) for t in T], np.int32)
     blank = int(rng.integers(0, V))
     L = max(1, int(S.max()))
@@ -51,7 +53,7 @@ def make_case(seed):
     if rng.random() < 0.7:  # mostly labels != blank, as in training data
         labels[labels == blank] = (blank + 1) % V if V > 1 else blank
     rows = int(np.sum(T.astype(np.int64) * (S + 1)))
-    acts = (rng.standard_normal((rows, V)) * rng.choice([0.5, 1.0, 3.0])).astype(np.float32)
+    acts = (rng.standard_normal((rows, V)) * rng.choice(ACT_SCALES)).astype(np.float32)
     scale = rng.choice([1.0, -0.5, 0.0, 2.0, 0.25], B).astype(np.float32)
     align, k = None, 0
     if rng.random() < 0.3:
