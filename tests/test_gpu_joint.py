@@ -158,8 +158,10 @@ def random_joint_case(seed):
     H = int(rng.choice([128, 256, 384, 512, 640]))
     V = int(rng.choice([2, 3, 17, 32, 64, 100, 130, 256, 1000, 1030]))
     B = int(rng.integers(1, 5))
-    enc, pred, w, bias, labels, T, S = make_case(int(rng.integers(1 << 30)), B, (1, int(rng.choice([8, 30, 60]))),
-                                                 int(rng.choice([0, 4, 12, 30])), H, V,
+    big = os.environ.get("MRNNT_JOINT_BIG") == "1"  # long utterances: occupancy skip, many row tiles
+    t_caps, s_caps = ([100, 200], [20, 60, 90]) if big else ([8, 30, 60], [0, 4, 12, 30])
+    enc, pred, w, bias, labels, T, S = make_case(int(rng.integers(1 << 30)), B, (1, int(rng.choice(t_caps))),
+                                                 int(rng.choice(s_caps)), H, V,
                                                  scale_in=float(rng.choice([0.5, 1.0, 2.0])))
     if rng.random() < 0.3:  # T = S somewhere
         T[0] = max(int(S[0]), 1)
