@@ -79,15 +79,16 @@ __global__ __launch_bounds__(64) void align_prefix_kernel(DevProblem p, const in
 
 __global__ __launch_bounds__(256) void align_band_kernel(DevProblem p, int k, const int *__restrict__ m,
                                                          int *__restrict__ min_s, int *__restrict__ max_s) {
-    const int b = blockIdx.y;
-    const int T = p.T[b];
-    const int64_t mb = p.col_off[b] + b;
-    const int64_t cb = p.col_off[b];
-    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < T; t += gridDim.x * blockDim.x) {
-        const int i0 = min(max(0, t + 1 - k), T);
-        const int i1 = max(0, min(T, t + 1 + k));
-        min_s[cb + t] = m[mb + i0];
-        max_s[cb + t] = m[mb + i1];
+    for (int b = blockIdx.y; b < p.B; b += gridDim.y) {  // grid y is capped at 65535 utterances per pass
+        const int T = p.T[b];
+        const int64_t mb = p.col_off[b] + b;
+        const int64_t cb = p.col_off[b];
+        for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < T; t += gridDim.x * blockDim.x) {
+            const int i0 = min(max(0, t + 1 - k), T);
+            const int i1 = max(0, min(T, t + 1 + k));
+            min_s[cb + t] = m[mb + i0];
+            max_s[cb + t] = m[mb + i1];
+        }
     }
 }
 
@@ -140,7 +141,7 @@ hipError_t launch_align(const DevProblem &p, const int *alignment, int64_t align
     align_prefix_kernel<<<p.B, 64, 0, stream>>>(p, alignment, align_stride, align_blank, mtmp);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    align_band_kernel<<<dim3(8, p.B), 256, 0, stream>>>(p, max_shift, mtmp, min_s, max_s);
+    align_band_kernel<<<dim3(8, std::min(p.B, 65535)), 256, 0, stream>>>(p, max_shift, mtmp, min_s, max_s);
     return hipGetLastError();
 }
 

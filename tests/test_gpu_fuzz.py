@@ -130,6 +130,23 @@ def test_many_utterances(op, dev, B, V, dtype):
     check_case(op, dev, c, cost_only_too=True)
 
 
+def test_more_utterances_than_grid_y_with_alignment(op, dev):
+    """B = 70000 > 65535 (the largest grid y dimension, which the alignment band kernel walks) with alignment."""
+    rng = np.random.default_rng(70000)
+    B, V = 70000, 4
+    T = rng.integers(1, 4, B).astype(np.int32)
+    S = np.array([rng.integers(0, t + 1) for t in T], np.int32)
+    labels = rng.integers(1, V, (B, max(1, int(S.max())))).astype(np.int32)
+    align = np.zeros((B, int(T.max())), np.int32)
+    for b in range(B):
+        align[b, np.sort(rng.choice(int(T[b]), int(S[b]), replace=False))] = labels[b, : S[b]]
+    rows = int(np.sum(T.astype(np.int64) * (S + 1)))
+    acts = rng.standard_normal((rows, V)).astype(np.float32)
+    c = dict(V=V, T=T, S=S, blank=0, labels=labels, acts=acts, scale=np.ones(B, np.float32), align=align, k=1,
+             dtype="f32", padded=False)
+    check_case(op, dev, c)
+
+
 def check_case(op, dev, c, cost_only_too=False):
     T, S, V = c["T"], c["S"], c["V"]
     tdt = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}[c["dtype"]]
