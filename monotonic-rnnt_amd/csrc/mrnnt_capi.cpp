@@ -182,7 +182,9 @@ int streaming_grid(int64_t cols, int per_cu) {
     }
     // per_cu workgroups of 4 waves per CU walking the columns grid-stride, never more than the columns;
     // per_cu == 0: one workgroup per column (hardware-scheduled)
-    const int64_t g = per_cu <= 0 ? std::min<int64_t>(cols, 0x7fffffff) : (int64_t)cu_count[dev] * per_cu;
+    // (the hardware-scheduled grid is capped at 2^22 workgroups: the dispatch size in work-items is 32-bit, and
+    // every streaming kernel walks its columns grid-stride, so larger problems just take more than one turn)
+    const int64_t g = per_cu <= 0 ? std::min<int64_t>(cols, 1 << 22) : (int64_t)cu_count[dev] * per_cu;
     return (int)std::max<int64_t>(1, std::min<int64_t>(g, cols));
 }
 

@@ -147,6 +147,21 @@ def test_more_utterances_than_grid_y_with_alignment(op, dev):
     check_case(op, dev, c)
 
 
+def test_more_columns_than_a_32bit_dispatch(op, dev):
+    """17 M lattice columns: one 256-thread workgroup per column would be 4.4 G work-items, past the 32-bit
+    dispatch size; the streaming kernels cap their grid and walk the columns grid-stride."""
+    rng = np.random.default_rng(17)
+    B, V = 17000, 4
+    T = np.full(B, 1000, np.int32)
+    S = (rng.random(B) < 0.01).astype(np.int32)  # mostly S = 0, a few S = 1
+    labels = rng.integers(1, V, (B, 1)).astype(np.int32)
+    rows = int(np.sum(T.astype(np.int64) * (S + 1)))
+    acts = rng.standard_normal((rows, V)).astype(np.float32)
+    c = dict(V=V, T=T, S=S, blank=0, labels=labels, acts=acts, scale=np.ones(B, np.float32), align=None, k=0,
+             dtype="f32", padded=False)
+    check_case(op, dev, c)
+
+
 def check_case(op, dev, c, cost_only_too=False):
     T, S, V = c["T"], c["S"], c["V"]
     tdt = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}[c["dtype"]]
