@@ -162,6 +162,22 @@ def test_more_columns_than_a_32bit_dispatch(op, dev):
     check_case(op, dev, c)
 
 
+@pytest.mark.parametrize("V,dtype", [(65539, "f32"), (100000, "f32"), (131072, "bf16")])
+def test_very_large_vocabulary(op, dev, V, dtype):
+    """Vocabularies far past the benchmark's 10000 (many chunks per row; V odd: the scalar kernels)."""
+    rng = np.random.default_rng(V)
+    T = np.array([7, 4, 1], np.int32)
+    S = np.array([3, 4, 0], np.int32)
+    blank = int(rng.integers(0, V))
+    labels = rng.integers(0, V, (3, 4)).astype(np.int32)
+    labels[labels == blank] = (blank + 1) % V
+    rows = int(np.sum(T * (S + 1)))
+    acts = (rng.standard_normal((rows, V)) * 2.0).astype(np.float32)
+    c = dict(V=V, T=T, S=S, blank=blank, labels=labels, acts=acts, scale=np.array([1.0, -0.5, 2.0], np.float32),
+             align=None, k=0, dtype=dtype, padded=False)
+    check_case(op, dev, c, cost_only_too=True)
+
+
 def check_case(op, dev, c, cost_only_too=False):
     T, S, V = c["T"], c["S"], c["V"]
     tdt = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}[c["dtype"]]
