@@ -26,6 +26,11 @@ T_EXTRA = int(os.environ.get("MRNNT_FUZZ_T_EXTRA", "40"))  # frames beyond the l
 @pytest.fixture(scope="module")
 def op():
     import monotonic_rnnt_op
+    import _mrnnt_lib as L
+    # long sweeps through another launch variant: MRNNT_FUZZ_TUNE="dp_halo=0,grad_variant=3"
+    for kv in filter(None, os.environ.get("MRNNT_FUZZ_TUNE", "").split(",")):
+        k, v = kv.split("=")
+        assert L.tune(k, int(v)) >= 0, k
     return monotonic_rnnt_op
 
 
