@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MRNNT_VERSION 2
+#define MRNNT_VERSION 3
 
 /* acts / grads element types */
 #define MRNNT_F32 0
@@ -121,6 +121,9 @@ typedef struct mrnnt_joint_problem {
     int64_t align_stride;
     int align_blank;
     int max_shift;
+    int64_t hact_ld;         /* (version 3) Hact row stride in elements, 0 = H; a multiple of 8 > H makes
+                                mrnnt_joint_backward write columns H .. hact_ld-1 of every row as [1, 0, ...],
+                                so that the dweight GEMM G^T Hact also yields dbias = sum_i G[i] in column H */
 } mrnnt_joint_problem;
 
 RNNTStatus mrnnt_joint_workspace_size(const mrnnt_joint_problem *p, size_t *bytes);
@@ -137,7 +140,8 @@ RNNTStatus mrnnt_joint_live_rows(const mrnnt_joint_problem *p, void *workspace, 
 /* After mrnnt_joint_live_rows: for live row i (n_live = the count it produced, read back by the caller),
  * G[i, :] = grad_scale[b] * dcost_b/dz (bf16 [n_live, V]), Hact[i, :] = tanh(enc + pred) (bf16 [n_live, H]),
  * bt_idx[i] = b*(enc_stride/H) + t and bs_idx[i] = b*(pred_stride/H) + s (int64; either may be NULL). Then
- * dweight = G^T Hact, dbias = sum_i G[i], and with dpre = (G weight) * (1 - Hact^2):
+ * dweight = G^T Hact, dbias = sum_i G[i] (= column H of G^T Hact when hact_ld > H), and with
+ * dpre = (G weight) * (1 - Hact^2):
  * denc[bt_idx[i]] += dpre[i], dpred[bs_idx[i]] += dpre[i]. grad_scale may be NULL (= 1). */
 RNNTStatus mrnnt_joint_backward(const mrnnt_joint_problem *p, void *workspace, int64_t n_live,
                                 const float *grad_scale, void *G, void *Hact, int64_t *bt_idx, int64_t *bs_idx,

@@ -396,6 +396,8 @@ RNNTStatus make_joint_plan(const mrnnt_joint_problem *jp, JointPlan *jl) {
         return fail(RNNT_STATUS_INVALID_VALUE, "joint H must be 128, 256, 384, 512 or 640 (got " + std::to_string(H) + ")");
     if (jp->enc_stride % 8 || jp->pred_stride % 8)
         return fail(RNNT_STATUS_INVALID_VALUE, "enc/pred utterance strides must be multiples of 8 elements");
+    if (jp->hact_ld != 0 && (jp->hact_ld < H || jp->hact_ld % 8))
+        return fail(RNNT_STATUS_INVALID_VALUE, "hact_ld must be 0 or a multiple of 8 that is >= H");
     if (jp->enc_stride < (int64_t)q.base.T_max * H || jp->pred_stride < (int64_t)(q.base.S_max + 1) * H)
         return fail(RNNT_STATUS_INVALID_VALUE, "enc/pred utterance strides smaller than max T * H / (max S + 1) * H");
     for (int b = 0; b < jp->B; ++b) {
@@ -437,6 +439,7 @@ JointArgs joint_args(const mrnnt_joint_problem *jp, const JointPlan &jl, void *w
     j.W = static_cast<const unsigned short *>(jp->weight);
     j.bias = jp->bias;
     j.H = jp->H;
+    j.hact_ld = jp->hact_ld ? jp->hact_ld : jp->H;
     j.lcol = reinterpret_cast<const int *>(w + jl.off_lcol);
     j.ls = reinterpret_cast<const int *>(w + jl.off_ls);
     j.n = n;

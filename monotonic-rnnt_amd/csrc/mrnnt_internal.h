@@ -57,7 +57,8 @@ struct JointArgs {
     const unsigned long long *n_dev;  // entries in the list, on the device (alignment windows), or nullptr
     // backward outputs, one row per list entry
     unsigned short *G;           // [n, V] bf16 dL/dz
-    unsigned short *Hact;        // [n, H] bf16 tanh(enc + pred)
+    unsigned short *Hact;        // [n, hact_ld] bf16 tanh(enc + pred) (columns >= H: [1, 0, ...])
+    int64_t hact_ld;             // Hact row stride (elements), >= H
     int64_t *bt_idx;             // [n] b * enc_sb / H + t   (row of enc viewed as [B * T_slots, H])
     int64_t *bs_idx;             // [n] b * pred_sb / H + s  (row of pred viewed as [B * S_slots, H])
     const float *scale;          // [B] upstream dL/dcost or nullptr

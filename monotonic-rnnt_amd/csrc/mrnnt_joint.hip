@@ -183,8 +183,15 @@ __device__ __forceinline__ void build_act(const JointArgs &j, const RowPos &q, i
             h[2 * w] = (__bf16)y.x;
             h[2 * w + 1] = (__bf16)y.y;
         }
-        if (STORE && v) *reinterpret_cast<bf16x8 *>(j.Hact + i * H + 16 * ks + 8 * half) = h;
+        if (STORE && v) *reinterpret_cast<bf16x8 *>(j.Hact + i * j.hact_ld + 16 * ks + 8 * half) = h;
         bfr[ks] = h;
+    }
+    if (STORE && v) {  // columns past H: a ones column (dbias from the dweight GEMM), then zeros
+        for (int64_t c = H + 8 * half; c < j.hact_ld; c += 16) {
+            bf16x8 e = {};
+            if (c == H) e[0] = (__bf16)1.0f;
+            *reinterpret_cast<bf16x8 *>(j.Hact + i * j.hact_ld + c) = e;
+        }
     }
 }
 
@@ -531,7 +538,7 @@ __global__ __launch_bounds__(256) void joint_reduce_kernel(DevProblem p, JointAr
         for (int64_t r = r0 + rsub; r < r1; r += RP) {
             const int s = j.ls[r];
             const uint2 dv = *reinterpret_cast<const uint2 *>(dH + r * H + h0 + hl);
-            const uint2 hv = *reinterpret_cast<const uint2 *>(j.Hact + r * H + h0 + hl);
+            const uint2 hv = *reinterpret_cast<const uint2 *>(j.Hact + r * j.hact_ld + h0 + hl);
             const float h_0 = bf16_lo(hv.x), h_1 = bf16_hi(hv.x), h_2 = bf16_lo(hv.y), h_3 = bf16_hi(hv.y);
             const float v0 = bf16_lo(dv.x) * (1.0f - h_0 * h_0), v1 = bf16_hi(dv.x) * (1.0f - h_1 * h_1);
             const float v2 = bf16_lo(dv.y) * (1.0f - h_2 * h_2), v3 = bf16_hi(dv.y) * (1.0f - h_3 * h_3);
@@ -613,7 +620,7 @@ __global__ __launch_bounds__(256) void joint_reduce_sparse_kernel(DevProblem p, 
         const int s = j.ls[r];
         const int tt = (int)(j.lcol[r] - c0 - t0);
         const uint2 dv = *reinterpret_cast<const uint2 *>(dH + r * H + h0 + hl);
-        const uint2 hv = *reinterpret_cast<const uint2 *>(j.Hact + r * H + h0 + hl);
+        const uint2 hv = *reinterpret_cast<const uint2 *>(j.Hact + r * j.hact_ld + h0 + hl);
         const float h_0 = bf16_lo(hv.x), h_1 = bf16_hi(hv.x), h_2 = bf16_lo(hv.y), h_3 = bf16_hi(hv.y);
         const float v[4] = {bf16_lo(dv.x) * (1.0f - h_0 * h_0), bf16_hi(dv.x) * (1.0f - h_1 * h_1),
                             bf16_lo(dv.y) * (1.0f - h_2 * h_2), bf16_hi(dv.y) * (1.0f - h_3 * h_3)};

@@ -77,6 +77,7 @@ class MrnntJointProblem(ctypes.Structure):
         ("align_stride", ctypes.c_int64),
         ("align_blank", ctypes.c_int),
         ("max_shift", ctypes.c_int),
+        ("hact_ld", ctypes.c_int64),
     ]
 
 
@@ -128,8 +129,8 @@ def load() -> ctypes.CDLL:
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.mrnnt_version() < 2:
-            raise ImportError(f"{LIB_PATH} is a stale build (ABI version {lib.mrnnt_version()} < 2); "
+        if lib.mrnnt_version() < 3:
+            raise ImportError(f"{LIB_PATH} is a stale build (ABI version {lib.mrnnt_version()} < 3); "
                               "rebuild with `make -C monotonic-rnnt_amd`")
         for kv in filter(None, os.environ.get("MRNNT_TUNE", "").split(",")):
             k, v = kv.split("=")

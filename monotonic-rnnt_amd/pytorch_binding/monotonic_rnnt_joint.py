@@ -10,8 +10,8 @@ without materialising them: the HIP kernels of `mrnnt_joint.hip` form each tile 
 (bf16 operands, fp32 accumulation) inside the log-softmax pass and again, for the live lattice rows only,
 inside the gradient pass. Backward returns gradients for enc, pred, weight and bias: the fused kernel writes
 the logit gradient G and the activations tanh(enc + pred) of the live rows (bf16); dweight = G^T Hact (split-K
-batched GEMM, fp32 out), dH = G weight and dbias = sum G are plain library GEMMs / reductions over those rows
-(hipBLASLt through torch), and mrnnt_joint_reduce folds dpre = dH (1 - Hact^2) into denc (sum over s) and dpred
+batched GEMM, fp32 out; Hact carries a ones column when dbias is needed, so dbias = sum G comes out of the same
+GEMM) and dH = G weight are plain library GEMMs over those rows (hipBLASLt through torch), and mrnnt_joint_reduce folds dpre = dH (1 - Hact^2) into denc (sum over s) and dpred
 (sum over t) in one pass.
 
 Shapes: enc [B, T_slots >= max T, H], pred [B, S_slots >= max S + 1, H], weight [V, H] (torch.nn.Linear
@@ -22,6 +22,7 @@ There is no CPU or eager fallback.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional
 
 import numpy as np
@@ -109,9 +110,10 @@ class _JointPrepared:
                                              1 if with_beta else 0, self.stream()), "mrnnt_joint_forward")
         return costs, ws
 
-    def backward_rows(self, ws, grad_scale, with_index=False):
+    def backward_rows(self, ws, grad_scale, with_index=False, bias_column=False):
         """The fused gradient pass over the live rows: (G [n, V], Hact [n, H]) and, with_index, the enc / pred
-        row of each live row (bt_idx, bs_idx)."""
+        row of each live row (bt_idx, bs_idx). bias_column: Hact is [n, _HACT_LD[H]] with column H = 1 (and zeros
+        after it), so G^T Hact carries dbias = sum_i G[i] in column H (no separate pass over G)."""
         lib = _L.load()
         with torch.cuda.device(self.device):
             cnt = torch.zeros(1, dtype=torch.int64, device=self.device)
@@ -119,7 +121,9 @@ class _JointPrepared:
                      "mrnnt_joint_live_rows")
             n = int(cnt.item())  # one 8-byte read-back sizes the row buffers
             G = torch.empty(max(1, n), self.V, dtype=torch.bfloat16, device=self.device)
-            Hact = torch.empty(max(1, n), self.H, dtype=torch.bfloat16, device=self.device)
+            ld = _HACT_LD[self.H] if bias_column else self.H
+            self.problem.hact_ld = ld  # mrnnt_joint_reduce reads Hact with the same stride
+            Hact = torch.empty(max(1, n), ld, dtype=torch.bfloat16, device=self.device)
             bt = bs = None
             if with_index:
                 bt = torch.empty(max(1, n), dtype=torch.int64, device=self.device)
@@ -141,6 +145,14 @@ class _JointPrepared:
                                                   _vp(Hact), _vp(d_enc), _vp(d_pred), self.stream()),
                      "mrnnt_joint_reduce")
         return d_enc if need_enc else None, d_pred if need_pred else None
+
+
+_BIAS_SUM = os.environ.get("MRNNT_JOINT_BIAS_SUM") == "1"
+# Hact row stride when it carries the dbias ones column: the widths at which hipBLASLt's split-K dW GEMM (n = 3.9 M
+# live rows, V = 1024) costs least over the plain H-wide one -- some widths pick much slower kernels
+# (profiles/r01/joint_bias_column_gemm.json). H = 512 keeps the separate G.sum: its cheapest wider GEMM (640) costs
+# +1.3 ms against 1.5 ms for G.sum, and the wider Hact store takes the rest (joint step +0.4 ms measured).
+_HACT_LD = {128: 192, 256: 288, 384: 392, 640: 656}
 
 
 def _split_k_weight_grad(G, Hact, chunks=32):
@@ -175,12 +187,19 @@ class MonotonicRNNTJointFunction(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_costs):
         prep, ws = ctx.prep, ctx.ws
-        G, Hact = prep.backward_rows(ws, grad_costs)
+        need_b = ctx.bias_dtype is not None and ctx.needs_input_grad[3]
+        # dbias rides on the dweight GEMM (a ones column in Hact); MRNNT_JOINT_BIAS_SUM=1: a separate G.sum (A/B)
+        bias_col = need_b and ctx.needs_input_grad[2] and not _BIAS_SUM and prep.H in _HACT_LD
+        G, Hact = prep.backward_rows(ws, grad_costs, bias_column=bias_col)
         ctx.prep = ctx.ws = None
         d_enc = d_pred = d_w = d_b = None
+        H = prep.H
         if ctx.needs_input_grad[2]:
-            d_w = _split_k_weight_grad(G, Hact).to(prep.weight.dtype)  # [V, H]
-        if ctx.bias_dtype is not None and ctx.needs_input_grad[3]:
+            dw = _split_k_weight_grad(G, Hact)  # [V, H] (+ dbias, zeros when Hact is wider)
+            d_w = dw[:, :H].to(prep.weight.dtype)
+            if bias_col:
+                d_b = dw[:, H].to(ctx.bias_dtype)
+        if need_b and not bias_col:
             d_b = G.sum(0, dtype=torch.float32).to(ctx.bias_dtype)
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
             dH = G @ prep.weight  # [n, H] bf16 (hipBLASLt)
