@@ -25,6 +25,11 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture(scope="module")
 def jop():
     import monotonic_rnnt_joint
+    import _mrnnt_lib as L
+    # sweeps through another launch variant: MRNNT_FUZZ_TUNE="joint_nbuf=3,joint_reduce_sparse=2"
+    for kv in filter(None, os.environ.get("MRNNT_FUZZ_TUNE", "").split(",")):
+        k, v = kv.split("=")
+        assert L.tune(k, int(v)) >= 0, k
     return monotonic_rnnt_joint
 
 
