@@ -1,31 +1,45 @@
 """bench.py -- MI355X monotonic RNN-T loss+grad throughput (BASELINE.json metric).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config headline|c2|ragged]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config headline|c2|ragged|ragged64|c5]
 
 One step = forward (log-softmax row reduce + alpha/beta DP) + backward (logit gradient, dL/dcost fused)
 over one batch through the autograd surface (monotonic_rnnt_loss(...).sum().backward()), plus, for N > 1,
 the single RCCL all-reduce of the summed loss. Inputs are synthetic and resident in HBM before timing.
-Scaling is weak: every rank owns its own B utterances (batch sharding, no data-path collective).
+
+--gpus N > 1 without a torch.distributed environment launches N ranks itself (torch.distributed.run, one
+process per GPU, 127.0.0.1 rendezvous) before this process touches the GPU, and exits with their status;
+rank 0 prints the JSON line. Under torchrun (WORLD_SIZE set) WORLD_SIZE must equal --gpus.
+
+Scaling: headline / c2 / c5 are weak (every rank owns its own B utterances); ragged (configs[3], B = 512
+global) is strong: the batch is sharded over the ranks by rows (contiguous prefix split).
+A rank whose shard does not fit acts + grads in HBM writes the gradient in place over the logits (the
+reference extension's output-buffer form, gpu_monotonic_rnnt(..., grads=acts)); a shard whose logits alone do
+not fit (configs[3] at N = 1: 292 GB) runs as chunks of utterances. In those two modes the logits are
+regenerated before each chunk outside the timed intervals, and the step time is the sum of the timed chunk
+intervals (each bracketed by barrier + synchronize).
 
 Rank 0 prints ONE JSON line with the contract fields plus:
-  roofline     : the gradient kernel (dominant), algorithmic bytes (N_live + N) * V * 4 per launch (N_live = in-band
-                 rows whose fp32 gradient is not exactly zero, the rows it reads) divided by its average duration
+  roofline     : the gradient kernel (dominant): algorithmic bytes (N_live + N) * V * elem of its launches (N_live =
+                 in-band rows whose fp32 gradient is not exactly zero, the rows it reads) divided by their duration
                  from HIP events recorded around each launch on its stream in the timed region; the SURVEY §8d
                  formula (N_v + N) * V * 4 is reported beside it as formula_bytes_per_launch / formula_gbps
   cpu_baseline : the reference's own CpuRNNTComputer<float> (oracle/_ref) -- or the oracle port when the reference
-                 build is absent -- timed on a bounded sample of the same workload on the host cores
+                 build is absent -- timed on a bounded sample of the same workload on the host's CPU share, as
+                 concurrent calls of at most the reference's 32-bit-offset utterance count each; the library's
+                 own host implementation (RNNT_CPU) on the same sample is reported beside it
   kernels      : per-kernel average ms and achieved GB/s
 """
 import argparse
 import ctypes
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
 import numpy as np
-import torch
-import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "monotonic-rnnt_amd", "pytorch_binding"))
@@ -34,56 +48,113 @@ METRIC = "utterances/sec + achieved HBM GB/s, (B,T,S,V)=(64,1000,200,1024)"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
 
 
+def ragged_lengths():
+    """configs[3]: B=512, T~U[200,1600], S~U[20,min(300,T)], seed 0."""
+    rng = np.random.default_rng(0)
+    Tg = rng.integers(200, 1601, 512).astype(np.int32)
+    Sg = np.array([rng.integers(20, min(300, t) + 1) for t in Tg], np.int32)
+    return Tg, Sg
+
+
 def lengths_for(config, rank, world):
-    """Per-rank utterance lengths (weak scaling: each rank owns its own B utterances)."""
+    """This rank's utterance lengths, V, workload name and scaling mode."""
     if config == "headline":  # BASELINE.json configs[2]
         B, T, S, V = 64, 1000, 200, 1024
-        return np.full(B, T, np.int32), np.full(B, S, np.int32), V, "B=64,T=1000,S=200,V=1024 (configs[2], headline)"
+        return np.full(B, T, np.int32), np.full(B, S, np.int32), V, "B=64,T=1000,S=200,V=1024 (configs[2], headline)", "weak"
     if config == "c2":  # configs[1]
         B, T, S, V = 16, 200, 40, 256
-        return np.full(B, T, np.int32), np.full(B, S, np.int32), V, "B=16,T=200,S=40,V=256 (configs[1])"
-    if config == "c5":  # configs[4]: V = 10000; 64 utterances = 514.6 GB of acts > 288 GB, so the batch runs as
-        # four 16-utterance chunks (128.6 GB acts + 128.6 GB grads each); one chunk is the measured unit
-        B, T, S, V = 16, 1000, 200, 10000
+        return np.full(B, T, np.int32), np.full(B, S, np.int32), V, "B=16,T=200,S=40,V=256 (configs[1])", "weak"
+    if config == "c5":  # configs[4]: V = 10000, 64 utterances = 514.6 GB of acts: run as chunks
+        B, T, S, V = 64, 1000, 200, 10000
         return (np.full(B, T, np.int32), np.full(B, S, np.int32), V,
-                "B=16 chunk of B=64,T=1000,S=200,V=10000 (configs[4], large vocab; batch = 4 chunks)")
-    if config == "ragged64":  # the first 64 utterances of configs[3] (fits one GPU with separate grads)
-        rng = np.random.default_rng(0)
-        Tg = rng.integers(200, 1601, 512).astype(np.int32)
-        Sg = np.array([rng.integers(20, min(300, t) + 1) for t in Tg], np.int32)
-        return Tg[:64], Sg[:64], 1024, "first 64 utterances of configs[3] (ragged T, S), V=1024"
-    if config == "ragged":  # configs[3]: B=512 global, T~U[200,1600], S~U[20,min(300,T)], sharded over ranks
-        rng = np.random.default_rng(0)
-        Tg = rng.integers(200, 1601, 512).astype(np.int32)
-        Sg = np.array([rng.integers(20, min(300, t) + 1) for t in Tg], np.int32)
+                "B=64,T=1000,S=200,V=10000 (configs[4], large vocab; chunked, in-place grads)", "weak")
+    if config == "ragged64":  # the first 64 utterances of configs[3]
+        Tg, Sg = ragged_lengths()
+        return Tg[:64], Sg[:64], 1024, "first 64 utterances of configs[3] (ragged T, S), V=1024", "weak"
+    if config == "ragged":  # configs[3], sharded over ranks
+        Tg, Sg = ragged_lengths()
         from distributed import shard_bounds
         lo, hi = shard_bounds(Tg.astype(np.int64) * (Sg + 1), world)[rank]
-        return Tg[lo:hi], Sg[lo:hi], 1024, f"B=512 ragged (T~U[200,1600], S~U[20,min(300,T)]), V=1024, rank slice [{lo},{hi})"
+        return (Tg[lo:hi], Sg[lo:hi], 1024,
+                f"B=512 ragged (T~U[200,1600], S~U[20,min(300,T)]), V=1024, sharded over {world}", "strong")
     raise SystemExit(f"unknown config {config}")
 
 
-def main():
+def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="headline", choices=["headline", "c2", "ragged", "ragged64", "c5"])
-    ap.add_argument("--cpu-sample", type=int, default=20, help="utterances in the CPU-baseline sample (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=16,
-                    help="OpenMP threads of the CPU baseline (the GPU box's CPU share per GPU is 16)")
+    ap.add_argument("--cpu-sample", type=int, default=16, help="utterances in the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="host threads for the CPU baseline (0 = this process's CPU share: affinity / cgroup quota)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--acts-dtype", default="f32", choices=["f32", "bf16", "f16"],
                     help="element type of acts/grads (extension; the headline metric is f32, the reference's type)")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
-                    help="launch knob for experiments (mrnnt_tune); the defaults are the tuned values")
+                    help="launch knob (runs the development build libmonotonic_rnnt_amd_dev.so; experiments only)")
     ap.add_argument("--align-k", type=int, default=None,
                     help="alignment-restricted loss (restrict_to_alignment, max_distance_from_alignment = K) on a "
                          "synthetic alignment with the labels evenly spaced over the frames")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI, the real path) or gloo (rehearsal: several ranks may share one GPU)")
-    args = ap.parse_args()
+    ap.add_argument("--hbm-budget-gb", type=float, default=0.0,
+                    help="cap the bytes a rank may allocate for acts (+ grads) (0 = free HBM minus a reserve)")
+    ap.add_argument("--cpu-worker", default=None, help=argparse.SUPPRESS)
+    return ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+
+# ---------------------------------------------------------------------------------------------------------
+# N-rank launch (before any GPU call in this process)
+
+def launch_ranks(args) -> int:
+    import torch
+    n = args.gpus
+    if args.dist_backend == "nccl" and torch.cuda.device_count() < n:  # device_count does not initialise HIP
+        print(f"bench.py: --gpus {n} needs {n} GPUs, {torch.cuda.device_count()} visible "
+              "(use --dist-backend gloo to rehearse several ranks on one GPU)", file=sys.stderr)
+        return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd, env=env).returncode
+
+
+# ---------------------------------------------------------------------------------------------------------
+
+def main():
+    args = parse()
+    if args.cpu_worker:
+        return cpu_worker(json.loads(args.cpu_worker))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    world = int(env_world or 1)
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
+    import _mrnnt_lib as L
+    if args.tune:
+        with L.use(L.load_dev()):
+            for kv in args.tune:
+                k, v = kv.split("=")
+                if L.tune(k, int(v)) < 0:
+                    raise SystemExit(f"unknown knob {k}")
+            run(args, world)
+    else:
+        run(args, world)
+
+
+def run(args, world):
+    import torch
+    import torch.distributed as dist
+    import monotonic_rnnt_op as op
+    import _mrnnt_lib as L
+
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dev_index = local_rank % max(1, torch.cuda.device_count())
@@ -96,123 +167,185 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=dev)
 
-    def coll_tensor(x):  # gloo collectives run on host tensors
+    def coll(x):  # gloo collectives run on host tensors
         return x.cpu() if gloo else x
 
-    import monotonic_rnnt_op as op
-    import _mrnnt_lib as L
+    def barrier():
+        if world > 1:
+            dist.barrier()
 
-    lib = L.load()
-    for kv in args.tune:
-        k, v = kv.split("=")
-        if L.tune(k, int(v)) < 0:
-            raise SystemExit(f"unknown knob {k}")
-    T, S, V, workload = lengths_for(args.config, rank, world)
+    T, S, V, workload, scaling = lengths_for(args.config, rank, world)
     B = len(T)
-    rows = int(np.sum(T.astype(np.int64) * (S + 1)))
+    elem = {"f32": 4, "bf16": 2, "f16": 2}[args.acts_dtype]
+    rows_u = T.astype(np.int64) * (S + 1)
+    rows = int(rows_u.sum())
     n_band = int(np.sum((S.astype(np.int64) + 1) * (T - S + 1) - 1))  # in-band rows N_v
     # global row offset of this rank's first utterance, so every rank streams different synthetic data
     all_rows = [rows]
     if world > 1:
-        t = coll_tensor(torch.tensor([rows], dtype=torch.int64, device=dev))
+        t = coll(torch.tensor([rows], dtype=torch.int64, device=dev))
         g = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(g, t)
         all_rows = [int(x.item()) for x in g]
     row0 = sum(all_rows[:rank])
 
-    stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-    acts = torch.empty((rows, V), dtype=torch.float32, device=dev)
-    L.check(lib.mrnnt_synth_acts(ctypes.c_void_p(acts.data_ptr()), row0 * V, rows * V, 0, 1, stream), "synth")
-    elem = {"f32": 4, "bf16": 2, "f16": 2}[args.acts_dtype]
-    if args.acts_dtype != "f32":
-        acts = acts.to(torch.bfloat16 if args.acts_dtype == "bf16" else torch.float16)
-        torch.cuda.empty_cache()
+    # memory plan: acts + grads resident (autograd path), else grads in place, else chunks of utterances
+    free, _ = torch.cuda.mem_get_info(dev)
+    budget = args.hbm_budget_gb * 1e9 if args.hbm_budget_gb > 0 else free - 6e9
+    ws_per_row = 48  # workspace bytes per lattice row (den fp32 + lpb/lpe/alpha/beta fp64, rounded up)
+    need = rows * V * elem
+    if 2 * need + rows * ws_per_row <= budget:
+        mode, chunks = "resident", [(0, B)]
+    else:
+        mode = "inplace"
+        chunks, lo, acc = [], 0, 0
+        for b in range(B):
+            nb = int(rows_u[b]) * (V * elem + ws_per_row)
+            if acc and acc + nb > budget:
+                chunks.append((lo, b))
+                lo, acc = b, 0
+            acc += nb
+        chunks.append((lo, B))
+        if args.acts_dtype != "f32":
+            raise SystemExit("the in-place / chunked modes regenerate fp32 logits; use --acts-dtype f32")
+    crow = np.concatenate([[0], np.cumsum(rows_u)])
+    max_chunk_rows = max(int(crow[hi] - crow[lo]) for lo, hi in chunks)
+
+    stream_h = torch.cuda.current_stream(dev).cuda_stream
+    acts_buf = torch.empty((max_chunk_rows, V), dtype=torch.float32, device=dev)
     rng = np.random.default_rng(1 + rank)
-    labels = torch.from_numpy(rng.integers(1, V, (B, max(1, int(S.max())))).astype(np.int32)).to(dev)
-    T_t = torch.from_numpy(T)
-    S_t = torch.from_numpy(S)
-    align, n_window = None, None
+    labels_all = rng.integers(1, V, (B, max(1, int(S.max())))).astype(np.int32)
+    labels_dev = torch.from_numpy(labels_all).to(dev)
+
+    def synth(lo, hi):
+        n = int(crow[hi] - crow[lo])
+        L.synth_acts(acts_buf.data_ptr(), (row0 + int(crow[lo])) * V, n * V, 0, True, stream_h)
+        return acts_buf[:n]
+
+    align = n_window = None
     if args.align_k is not None:
-        al_np, n_window = synthetic_alignment(labels.cpu().numpy(), T, S, args.align_k)
+        if mode != "resident":
+            raise SystemExit("--align-k needs a resident config")
+        al_np, n_window = synthetic_alignment(labels_all, T, S, args.align_k)
         align = torch.from_numpy(al_np).to(dev)
         workload += f", alignment-restricted (k={args.align_k}, labels evenly spaced)"
-    acts.requires_grad_(True)
-    torch.cuda.synchronize()
 
-    def step():
-        acts.grad = None
-        costs = op.monotonic_rnnt_loss(acts, labels, T_t, S_t, align, args.align_k or 0, blank_label=0)
-        loss = costs.sum()
-        loss.backward()
-        if world > 1:
-            tot = coll_tensor(loss.detach().clone())
-            dist.all_reduce(tot)  # the one RCCL exchange of the path: 4 bytes over xGMI
-        return loss
+    T_t, S_t = torch.from_numpy(T), torch.from_numpy(S)
+    if mode == "resident":
+        acts = synth(0, B)
+        if args.acts_dtype != "f32":
+            acts = acts.to(torch.bfloat16 if args.acts_dtype == "bf16" else torch.float16)
+            del acts_buf
+            torch.cuda.empty_cache()
+        acts.requires_grad_(True)
+        torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    L.profile_enable(True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loss = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+        def step():
+            acts.grad = None
+            costs = op.monotonic_rnnt_loss(acts, labels_dev, T_t, S_t, align, args.align_k or 0, blank_label=0)
+            loss = costs.sum()
+            loss.backward()
+            if world > 1:
+                tot = coll(loss.detach().clone())
+                dist.all_reduce(tot)  # the one RCCL exchange of the path: 4 bytes over xGMI
+            return loss
+
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        barrier()
+        L.profile_enable(True)
+        torch.cuda.synchronize()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            loss = step()
+        torch.cuda.synchronize()
+        barrier()
+        elapsed = time.perf_counter() - t0
+        loss_val = float(loss.item())
+    else:
+        costs_c = torch.zeros(B, dtype=torch.float32, device=dev)
+        T_d, S_d = T_t.to(dev), S_t.to(dev)
+
+        def chunk_step(lo, hi):
+            """Regenerate the chunk's logits (not timed), then one timed forward + in-place backward."""
+            a = synth(lo, hi)
+            torch.cuda.synchronize()
+            barrier()
+            t0 = time.perf_counter()
+            op.monotonic_rnnt_cpp.gpu_monotonic_rnnt(a, labels_dev[lo:hi], T_d[lo:hi], S_d[lo:hi], costs_c[lo:hi],
+                                                     a, 0)
+            if world > 1 and hi == B:
+                tot = coll(costs_c.sum().reshape(1))
+                dist.all_reduce(tot)  # the loss all-reduce, once per step
+            torch.cuda.synchronize()
+            barrier()
+            return time.perf_counter() - t0
+
+        for _ in range(args.warmup):
+            for lo, hi in chunks:
+                chunk_step(lo, hi)
+        L.profile_enable(True)
+        elapsed = 0.0
+        for _ in range(args.steps):
+            for lo, hi in chunks:
+                elapsed += chunk_step(lo, hi)
+        loss_val = float(costs_c.sum().item())
+        acts = None
     prof = L.profile_read()
     L.profile_enable(False)
-    el = coll_tensor(torch.tensor([elapsed], dtype=torch.float64, device=dev))
+    el = coll(torch.tensor([elapsed], dtype=torch.float64, device=dev))
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
-    total_utts = coll_tensor(torch.tensor([B], dtype=torch.int64, device=dev))
+    total_utts = coll(torch.tensor([B], dtype=torch.int64, device=dev))
     if world > 1:
         dist.all_reduce(total_utts)
     total_utts = int(total_utts.item())
 
     # live rows: in-band rows whose gradient is not exactly zero in fp32 -- the only acts rows the gradient
     # kernel reads (occupancy skip, DESIGN.md §4); counted once after the timed region
-    live = live_rows(op, L, acts, labels, T_t, S_t, dev, align, args.align_k or 0)
+    live = 0
+    for lo, hi in chunks:
+        a = acts.detach() if mode == "resident" else synth(lo, hi)
+        live += live_rows(op, L, a, labels_dev[lo:hi], T_t[lo:hi], S_t[lo:hi], dev, align, args.align_k or 0)
     grad_bytes = (live + rows) * V * elem  # algorithmic: read live acts rows once, write every grads row once
     formula_grad_bytes = (n_band + rows) * V * elem  # SURVEY.md §8d formula: every in-band row read
     n_read = n_band if n_window is None else n_window  # rows the log-softmax pass reads
     softmax_bytes = n_read * V * elem
     step_bytes = (n_read + live + rows) * V * elem
+    n_chunks = len(chunks)
 
-    def avg_ms(name):
+    def tot_ms(name):
         ms, n = prof[name]
-        return ms / n if n else None
+        return (ms, n) if n else (None, 0)
 
-    g_ms = avg_ms("grad")
-    s_ms = avg_ms("log_softmax")
-    d_ms = avg_ms("alpha_beta")
-    achieved = grad_bytes / (g_ms * 1e-3) / 1e9 if g_ms else None
+    g_ms, g_n = tot_ms("grad")
+    s_ms, s_n = tot_ms("log_softmax")
+    d_ms, d_n = tot_ms("alpha_beta")
+    # the bytes of all gradient launches of the timed steps over their summed duration
+    achieved = grad_bytes * args.steps / (g_ms * 1e-3) / 1e9 if g_ms else None
+    g_avg = g_ms / g_n if g_ms else None
 
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_grad_traffic.json")
-    if os.path.exists(pmc_path):
+    if os.path.exists(pmc_path) and mode == "resident" and not args.tune:
         try:
             pm = json.load(open(pmc_path))
-            # only a measurement of this config and of the kernel this run launches counts
-            gv = L.tune("grad_variant")
-            fam = {3: "grad_rows_kernel", 5: "grad_staged_kernel", 6: "grad_staged_kernel"}.get(gv, "grad_kernel")
-            elem = {"f32": "IoF32", "bf16": "IoBF16", "f16": "IoF16"}[args.acts_dtype]
-            if pm.get("config") == args.config and pm.get("kernel", "").startswith(f"{fam}<{elem}"):
+            ek = {"f32": "IoF32", "bf16": "IoBF16", "f16": "IoF16"}[args.acts_dtype]
+            if pm.get("config") == args.config and pm.get("kernel", "").startswith(f"grad_staged_kernel<{ek}"):
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
 
-    copy_gbps = same_buffers_copy_gbps(lib, L, dev, acts.detach(), acts.grad)
+    copy_gbps = None
+    if mode == "resident" and acts.grad is not None:
+        copy_gbps = same_buffers_copy_gbps(L, dev, acts.detach(), acts.grad)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_sample > 0 and args.acts_dtype == "f32":
-        cpu = cpu_baseline(lib, L, acts, labels, T, S, V, args.cpu_sample, stream, args.cpu_threads)
+        cpu = cpu_baseline(op, T, S, V, labels_all, row0, args.cpu_sample, args.cpu_threads)
 
     if rank == 0:
         out = {
@@ -224,56 +357,60 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": args.acts_dtype,
             "data": "synthetic: counter-hash N(0,1)-like acts (seed 0), labels U[1,V-1] (seed 1+rank); inputs resident in HBM",
             "config": {"workload": workload, "utterances_per_gpu": B, "global_batch": total_utts,
                        "rows_per_gpu": rows, "inband_rows_per_gpu": n_band, "V": V,
+                       "memory_mode": mode, "chunks_per_step": n_chunks,
                        **({"window_rows_per_gpu": n_window} if n_window is not None else {}),
                        "parallelism": f"dp{world} (batch-sharded, one 4-byte "
                                       f"{'gloo (rehearsal)' if gloo else 'RCCL'} loss all-reduce)"},
-            "achieved_hbm_gbps_step": round(step_bytes * total_utts / B * args.steps / elapsed / 1e9, 1),
-            "roofline": {"kernel": "logit gradient (grad_variant %d)" % L.tune("grad_variant"), "bound": "hbm",
+            "achieved_hbm_gbps_step": round(step_bytes * args.steps / elapsed / 1e9, 1),
+            "roofline": {"kernel": "logit gradient", "bound": "hbm",
                          "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4) if achieved else None,
-                         "traffic": traffic, "algorithmic_bytes_per_launch": grad_bytes,
-                         "avg_launch_ms": round(g_ms, 4) if g_ms else None,
+                         "traffic": traffic, "algorithmic_bytes_per_launch": grad_bytes // n_chunks,
+                         "avg_launch_ms": round(g_avg, 4) if g_avg else None,
                          "live_rows": live, "inband_rows": n_band,
-                         "formula_bytes_per_launch": formula_grad_bytes,
-                         "formula_gbps": round(formula_grad_bytes / (g_ms * 1e-3) / 1e9, 1) if g_ms else None,
+                         "formula_bytes_per_launch": formula_grad_bytes // n_chunks,
+                         "formula_gbps": round(formula_grad_bytes * args.steps / (g_ms * 1e-3) / 1e9, 1) if g_ms else None,
                          "copy_gbps_same_buffers": copy_gbps,
                          "frac_of_copy_same_buffers": round(achieved / copy_gbps, 4) if achieved and copy_gbps else None},
             "kernels": {
-                "log_softmax": {"avg_ms": round(s_ms, 4) if s_ms else None,
-                                "gbps": round(softmax_bytes / (s_ms * 1e-3) / 1e9, 1) if s_ms else None},
-                "alpha_beta": {"avg_ms": round(d_ms, 4) if d_ms else None},
-                "grad": {"avg_ms": round(g_ms, 4) if g_ms else None, "gbps": round(achieved, 1) if achieved else None},
+                "log_softmax": {"avg_ms": round(s_ms / s_n, 4) if s_ms else None,
+                                "gbps": round(softmax_bytes * args.steps / (s_ms * 1e-3) / 1e9, 1) if s_ms else None},
+                "alpha_beta": {"avg_ms": round(d_ms / d_n, 4) if d_ms else None},
+                "grad": {"avg_ms": round(g_avg, 4) if g_avg else None, "gbps": round(achieved, 1) if achieved else None},
             },
             "cpu_baseline": cpu,
             "tune": args.tune or None,
-            "alloc": {"acts": acts.data_ptr(), "grads": acts.grad.data_ptr()},
-            "loss_check": float(loss.item()),
+            "loss_check": loss_val,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def same_buffers_copy_gbps(lib, L, dev, src_t, dst_t, gib=8, reps=5):
+def same_buffers_copy_gbps(L, dev, src_t, dst_t, gib=8, reps=5):
     """Device-copy rate on THIS run's own buffers (mrnnt_copy_probe: the gradient pass's access pattern,
     nontemporal, read + write bytes / time, HIP events on the stream it runs on), acts -> grads, after the timed
-    region. HBM streaming rates depend on where a buffer sits physically: two 52 GB buffers of one process can
-    differ by ~20 % for writes and ~10 % for reads (profiles/r01/grad_placement_study.json), so the gradient
-    kernel is compared with a plain copy between the same two buffers. None if the buffers are too small."""
+    region. HBM streaming rates depend on where a buffer sits physically (profiles/r01/grad_placement_study.json),
+    so the gradient kernel is compared with a plain copy between the same two buffers. None if too small."""
+    import torch
     n = min(gib << 30, src_t.numel() * src_t.element_size(), dst_t.numel() * dst_t.element_size())
     n -= n % 16
     if n < (1 << 30):
         return None
     stream = torch.cuda.current_stream(dev)
     sp = ctypes.c_void_p(stream.cuda_stream)
-    run = lambda: L.check(lib.mrnnt_copy_probe(ctypes.c_void_p(dst_t.data_ptr()), ctypes.c_void_p(src_t.data_ptr()),  # noqa: E731
-                                               n, sp), "copy_probe")
+    tools = L.devtools()
+
+    def run():
+        if tools.mrnnt_copy_probe(ctypes.c_void_p(dst_t.data_ptr()), ctypes.c_void_p(src_t.data_ptr()), n, sp):
+            raise RuntimeError("copy probe failed")
+
     run()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
@@ -288,7 +425,7 @@ def same_buffers_copy_gbps(lib, L, dev, src_t, dst_t, gib=8, reps=5):
 def synthetic_alignment(labels, T, S, k):
     """[B, T_max] alignment with label i of utterance b at frame floor((i + 0.5) T_b / S_b) (blank = 0 elsewhere),
     and the number of lattice rows the log-softmax pass reads under it (the alignment window of each column:
-    mrnnt_softmax.hip align_window, from the band of gpu_workspace_manager.h:191-219)."""
+    mrnnt_device.h align_window, from the band of gpu_workspace_manager.h:191-219)."""
     B = len(T)
     al = np.zeros((B, int(T.max())), np.int32)
     n_window = 0
@@ -310,7 +447,8 @@ def synthetic_alignment(labels, T, S, k):
 
 def live_rows(op, L, acts, labels, T, S, dev, align=None, k=0):
     """In-band rows the gradient kernel reads on this workload (mrnnt_grad_live_rows after one forward)."""
-    prep = op._Prepared(acts.detach(), labels, T, S, align, k, 0)
+    import torch
+    prep = op._Prepared(acts, labels, T, S, align, k, 0)
     _, ws = op._forward(prep, with_beta=True)
     cnt = torch.zeros(1, dtype=torch.int64, device=dev)
     L.check(L.load().mrnnt_grad_live_rows(ctypes.byref(prep.problem), ctypes.c_void_p(ws.data_ptr()),
@@ -318,40 +456,111 @@ def live_rows(op, L, acts, labels, T, S, dev, align=None, k=0):
     return int(cnt.item())
 
 
-def cpu_baseline(lib, L, acts, labels, T, S, V, n_sample, stream, max_threads=16):
-    """Time the reference CPU path on the first n_sample utterances of the same synthetic workload."""
+# ---------------------------------------------------------------------------------------------------------
+# CPU baseline
+
+def host_cpu_share():
+    """CPUs this process may use: the affinity mask, capped by a cgroup v2 cpu.max quota when there is one
+    (the GPU box shows the whole machine's CPUs in nproc / os.cpu_count but grants a share per GPU)."""
+    nproc = os.cpu_count() or 1
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else nproc
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except Exception:
+        quota = None
+    env = os.environ.get("OMP_NUM_THREADS")
+    share = min(aff, quota) if quota else aff
+    return {"nproc": nproc, "affinity": aff, "cgroup_quota": quota,
+            "omp_num_threads_env": int(env) if env and env.isdigit() else None, "share": share}
+
+
+def cpu_worker(job):
+    """One reference call in its own process (bench.py --cpu-worker JSON): regenerate the sample's logits on the
+    host with the GPU run's generator, then time the reference's cost_and_grad (or the oracle port)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    T = np.asarray(job["T"], np.int32)
+    S = np.asarray(job["S"], np.int32)
+    V = int(job["V"])
+    labels = np.asarray(job["labels"], np.int32)
+    rows = int(np.sum(T.astype(np.int64) * (S + 1)))
+    acts = O.synth_acts(int(job["begin"]), rows * V, seed=0).reshape(rows, V)
+    fn = O.ref_rnnt if job["kind"] == "reference" else O.oracle_rnnt
+    t0 = time.perf_counter()
+    costs, _ = fn(acts, labels, T, S, precision="f32", num_threads=int(job["threads"]))
+    dt = time.perf_counter() - t0
+    print(json.dumps({"seconds": dt, "utterances": len(T), "finite": bool(np.all(np.isfinite(costs)))}), flush=True)
+    return 0
+
+
+def cpu_baseline(op, T, S, V, labels, row0, n_sample, threads_arg=0):
+    """Time the reference CPU path on the first n_sample utterances of the same synthetic workload, using the
+    host's CPU share. The reference indexes acts with 32-bit offsets (cpu_workspace_manager.h:48,125-135) and
+    parallelises over utterances only (cpu_rnnt.h:54-57), so one call takes at most 2^31 / (rows per utterance
+    * V) utterances (10 at the headline) with one busy thread each: the sample runs as concurrent calls in
+    separate processes, together using every core of the share."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     try:
         import oracle as O
     except Exception as e:  # pragma: no cover
         return {"error": f"oracle unavailable: {e}"}
-    n = min(n_sample, len(T))
+    host = host_cpu_share()
+    cores = threads_arg if threads_arg > 0 else host["share"]
     kind = "reference" if O.ref_available() else "port"
-    fn = O.ref_rnnt if kind == "reference" else O.oracle_rnnt
-    # the reference indexes acts with 32-bit offsets (cpu_workspace_manager.h:48): one call takes at most
-    # 2^31 / (rows per utterance * V) utterances (10 at the headline); the sample is that call (<= max_threads
-    # utterances, OpenMP over utterances) repeated until n_sample utterances have been processed
+    n = min(n_sample, len(T))
     rows_u = T[:n].astype(np.int64) * (S[:n] + 1)
-    g = 1
-    while g < min(n, max_threads) and int(rows_u[:g + 1].sum()) * V < 2 ** 31:
-        g += 1
-    reps = (n + g - 1) // g
-    rows = int(rows_u[:g].sum())
-    host = acts.detach()[:rows].float().cpu().numpy()
-    lab = labels[:g].cpu().numpy()
-    threads = max(1, min(g, os.cpu_count() or 1))
-    finite = True
+    per_call_cap = max(1, int((2 ** 31 - 1) // (int(rows_u.max()) * V)))  # int32 offsets of one call
+    calls = min(n, max(math.ceil(n / per_call_cap), math.ceil(cores / per_call_cap)))
+    bounds = np.linspace(0, n, calls + 1).astype(int)
+    threads = [max(1, min(int(bounds[c + 1] - bounds[c]), cores // calls)) for c in range(calls)]
+    crow = np.concatenate([[0], np.cumsum(rows_u)])
+    procs = []
+    for c in range(calls):
+        lo, hi = int(bounds[c]), int(bounds[c + 1])
+        job = {"T": T[lo:hi].tolist(), "S": S[lo:hi].tolist(), "V": V,
+               "labels": labels[lo:hi, :max(1, int(S[lo:hi].max()))].tolist(),
+               "begin": int((row0 + crow[lo]) * V), "kind": kind, "threads": threads[c]}
+        env = dict(os.environ, OMP_NUM_THREADS=str(threads[c]))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-worker", json.dumps(job)],
+                                      stdout=subprocess.PIPE, env=env, text=True))
+    res = []
+    for p in procs:
+        out, _ = p.communicate()
+        if p.returncode != 0:
+            return {"error": f"cpu worker exited with {p.returncode}"}
+        res.append(json.loads(out.strip().splitlines()[-1]))
+    wall = max(r["seconds"] for r in res)
+    done = sum(r["utterances"] for r in res)
+    out = {"value": round(done / wall, 4), "unit": "utt/s", "cores": sum(threads), "kind": kind, "host": host,
+           "concurrent_calls": calls, "threads_per_call": threads,
+           "sample": f"{done} utterances of the same workload (first T={int(T[0])}, S={int(S[0])}, V={V}): "
+                     f"{calls} concurrent reference calls in separate processes (<= {per_call_cap} utterances per "
+                     f"call: 32-bit offsets), cost_and_grad at fp32, OpenMP over utterances, slowest call "
+                     f"{wall:.2f} s",
+           "finite": all(r["finite"] for r in res)}
+    out["product_cpu"] = product_cpu_rate(op, T[:n], S[:n], V, labels[:n], row0, cores)
+    return out
+
+
+def product_cpu_rate(op, T, S, V, labels, row0, threads):
+    """The library's own host implementation (RNNT_CPU, cpu_monotonic_rnnt) on the same sample: one call,
+    OpenMP over lattice columns on every core of the share. Reported next to the reference baseline."""
+    import torch
+    import oracle as O
+    rows = int(np.sum(T.astype(np.int64) * (S + 1)))
+    acts = torch.from_numpy(O.synth_acts(row0 * V, rows * V, seed=0).reshape(rows, V))
+    grads = torch.empty_like(acts)
+    costs = torch.zeros(len(T))
+    lab = torch.from_numpy(np.ascontiguousarray(labels[:, :max(1, int(S.max()))]))
+    args = (acts, lab, torch.from_numpy(T), torch.from_numpy(S), costs, grads, 0, threads)
     t0 = time.perf_counter()
-    for _ in range(reps):
-        costs, _ = fn(host, lab, T[:g], S[:g], precision="f32", num_threads=threads)
-        finite = finite and bool(np.all(np.isfinite(costs)))
+    op.monotonic_rnnt_cpp.cpu_monotonic_rnnt(*args)
     dt = time.perf_counter() - t0
-    n = g * reps
-    return {"value": round(n / dt, 4), "unit": "utt/s", "cores": threads, "kind": kind,
-            "sample": f"{n} utterances of the same workload (T={int(T[0])}, S={int(S[0])}, V={V}): "
-                      f"{reps} call(s) of {g}, cost_and_grad at fp32, OpenMP over utterances "
-                      f"({threads} threads), {dt:.2f} s",
-            "finite": finite}
+    return {"value": round(len(T) / dt, 4), "unit": "utt/s", "threads": threads, "seconds": round(dt, 3),
+            "finite": bool(torch.isfinite(costs).all())}
 
 
 if __name__ == "__main__":

@@ -86,6 +86,14 @@ RNNTStatus mrnnt_cost_and_grad(const mrnnt_problem *p, void *workspace, size_t w
 RNNTStatus mrnnt_read_loglik(const mrnnt_problem *p, const void *workspace, double *ll_fwd_dev, double *ll_bwd_dev,
                              hipStream_t stream);
 
+/* Per-row state of the last mrnnt_forward on this workspace, for inspection / parity tests: den[r] (fp32
+ * log-softmax denominator -max - log sum exp(z - max) of the rows the forward reduced: the in-band or
+ * alignment-window rows, 0 elsewhere), alpha[r] = alpha(t, s) and beta[r] = beta(t, s) (fp64, -inf outside the
+ * band; beta only after with_beta = 1), all in the packed lattice row order r = sum_{b'<b} T_b'(S_b'+1) +
+ * t (S_b+1) + s. Device buffers of N elements; any may be NULL. Asynchronous on `stream`. */
+RNNTStatus mrnnt_read_state(const mrnnt_problem *p, const void *workspace, float *den_dev, double *alpha_dev,
+                            double *beta_dev, hipStream_t stream);
+
 /* Message describing the last non-success status returned on this thread. */
 const char *mrnnt_last_error(void);
 
@@ -95,6 +103,26 @@ const char *mrnnt_last_error(void);
  * stored without reading acts ("occ_skip" knob, on by default). Inspection/bench only; asynchronous. */
 RNNTStatus mrnnt_grad_live_rows(const mrnnt_problem *p, const void *workspace, unsigned long long *count_dev,
                                 hipStream_t stream);
+
+/* ---- host implementation (RNNT_CPU; reference cpu_rnnt.h / pytorch_binding cpu_monotonic_rnnt) --------
+ * The same problem description with every pointer on the HOST: acts (fp32 only), labels, alignment,
+ * T_host / S_host (T_dev / S_dev are ignored), workspace, costs, grads, grad_scale. Lengths, strides and
+ * labels are validated (a label outside [0, V) is RNNT_STATUS_INVALID_VALUE). num_threads <= 0 uses the
+ * OpenMP default. Results follow the GPU path's semantics (fp64 recursion, occupancy-exact zero rows). */
+RNNTStatus mrnnt_cpu_workspace_size(const mrnnt_problem *p, size_t *bytes);
+
+/* Log-softmax row reduce + alpha (and, if with_beta, beta) recursion; costs[b] = -log p (may be NULL). */
+RNNTStatus mrnnt_cpu_forward(const mrnnt_problem *p, void *workspace, size_t workspace_bytes, float *costs,
+                             int with_beta, int num_threads);
+
+/* grads[r, v] = grad_scale[b(r)] * dcost_b / dacts[r, v] for every row (grad_scale may be NULL = 1), after
+ * mrnnt_cpu_forward(with_beta=1) on the same workspace and inputs. grads may be acts itself (in place). */
+RNNTStatus mrnnt_cpu_backward(const mrnnt_problem *p, const void *workspace, const float *grad_scale, float *grads,
+                              int num_threads);
+
+/* mrnnt_read_state for the host implementation (host buffers). */
+RNNTStatus mrnnt_cpu_read_state(const mrnnt_problem *p, const void *workspace, float *den, double *alpha,
+                                double *beta);
 
 /* ---- fused joint network + loss (extension) -------------------------------------
  * The logits are not an input: z(b,t,s,:) = weight * tanh(enc[b,t,:] + pred[b,s,:]) + bias is formed on the
@@ -162,28 +190,6 @@ int mrnnt_version(void);
  *   [5] joint forward, [6] joint backward, [7] joint reduce. */
 void mrnnt_profile_enable(int enable);
 int mrnnt_profile_read(double *total_ms, int64_t *launches, int n);
-
-/* Launch-shape knobs for experiments (defaults are the tuned values): "softmax_variant" (rows per wave
- * of the log-softmax kernel: 0 one, 2 two), "grad_variant" (0 one row per wave, 2 two rows, 3 row-stride
- * sweep for the packed layout), "softmax_grid_per_cu" / "grad_grid_per_cu" (persistent workgroups per
- * CU, 0 = one workgroup per lattice column; "grid_per_cu" sets both), "nt_store" / "nt_load" (0/1:
- * nontemporal grads stores / acts loads), "occ_skip" (0/1: skip the acts read of rows
- * whose gradient is exactly zero, see mrnnt_grad_live_rows), "joint_nbuf" (2/3 LDS weight buffers of
- * the fused joint kernels).
- * Sets `key` to `value` (value < 0: query only) and returns the previous value, or -1 for an unknown key.
- * Process-global; not thread-safe against concurrent launches. */
-int mrnnt_tune(const char *key, int value);
-
-/* Bench helper: fill out[0..count) with the counter-based synthetic generator (bit-identical to the
- * host twin in oracle/rnnt_oracle.c): element i gets hash(seed, begin + i) as N(0,1)-like
- * (normal=1) or U[0,1) (normal=0). */
-RNNTStatus mrnnt_synth_acts(float *out, int64_t begin, int64_t count, uint64_t seed, int normal, hipStream_t stream);
-
-/* Bench helper (not part of the reference interface): copy `bytes` (a multiple of 16, 16-byte aligned
- * pointers) from src to dst on the device in the gradient pass's access pattern (contiguous slabs per
- * workgroup, nontemporal loads and stores), so a bench can report this card's own copy rate next to the
- * kernels' rates. */
-RNNTStatus mrnnt_copy_probe(void *dst, const void *src, size_t bytes, hipStream_t stream);
 
 #ifdef __cplusplus
 }

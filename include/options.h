@@ -9,7 +9,7 @@ typedef struct ihipStream_t *hipStream_t;
 typedef enum { RNNT_CPU = 0, RNNT_GPU = 1 } rnntComputeLocation;
 
 struct RNNTOptions {
-    /* The maximum number of threads that can be used (CPU only in the reference; ignored here) */
+    /* The maximum number of threads that can be used (RNNT_CPU only; <= 0 = the OpenMP default) */
     int num_threads;
 
     /* HIP stream the kernels are launched on (0 = legacy default stream) */
@@ -18,9 +18,8 @@ struct RNNTOptions {
     /* the label value/index that the RNNT calculation should use as the blank label */
     int blank_label;
 
-    /* where the calculation should take place. This build executes RNNT_GPU only; RNNT_CPU returns
-     * RNNT_STATUS_EXECUTION_FAILED (mirrors the reference's behaviour for a location it was not built
-     * for, src/rnnt_entrypoint.cpp:41-43). */
+    /* where the calculation should take place: RNNT_GPU (HIP kernels, GpuRNNTWorkspaceManager<float>) or
+     * RNNT_CPU (the library's host implementation, CpuRNNTWorkspaceManager<float>) */
     rnntComputeLocation loc;
 };
 

@@ -2,12 +2,15 @@
  * (reference include/rnnt_entrypoint.h:13-27, src/rnnt_entrypoint.cpp:16-48), served by
  * libmonotonic_rnnt_amd.so.
  *
- *   workspace_manager : a GpuRNNTWorkspaceManager<float> (gpu_workspace_manager.h) whose workspace was
- *                       set with set_workspace() or create_workspace()
- *   options           : RNNTOptions; loc must be RNNT_GPU, kernels go to options.stream
+ *   workspace_manager : loc = RNNT_GPU: a GpuRNNTWorkspaceManager<float> (gpu_workspace_manager.h);
+ *                       loc = RNNT_CPU: a CpuRNNTWorkspaceManager<float> (cpu_workspace_manager.h);
+ *                       its workspace set with set_workspace() or create_workspace(). A manager of the other
+ *                       kind is RNNT_STATUS_INVALID_VALUE.
+ *   options           : RNNTOptions; GPU kernels go to options.stream, CPU work uses options.num_threads
  *   costs             : HOST pointer [B], required (NULL -> RNNT_STATUS_INVALID_VALUE); the call returns
- *                       after the costs have been copied to the host (as the reference does)
- *   gradients         : DEVICE pointer [sum_b T_b (S_b+1), V] or NULL for cost only
+ *                       after the costs are on the host (as the reference does)
+ *   gradients         : [sum_b T_b (S_b+1), V], DEVICE pointer (GPU) or HOST pointer (CPU), or NULL for cost
+ *                       only
  */
 #ifndef MONOTONIC_RNNT_ENTRYPOINT_H
 #define MONOTONIC_RNNT_ENTRYPOINT_H

@@ -18,6 +18,8 @@
 // The library is built with -fvisibility=hidden: only the declarations of the public headers below are
 // exported (the kernels and launchers in mrnnt_internal.h stay internal).
 #pragma GCC visibility push(default)
+#include "cpu_rnnt.h"
+#include "cpu_workspace_manager.h"
 #include "gpu_rnnt.h"
 #include "gpu_workspace_manager.h"
 #include "mrnnt.h"
@@ -35,6 +37,12 @@ RNNTStatus fail(RNNTStatus st, const std::string &msg) {
     g_last_error = msg;
     return st;
 }
+
+}  // namespace
+
+RNNTStatus mrnnt::set_error(RNNTStatus st, const std::string &msg) { return fail(st, msg); }
+
+namespace {
 
 RNNTStatus fail_hip(hipError_t e, const char *where) {
     return fail(RNNT_STATUS_EXECUTION_FAILED, std::string(where) + ": " + hipGetErrorString(e));
@@ -77,6 +85,13 @@ RNNTStatus make_plan(const mrnnt_problem *p, Plan *pl) {
     if (q.S_max + 1 > kMaxLabelsPlusOne)
         return fail(RNNT_STATUS_INVALID_VALUE, "max label length " + std::to_string(q.S_max) + " exceeds " +
                                                    std::to_string(kMaxLabelsPlusOne - 1));
+    // the kernels read labels[b * label_stride + s] for s < S_b and alignment[b * align_stride + t] for t < T_b
+    if (q.S_max > 0 && p->label_stride < q.S_max)
+        return fail(RNNT_STATUS_INVALID_VALUE, "label row stride " + std::to_string(p->label_stride) +
+                                                   " < max label length " + std::to_string(q.S_max));
+    if (p->alignment && p->align_stride < q.T_max)
+        return fail(RNNT_STATUS_INVALID_VALUE, "alignment row stride " + std::to_string(p->align_stride) +
+                                                   " < max input length " + std::to_string(q.T_max));
     if (p->acts_dtype != ELEM_F32 && p->acts_dtype != ELEM_BF16 && p->acts_dtype != ELEM_F16)
         return fail(RNNT_STATUS_INVALID_VALUE, "unknown acts_dtype " + std::to_string(p->acts_dtype));
     q.elem = p->acts_dtype;
@@ -335,6 +350,23 @@ RNNTStatus mrnnt_read_loglik(const mrnnt_problem *p, const void *ws, double *ll_
     if (ll_bwd_dev && hipMemcpyAsync(ll_bwd_dev, w + pl.off_llb, sizeof(double) * pl.B, hipMemcpyDeviceToDevice,
                                      stream) != hipSuccess)
         return fail(RNNT_STATUS_MEMOPS_FAILED, "copy ll_bwd");
+    return RNNT_STATUS_SUCCESS;
+}
+
+RNNTStatus mrnnt_read_state(const mrnnt_problem *p, const void *ws, float *den_dev, double *alpha_dev,
+                            double *beta_dev, hipStream_t stream) {
+    Plan pl;
+    RNNTStatus st = make_plan(p, &pl);
+    if (st != RNNT_STATUS_SUCCESS) return st;
+    if (!ws) return fail(RNNT_STATUS_INVALID_VALUE, "workspace is null");
+    const DevProblem d = make_dev(p, pl, ws);
+    if (den_dev && hipMemcpyAsync(den_dev, d.den, sizeof(float) * pl.N, hipMemcpyDeviceToDevice, stream) != hipSuccess)
+        return fail(RNNT_STATUS_MEMOPS_FAILED, "copy den");
+    if (alpha_dev &&
+        hipMemcpyAsync(alpha_dev, d.alpha, sizeof(double) * pl.N, hipMemcpyDeviceToDevice, stream) != hipSuccess)
+        return fail(RNNT_STATUS_MEMOPS_FAILED, "copy alpha");
+    if (beta_dev && hipMemcpyAsync(beta_dev, d.beta, sizeof(double) * pl.N, hipMemcpyDeviceToDevice, stream) != hipSuccess)
+        return fail(RNNT_STATUS_MEMOPS_FAILED, "copy beta");
     return RNNT_STATUS_SUCCESS;
 }
 
@@ -605,7 +637,9 @@ int mrnnt_profile_read(double *total_ms, int64_t *launches, int n) {
     return bad;
 }
 
-int mrnnt_tune(const char *key, int value) {
+#ifdef MRNNT_DEVTOOLS
+// launch knobs: exported by the development build only (libmonotonic_rnnt_amd_dev.so, `make dev`)
+__attribute__((visibility("default"))) int mrnnt_tune(const char *key, int value) {
     if (!key) return -1;
     int *slot = nullptr;
     Tuning &t = tuning();
@@ -630,20 +664,7 @@ int mrnnt_tune(const char *key, int value) {
     if (value >= 0) *slot = value;
     return prev;
 }
-
-RNNTStatus mrnnt_synth_acts(float *out, int64_t begin, int64_t count, uint64_t seed, int normal, hipStream_t stream) {
-    const hipError_t e = launch_synth(out, begin, count, seed, normal, stream);
-    if (e != hipSuccess) return fail_hip(e, "synth kernel");
-    return RNNT_STATUS_SUCCESS;
-}
-
-RNNTStatus mrnnt_copy_probe(void *dst, const void *src, size_t bytes, hipStream_t stream) {
-    if ((bytes & 15) || (reinterpret_cast<uintptr_t>(dst) & 15) || (reinterpret_cast<uintptr_t>(src) & 15))
-        return fail(RNNT_STATUS_INVALID_VALUE, "copy_probe: bytes and pointers must be 16-byte aligned");
-    const hipError_t e = launch_copy_probe(dst, src, bytes, stream);
-    if (e != hipSuccess) return fail_hip(e, "copy probe kernel");
-    return RNNT_STATUS_SUCCESS;
-}
+#endif  // MRNNT_DEVTOOLS
 
 }  // extern "C"
 
@@ -724,6 +745,20 @@ RNNTStatus manager_compute(GpuRNNTWorkspaceManager<float> &wm, int blank, hipStr
     RNNTStatus st = manager_size(s, T, S, &bytes, &coff);
     if (st != RNNT_STATUS_SUCCESS) return st;
     mrnnt_problem p = problem_of(s, T, S, blank);
+    // this surface synchronises anyway (host costs): read the labels back and range-check them, as the flat
+    // entry points cannot without a sync (there an out-of-range device label gives a NaN cost)
+    if (p.label_stride > 0) {
+        std::vector<int> lab((size_t)s->B * p.label_stride);
+        if (hipMemcpy(lab.data(), s->labels, sizeof(int) * lab.size(), hipMemcpyDeviceToHost) != hipSuccess)
+            return fail(RNNT_STATUS_MEMOPS_FAILED, "copying labels to host");
+        for (int b = 0; b < s->B; ++b)
+            for (int i = 0; i < S[b]; ++i) {
+                const int l = lab[(size_t)b * p.label_stride + i];
+                if (l < 0 || l >= s->V)
+                    return fail(RNNT_STATUS_INVALID_VALUE, "label " + std::to_string(l) + " at (" + std::to_string(b) +
+                                                               ", " + std::to_string(i) + ") outside [0, V)");
+            }
+    }
     float *costs_dev = reinterpret_cast<float *>(static_cast<char *>(s->workspace) + coff);
     st = mrnnt_cost_and_grad(&p, s->workspace, coff, costs_dev, grads, nullptr, stream);
     if (st != RNNT_STATUS_SUCCESS) return st;
@@ -827,11 +862,14 @@ RNNTStatus GpuRNNTComputer<float>::cost(float *costs) {
 
 extern "C" RNNTStatus compute_rnnt_loss(RNNTWorkspaceManager &workspace_manager, RNNTOptions options, float *costs,
                                         float *gradients) {
-    // src/rnnt_entrypoint.cpp:16-48
+    // src/rnnt_entrypoint.cpp:16-48 (a manager of the wrong kind is RNNT_STATUS_INVALID_VALUE here; the
+    // reference's reference-typed dynamic_cast throws std::bad_cast across the C boundary)
     if (costs == nullptr) return fail(RNNT_STATUS_INVALID_VALUE, "costs is null");
     if (options.loc == RNNT_CPU) {
-        std::fprintf(stderr, "CPU execution requested, but this is the MI355X (HIP) build of monotonic RNN-T\n");
-        return fail(RNNT_STATUS_EXECUTION_FAILED, "CPU execution requested, but this is the MI355X (HIP) build");
+        auto *cm = dynamic_cast<CpuRNNTWorkspaceManager<float> *>(&workspace_manager);
+        if (!cm) return fail(RNNT_STATUS_INVALID_VALUE, "workspace manager is not a CpuRNNTWorkspaceManager<float>");
+        CpuRNNTComputer<float> computer(*cm, options.blank_label, options.num_threads);
+        return gradients != nullptr ? computer.cost_and_grad(costs, gradients) : computer.cost(costs);
     }
     if (options.loc != RNNT_GPU) return fail(RNNT_STATUS_INVALID_VALUE, "unknown compute location");
     auto *gm = dynamic_cast<GpuRNNTWorkspaceManager<float> *>(&workspace_manager);

@@ -122,6 +122,16 @@ __device__ __forceinline__ void align_window(const DevProblem &p, int64_t c, int
     hi = min(hi, whi);
 }
 
+// Label of row s as the log-softmax kernels use it (has = s < S). Device labels are not range-checked on the
+// host (that would need a sync), so a label outside [0, V) reads no logit: it is returned as -1 (no capture)
+// and the row's label logit `ze` starts as NaN, so its lp -- hence the utterance's cost and gradient -- is NaN.
+// A row without a label (s == S) returns -1 with ze = 0.
+__device__ __forceinline__ int checked_label(bool has, int l, int V, float &ze) {
+    const bool bad = has && (unsigned)l >= (unsigned)V;
+    ze = bad ? __builtin_nanf("") : 0.0f;
+    return (has && !bad) ? l : -1;
+}
+
 __device__ __forceinline__ void write_row(const DevProblem &p, int64_t row, float m, float sum, float zb, float ze) {
     const double den = -(double)m - log((double)sum);
     p.den[row] = (float)den;
@@ -216,7 +226,7 @@ __device__ __forceinline__ float zero_row_value(double ll, float sc) {
     return (ll > NEG_INF_D ? 0.0f : __builtin_nanf("")) * sc;
 }
 
-// The dead-row predicate (mrnnt_internal.h kDeadLogOcc); NaN state is live.
+// The dead-row predicate (mrnnt_host.h kDeadLogOcc); NaN state is live.
 __device__ __forceinline__ bool row_live(double log_occ) { return !(log_occ < kDeadLogOcc); }
 
 __device__ __forceinline__ RowCoef row_coef(const DevProblem &p, int t, int T, int S, int s, int64_t row, double ll,
@@ -235,7 +245,7 @@ __device__ __forceinline__ RowCoef row_coef(const DevProblem &p, int t, int T, i
     rc.cb = fast_exp2((float)((p.lpb[row] + base + b1) * kLog2eD));
     rc.ce = (s < S) ? fast_exp2((float)((p.lpe[row] + base + b2) * kLog2eD)) : 0.0f;
     const int lab = (s < S) ? lab_b[s] : -1;
-    rc.lab = (lab == p.blank) ? -1 : lab;
+    rc.lab = (lab == p.blank || (unsigned)lab >= (unsigned)p.V) ? -1 : lab;  // out of range: never matched / written
     return rc;
 }
 

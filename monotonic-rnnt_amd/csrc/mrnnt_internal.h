@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "mrnnt_host.h"
+
 namespace mrnnt {
 
 // Element type of acts and grads (the math is fp32/fp64 inside the kernels).
@@ -109,15 +111,8 @@ hipError_t launch_dp(const DevProblem &p, int S_max, int with_beta, float *costs
 hipError_t launch_grad(const DevProblem &p, int elem, const float *scale, void *grads, int grid, hipStream_t stream);
 hipError_t launch_count_live(const DevProblem &p, unsigned long long *count, hipStream_t stream);
 hipError_t launch_pad_zero(const DevProblem &p, int elem, void *grads, hipStream_t stream);
-hipError_t launch_copy_probe(void *dst, const void *src, size_t bytes, hipStream_t stream);
-hipError_t launch_synth(float *out, int64_t begin, int64_t count, uint64_t seed, int normal, hipStream_t stream);
 
-// A lattice row (t, s) with alpha(t-1, s) + beta(t, s) - ll < kDeadLogOcc has occupancy below e^-110 =
-// 2^-158.7: every element of its fp32 gradient, p_v * occupancy minus the blank / label corrections (each
-// bounded by the occupancy), is below half the smallest fp32 denormal (2^-150) and rounds to exactly 0 --
-// in this kernel and in the reference's fp32 arithmetic alike. Such rows are stored as 0 * grad_scale
-// without reading acts. (NaN state compares false and takes the full path.)
-constexpr double kDeadLogOcc = -110.0;
+// kDeadLogOcc (the exact-zero gradient-row threshold) is in mrnnt_host.h, shared with the CPU implementation.
 
 // Largest S+1 the recursion instantiations cover (8 waves x 64 lanes x 4 cells per lane).
 constexpr int kMaxLabelsPlusOne = 2048;

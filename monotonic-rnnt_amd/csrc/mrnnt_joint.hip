@@ -155,7 +155,9 @@ __device__ __forceinline__ RowPos row_pos(const DevProblem &p, const JointArgs &
     q.T = p.T[q.b];
     q.S = p.S[q.b];
     q.row = p.row_off[q.b] + (int64_t)q.t * (q.S + 1) + q.s;
-    q.lab = q.s < q.S ? p.labels[(int64_t)q.b * p.label_stride + q.s] : -1;
+    // -2: a label outside [0, V) (device labels are not range-checked on the host): no capture, lpe = NaN
+    const int l = q.s < q.S ? p.labels[(int64_t)q.b * p.label_stride + q.s] : -1;
+    q.lab = (q.s < q.S && (unsigned)l >= (unsigned)p.V) ? -2 : l;
     q.valid = true;
     return q;
 }
@@ -409,7 +411,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
         const double den = -(double)mn - log((double)sum);
         p.den[q.row] = (float)den;
         p.lpb[q.row] = (double)zb + den;
-        p.lpe[q.row] = (q.lab >= 0 ? (double)ze : 0.0) + den;
+        p.lpe[q.row] = (q.lab >= 0 ? (double)ze : (q.lab == -2 ? __builtin_nan("") : 0.0)) + den;
     }
 }
 

@@ -1,5 +1,5 @@
 // mrnnt_setup.hip -- per-call metadata on the device (no host copies): lattice row/column offsets from the
-// length arrays, the alignment band, plus the bench/test synthetic generator and the launch knobs.
+// length arrays, the alignment band, and the launch knobs.
 #include "mrnnt_device.h"
 
 namespace mrnnt {
@@ -92,33 +92,6 @@ __global__ __launch_bounds__(256) void align_band_kernel(DevProblem p, int k, co
     }
 }
 
-// synthetic generator (bench / tests), bit-identical to mrnnt_oracle_synth_acts (oracle/rnnt_oracle.c):
-// integer hashing + one exact int->float conversion and one multiply, nothing that rounds differently
-// on the host.
-__device__ __forceinline__ uint64_t splitmix(uint64_t x) {
-    x += 0x9E3779B97F4A7C15ull;
-    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-    return x ^ (x >> 31);
-}
-
-__global__ __launch_bounds__(256) void synth_kernel(float *__restrict__ out, int64_t begin, int64_t count,
-                                                    uint64_t seed, int normal) {
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) {
-        const uint64_t h = splitmix(seed * 0xD1B54A32D192ED03ull + (uint64_t)(begin + i));
-        float v;
-        if (!normal) {
-            v = (float)(uint32_t)(h >> 40) * (1.0f / 16777216.0f);
-        } else {
-            const int32_t s4 = (int32_t)(h & 0xFFFF) + (int32_t)((h >> 16) & 0xFFFF) +
-                               (int32_t)((h >> 32) & 0xFFFF) + (int32_t)(h >> 48);
-            v = (float)(s4 - 131070) * (1.0f / 37837.23f);
-        }
-        out[i] = v;
-    }
-}
-
 // col_b[c] = utterance of lattice column c: one load instead of a binary search over col_off per workgroup
 __global__ __launch_bounds__(256) void col_map_kernel(const int *__restrict__ T, const int64_t *__restrict__ col_off,
                                                       int *__restrict__ col_b) {
@@ -142,48 +115,6 @@ hipError_t launch_align(const DevProblem &p, const int *alignment, int64_t align
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     align_band_kernel<<<dim3(8, std::min(p.B, 65535)), 256, 0, stream>>>(p, max_shift, mtmp, min_s, max_s);
-    return hipGetLastError();
-}
-
-// bandwidth probe: a device copy in the gradient pass's access pattern -- each workgroup streams its own
-// contiguous slab of 16-byte elements, 4 loads in flight per lane, nontemporal loads and stores
-__global__ __launch_bounds__(256) void copy_probe_kernel(const u4 *__restrict__ a, u4 *__restrict__ b, int64_t n,
-                                                         int64_t slab) {
-    for (int64_t c0 = (int64_t)blockIdx.x * slab; c0 < n; c0 += (int64_t)gridDim.x * slab) {
-        const int64_t end = min(c0 + slab, n);
-        for (int64_t i = c0 + threadIdx.x; i < end; i += 256 * 4) {
-            u4 x[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (i + 256 * u < end) x[u] = __builtin_nontemporal_load(&a[i + 256 * u]);
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (i + 256 * u < end) __builtin_nontemporal_store(x[u], &b[i + 256 * u]);
-        }
-    }
-}
-
-hipError_t launch_copy_probe(void *dst, const void *src, size_t bytes, hipStream_t stream) {
-    const int64_t n = (int64_t)(bytes / 16);
-    if (n <= 0) return hipSuccess;
-    int dev = 0, cus = 256;
-    hipError_t e = hipGetDevice(&dev);
-    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (e != hipSuccess) return e;
-    // 32 workgroups per CU, each streaming >= 8 slabs in turn (a single pass of one slab per workgroup
-    // measures the launch tail, not the memory); slabs of 16 KiB .. 800 KiB, whole 4 KiB workgroup steps
-    const int64_t blocks_max = (int64_t)32 * cus;
-    const int64_t slab = std::min<int64_t>(50 * 1024, std::max<int64_t>(1024, n / (blocks_max * 8) / 1024 * 1024));
-    const int64_t blocks = std::min<int64_t>((n + slab - 1) / slab, blocks_max);
-    copy_probe_kernel<<<(int)blocks, 256, 0, stream>>>(static_cast<const u4 *>(src), static_cast<u4 *>(dst), n, slab);
-    return hipGetLastError();
-}
-
-hipError_t launch_synth(float *out, int64_t begin, int64_t count, uint64_t seed, int normal, hipStream_t stream) {
-    if (count <= 0) return hipSuccess;
-    int64_t blocks = (count + 255) / 256;
-    if (blocks > 65536) blocks = 65536;
-    synth_kernel<<<(int)blocks, 256, 0, stream>>>(out, begin, count, seed, normal);
     return hipGetLastError();
 }
 

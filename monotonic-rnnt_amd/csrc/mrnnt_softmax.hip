@@ -59,11 +59,10 @@ __global__ __launch_bounds__(256) void softmax_kernel(DevProblem p) {
             for (int r = 0; r < R; ++r) {
                 const int sr = s + r;
                 ok[r] = sr <= hi;
-                lab[r] = (ok[r] && sr < S) ? lab_b[sr] : -1;
+                lab[r] = checked_label(ok[r] && sr < S, (ok[r] && sr < S) ? lab_b[sr] : 0, p.V, ze[r]);
                 m[r] = NEG_INF_F;
                 sum[r] = 0.0f;
                 zb[r] = 0.0f;
-                ze[r] = 0.0f;
             }
             for (int base = 0; base < VL; base += 64 * U) {
                 Vec x[R][U];
@@ -107,7 +106,7 @@ __global__ __launch_bounds__(256) void softmax_kernel(DevProblem p) {
             for (int r = 0; r < R; ++r) {
                 if (!ok[r]) continue;
                 const float zbv = __shfl(zb[r], blane);
-                const float zev = lab[r] >= 0 ? __shfl(ze[r], (lab[r] / E) & 63) : 0.0f;
+                const float zev = lab[r] >= 0 ? __shfl(ze[r], (lab[r] / E) & 63) : ze[r];  // ze: 0, or NaN (bad label)
                 if (lane == 0) write_row(p, rowc + s + r, m[r], sum[r], zbv, zev);
             }
         }
@@ -161,11 +160,11 @@ __global__ __launch_bounds__(256) void softmax_lean_kernel(DevProblem p) {
             int lab[R];
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                lab[r] = (r < nrow && s + r < S) ? __builtin_amdgcn_readfirstlane(lab_b[s + r]) : -1;
+                const bool has = r < nrow && s + r < S;
+                lab[r] = checked_label(has, has ? __builtin_amdgcn_readfirstlane(lab_b[s + r]) : 0, p.V, ze[r]);
                 m[r] = NEG_INF_F;
                 sum[r] = 0.0f;
                 zb[r] = 0.0f;
-                ze[r] = 0.0f;
             }
             for (int base = 0; base < VL; base += CH) {
                 Vec x[R][U];
@@ -264,9 +263,10 @@ __global__ __launch_bounds__(256) void softmax_scalar_kernel(DevProblem p) {
         const int *__restrict__ lab_b = p.labels + (int64_t)b * p.label_stride;
         zero_fill_outside_band(p, rowc, S, lo, hi);
         for (int s = lo + wave; s <= hi; s += 4) {
-            const int lab = s < S ? lab_b[s] : -1;
+            float ze;
+            const int lab = checked_label(s < S, s < S ? lab_b[s] : 0, V, ze);
             const Sc *__restrict__ z = acts + (arow + s) * (int64_t)V;
-            float m = NEG_INF_F, sum = 0.0f, zb = 0.0f, ze = 0.0f;
+            float m = NEG_INF_F, sum = 0.0f, zb = 0.0f;
             for (int v0 = 0; v0 < V; v0 += 256) {
                 float x[4];
 #pragma unroll
@@ -286,7 +286,7 @@ __global__ __launch_bounds__(256) void softmax_scalar_kernel(DevProblem p) {
             }
             wave_reduce_max_sum(m, sum);
             const float zbv = __shfl(zb, blank & 63);
-            const float zev = lab >= 0 ? __shfl(ze, lab & 63) : 0.0f;
+            const float zev = lab >= 0 ? __shfl(ze, lab & 63) : ze;  // ze: 0, or NaN (bad label)
             if (lane == 0) write_row(p, rowc + s, m, sum, zbv, zev);
         }
     }

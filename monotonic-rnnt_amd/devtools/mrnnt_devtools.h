@@ -1,0 +1,26 @@
+/* mrnnt_devtools.h -- libmrnnt_devtools.so, bench / test helpers (not part of the product ABI).
+ * Return 0 on success, 2 on invalid arguments, 3 on a launch failure. */
+#ifndef MONOTONIC_RNNT_DEVTOOLS_H
+#define MONOTONIC_RNNT_DEVTOOLS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+typedef struct ihipStream_t *hipStream_t;
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* out[0..count) = element (begin + i) of the counter-based generator: N(0,1)-like (normal=1) or U[0,1). */
+int mrnnt_synth_acts(float *out, int64_t begin, int64_t count, uint64_t seed, int normal, hipStream_t stream);
+
+/* Nontemporal device copy of `bytes` (multiple of 16, 16-byte aligned pointers) in the gradient pass's
+ * access pattern (contiguous slabs per workgroup). */
+int mrnnt_copy_probe(void *dst, const void *src, size_t bytes, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

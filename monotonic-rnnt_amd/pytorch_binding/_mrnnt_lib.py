@@ -1,18 +1,25 @@
 """ctypes binding of libmonotonic_rnnt_amd.so (the flat C ABI in include/mrnnt.h).
 
-There is no fallback: if the HIP library is missing or fails to load, importing this module raises.
-Build it with `python __graft_entry__.py` (or `make -C monotonic-rnnt_amd`). MRNNT_LIB=<path> loads another
-build of the same ABI instead (A/B measurements of compile-time variants, tools/); MRNNT_TUNE="key=value,..."
-sets launch knobs (mrnnt_tune) at load.
+There is no fallback: if the library is missing or fails to load, importing this module raises.
+Build it with `python __graft_entry__.py` (or `make -C monotonic-rnnt_amd`).
+
+Besides the product library, two development builds sit next to it (never loaded by the product path):
+  libmonotonic_rnnt_amd_dev.so : the same kernels with the launch knobs exported (mrnnt_tune); load_dev(),
+                                 and `with use(load_dev()):` routes this module's callers through it (tests
+                                 of the launch variants, tools/kbench.py)
+  libmrnnt_devtools.so         : synthetic logits and a copy probe for bench.py / tests (devtools())
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import threading
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.environ.get("MRNNT_LIB") or os.path.join(PKG_DIR, "libmonotonic_rnnt_amd.so")
+LIB_PATH = os.path.join(PKG_DIR, "libmonotonic_rnnt_amd.so")
+DEV_PATH = os.path.join(PKG_DIR, "libmonotonic_rnnt_amd_dev.so")
+TOOLS_PATH = os.path.join(PKG_DIR, "libmrnnt_devtools.so")
 
 RNNT_STATUS_SUCCESS = 0
 RNNT_STATUS_MEMOPS_FAILED = 1
@@ -88,56 +95,112 @@ class MrnntError(RuntimeError):
 
 
 _lib = None
+_dev = None
+_tools = None
+_override = None
 _lock = threading.Lock()
 
 
+def _bind(path: str, dev: bool = False) -> ctypes.CDLL:
+    if not os.path.exists(path):
+        raise ImportError(f"monotonic RNN-T library not built: {path} is missing "
+                          "(run `python __graft_entry__.py` or `make -C monotonic-rnnt_amd`)")
+    lib = ctypes.CDLL(path)
+    P = ctypes.POINTER(MrnntProblem)
+    JP = ctypes.POINTER(MrnntJointProblem)
+    vp, i, i64, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_size_t
+    sig = {
+        "mrnnt_workspace_size": (i, [P, ctypes.POINTER(sz)]),
+        "mrnnt_forward": (i, [P, vp, sz, vp, i, vp]),
+        "mrnnt_backward": (i, [P, vp, vp, vp, vp]),
+        "mrnnt_cost_and_grad": (i, [P, vp, sz, vp, vp, vp, vp]),
+        "mrnnt_read_loglik": (i, [P, vp, vp, vp, vp]),
+        "mrnnt_grad_live_rows": (i, [P, vp, vp, vp]),
+        "mrnnt_read_state": (i, [P, vp, vp, vp, vp, vp]),
+        "mrnnt_cpu_read_state": (i, [P, vp, vp, vp, vp]),
+        "mrnnt_cpu_workspace_size": (i, [P, ctypes.POINTER(sz)]),
+        "mrnnt_cpu_forward": (i, [P, vp, sz, vp, i, i]),
+        "mrnnt_cpu_backward": (i, [P, vp, vp, vp, i]),
+        "mrnnt_joint_workspace_size": (i, [JP, ctypes.POINTER(sz)]),
+        "mrnnt_joint_forward": (i, [JP, vp, sz, vp, i, vp]),
+        "mrnnt_joint_live_rows": (i, [JP, vp, vp, vp]),
+        "mrnnt_joint_backward": (i, [JP, vp, i64, vp, vp, vp, vp, vp, vp]),
+        "mrnnt_joint_reduce": (i, [JP, vp, i64, vp, vp, vp, vp, vp]),
+        "mrnnt_last_error": (ctypes.c_char_p, []),
+        "mrnnt_version": (i, []),
+        "mrnnt_profile_enable": (None, [i]),
+        "mrnnt_profile_read": (i, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64), i]),
+    }
+    if dev:
+        sig["mrnnt_tune"] = (i, [ctypes.c_char_p, i])
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.mrnnt_version() < 3:
+        raise ImportError(f"{path} is a stale build (ABI version {lib.mrnnt_version()} < 3); "
+                          "rebuild with `make -C monotonic-rnnt_amd`")
+    return lib
+
+
 def load() -> ctypes.CDLL:
+    """The library every call of this package goes through: the product build (or, inside `use(...)`, the
+    library given there)."""
     global _lib
+    if _override is not None:
+        return _override
     if _lib is not None:
         return _lib
     with _lock:
-        if _lib is not None:
-            return _lib
-        if not os.path.exists(LIB_PATH):
-            raise ImportError(f"monotonic RNN-T HIP library not built: {LIB_PATH} is missing "
-                              "(run `python __graft_entry__.py` or `make -C monotonic-rnnt_amd`)")
-        lib = ctypes.CDLL(LIB_PATH)
-        P = ctypes.POINTER(MrnntProblem)
-        JP = ctypes.POINTER(MrnntJointProblem)
-        vp, i, i64, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_size_t
-        sig = {
-            "mrnnt_workspace_size": (i, [P, ctypes.POINTER(sz)]),
-            "mrnnt_forward": (i, [P, vp, sz, vp, i, vp]),
-            "mrnnt_backward": (i, [P, vp, vp, vp, vp]),
-            "mrnnt_cost_and_grad": (i, [P, vp, sz, vp, vp, vp, vp]),
-            "mrnnt_read_loglik": (i, [P, vp, vp, vp, vp]),
-            "mrnnt_grad_live_rows": (i, [P, vp, vp, vp]),
-            "mrnnt_joint_workspace_size": (i, [JP, ctypes.POINTER(sz)]),
-            "mrnnt_joint_forward": (i, [JP, vp, sz, vp, i, vp]),
-            "mrnnt_joint_live_rows": (i, [JP, vp, vp, vp]),
-            "mrnnt_joint_backward": (i, [JP, vp, i64, vp, vp, vp, vp, vp, vp]),
-            "mrnnt_joint_reduce": (i, [JP, vp, i64, vp, vp, vp, vp, vp]),
-            "mrnnt_last_error": (ctypes.c_char_p, []),
-            "mrnnt_version": (i, []),
-            "mrnnt_profile_enable": (None, [i]),
-            "mrnnt_profile_read": (i, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64), i]),
-            "mrnnt_synth_acts": (i, [vp, i64, i64, ctypes.c_uint64, i, vp]),
-            "mrnnt_copy_probe": (i, [vp, vp, sz, vp]),
-            "mrnnt_tune": (i, [ctypes.c_char_p, i]),
-        }
-        for name, (res, args) in sig.items():
-            fn = getattr(lib, name)
-            fn.restype = res
-            fn.argtypes = args
-        if lib.mrnnt_version() < 3:
-            raise ImportError(f"{LIB_PATH} is a stale build (ABI version {lib.mrnnt_version()} < 3); "
-                              "rebuild with `make -C monotonic-rnnt_amd`")
-        for kv in filter(None, os.environ.get("MRNNT_TUNE", "").split(",")):
-            k, v = kv.split("=")
-            if lib.mrnnt_tune(k.strip().encode(), int(v)) < 0:
-                raise ValueError(f"MRNNT_TUNE: unknown knob {k!r}")
-        _lib = lib
-        return lib
+        if _lib is None:
+            _lib = _bind(LIB_PATH)
+        return _lib
+
+
+def load_dev() -> ctypes.CDLL:
+    """The development build (same kernels, launch knobs exported through mrnnt_tune)."""
+    global _dev
+    with _lock:
+        if _dev is None:
+            _dev = _bind(DEV_PATH, dev=True)
+        return _dev
+
+
+@contextlib.contextmanager
+def use(lib: ctypes.CDLL):
+    """Route load() -- hence every op of this package -- through `lib` (e.g. load_dev()) inside the block."""
+    global _override
+    prev = _override
+    _override = lib
+    try:
+        yield lib
+    finally:
+        _override = prev
+
+
+def devtools() -> ctypes.CDLL:
+    """libmrnnt_devtools.so: mrnnt_synth_acts / mrnnt_copy_probe (bench and tests only)."""
+    global _tools
+    with _lock:
+        if _tools is None:
+            if not os.path.exists(TOOLS_PATH):
+                raise ImportError(f"{TOOLS_PATH} is missing (run `make -C monotonic-rnnt_amd`)")
+            t = ctypes.CDLL(TOOLS_PATH)
+            t.mrnnt_synth_acts.restype = ctypes.c_int
+            t.mrnnt_synth_acts.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_uint64,
+                                           ctypes.c_int, ctypes.c_void_p]
+            t.mrnnt_copy_probe.restype = ctypes.c_int
+            t.mrnnt_copy_probe.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+            _tools = t
+        return _tools
+
+
+def synth_acts(out_ptr: int, begin: int, count: int, seed: int, normal: bool, stream: int) -> None:
+    """Fill a device fp32 buffer with the counter-based synthetic generator (devtools)."""
+    rc = devtools().mrnnt_synth_acts(ctypes.c_void_p(out_ptr), begin, count, seed, 1 if normal else 0,
+                                     ctypes.c_void_p(stream))
+    if rc != 0:
+        raise RuntimeError(f"mrnnt_synth_acts failed ({rc})")
 
 
 def check(status: int, where: str) -> None:
@@ -147,8 +210,12 @@ def check(status: int, where: str) -> None:
 
 
 def tune(key: str, value: int = -1) -> int:
-    """Set a launch-shape knob (mrnnt_tune); returns the previous value (-1 = unknown key)."""
-    return load().mrnnt_tune(key.encode(), int(value))
+    """Set a launch-shape knob of the current library (needs the development build: `with use(load_dev()):`);
+    returns the previous value (-1 = unknown key)."""
+    lib = load()
+    if not hasattr(lib, "mrnnt_tune") or lib.mrnnt_tune.restype is not ctypes.c_int:
+        raise RuntimeError("launch knobs need the development build: `with _mrnnt_lib.use(_mrnnt_lib.load_dev()):`")
+    return lib.mrnnt_tune(key.encode(), int(value))
 
 
 def profile_enable(on: bool = True) -> None:

@@ -9,15 +9,19 @@ pytorch_binding/monotonic_rnnt_op.py:
   monotonic_rnnt_cpp.gpu_monotonic_rnnt(...) / .gpu_monotonic_rnnt_align_restrict(...)
                                               (reference pybind names, monotonic_rnnt.cu:81-152)
 
-Execution goes through the C ABI of libmonotonic_rnnt_amd.so (HIP kernels on the current torch stream);
-there is no CPU or eager-PyTorch fallback -- CPU tensors raise.
+Execution goes through the C ABI of libmonotonic_rnnt_amd.so: GPU tensors run the HIP kernels on the current
+torch stream; CPU tensors run the library's own multithreaded host implementation (mrnnt_cpu_*, the
+reference's cpu_monotonic_rnnt path). There is no eager-PyTorch fallback.
 
 Behavioural differences from the reference, all deliberate:
   * forward runs the log-softmax reduce and the alpha/beta recursion; the logit gradient is produced
     in backward with dL/dcost[b] fused into the kernel (the reference writes grads in forward into a
     zeros_like(acts) and rescales them in backward: 3 extra passes over an N x V tensor, :32-36, :96-118);
   * costs are computed on the device (the reference computes into a host tensor and copies, :37, :90);
-  * labels / alignment use their true row strides (the reference assumes max(S) / max(T));
+  * labels / alignment use their true row strides (the reference assumes max(S) / max(T)); strides below
+    max(S) / max(T), and (for host labels) labels outside [0, V), are rejected;
+  * acts without requires_grad take the cost-only path on both devices (the reference's CPU path segfaults
+    writing into its empty grads tensor);
   * MonotonicRNNTLoss.forward uses self.blank_label (the reference reads a missing self.blank, :214).
 
 Extensions beyond the reference: bf16/fp16 acts (costs stay fp32) and the padded
@@ -47,45 +51,70 @@ def _ptr(t: Optional[torch.Tensor]):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
+# Host lengths go up once per distinct (T, S) content and device: training loops repeat a handful of shapes, so
+# the pinned staging copy and its H2D transfer are paid once, not per call. Entries are never written after
+# creation (the kernels only read them).
+_LEN_CACHE: "dict" = {}
+_LEN_CACHE_MAX = 64
+
+
 def _lengths_on_device(input_lengths, label_lengths, T_host, S_host, dev):
     """Device int32 copies of the lengths: device inputs are converted in place on the GPU; host inputs go up
-    as one pinned, non-blocking copy (stream-ordered before the kernels, no host wait)."""
+    as one pinned, non-blocking copy (stream-ordered before the kernels, no host wait), cached by content."""
     if input_lengths.is_cuda or label_lengths.is_cuda:
         return (input_lengths.detach().to(dev, torch.int32).contiguous().view(-1),
                 label_lengths.detach().to(dev, torch.int32).contiguous().view(-1))
-    ts = torch.from_numpy(np.stack([T_host, S_host])).pin_memory().to(dev, non_blocking=True)
-    return ts[0], ts[1]
+    key = (dev, T_host.tobytes(), S_host.tobytes())
+    hit = _LEN_CACHE.get(key)
+    if hit is None:
+        ts = torch.from_numpy(np.stack([T_host, S_host])).pin_memory().to(dev, non_blocking=True)
+        if len(_LEN_CACHE) >= _LEN_CACHE_MAX:
+            _LEN_CACHE.pop(next(iter(_LEN_CACHE)))
+        hit = _LEN_CACHE[key] = (ts[0], ts[1])
+    return hit
+
+
+def _host_int32(t: torch.Tensor) -> np.ndarray:
+    t = t.detach()
+    if t.is_cuda:
+        t = t.cpu()  # a sync, as the reference's cudaMemcpy of the lengths (gpu_workspace_manager.h:87-96)
+    return np.ascontiguousarray(t.numpy() if t.dtype == torch.int32 else t.to(torch.int32).numpy()).reshape(-1)
 
 
 class _Prepared:
-    """Device/host views of one call's inputs plus the filled mrnnt_problem."""
+    """Views of one call's inputs on the device they live on, plus the filled mrnnt_problem.
 
-    def __init__(self, acts, labels, input_lengths, label_lengths, alignment, max_shift, blank_label):
-        if not acts.is_cuda:
-            raise RuntimeError("monotonic_rnnt (MI355X build): acts must be a GPU tensor; "
-                               "this build has no CPU implementation")
+    GPU acts: device lengths / labels / alignment (host lengths plan the launch). CPU acts: every pointer on
+    the host (the mrnnt_cpu_* entry points)."""
+
+    def __init__(self, acts, labels, input_lengths, label_lengths, alignment, max_shift, blank_label,
+                 num_threads=0):
         if acts.dtype not in _ELEM:
             raise RuntimeError("monotonic_rnnt: acts must be float32 (reference monotonic_rnnt.cu:19,84), "
-                               f"or bfloat16 / float16 (extension); got {acts.dtype}")
+                               f"or bfloat16 / float16 (extension, GPU only); got {acts.dtype}")
         if acts.dim() not in (2, 4):
             raise RuntimeError("monotonic_rnnt: acts must be packed 2-D [sum_b T_b (S_b+1), V] "
                                "or padded 4-D [B, max_T, max_S+1, V]")
+        self.on_gpu = acts.is_cuda
+        if not self.on_gpu and acts.dtype != torch.float32:
+            raise RuntimeError(f"monotonic_rnnt: the CPU implementation takes float32 acts, got {acts.dtype}")
         dev = acts.device
         self.acts = acts.contiguous()
+        self.num_threads = int(num_threads)
         B = labels.size(0)
-        # The plan (sizes, validation) needs the lengths on the host and the kernels need them on the device.
-        # Device lengths are read back (a sync, as the reference's cudaMemcpy, gpu_workspace_manager.h:63-69);
-        # host lengths go up in one pinned, non-blocking copy, so the call never waits for the GPU.
-        self.T_host = np.ascontiguousarray(input_lengths.detach().to("cpu", torch.int32).numpy()).reshape(-1)
-        self.S_host = np.ascontiguousarray(label_lengths.detach().to("cpu", torch.int32).numpy()).reshape(-1)
+        self.T_host = _host_int32(input_lengths)
+        self.S_host = _host_int32(label_lengths)
         if self.T_host.size != B or self.S_host.size != B:
             raise RuntimeError(f"monotonic_rnnt: expected {B} input/label lengths, "
                                f"got {self.T_host.size}/{self.S_host.size}")
-        self.T_dev, self.S_dev = _lengths_on_device(input_lengths, label_lengths, self.T_host, self.S_host, dev)
         lab = labels.detach().to(dev, torch.int32)
         if lab.dim() == 1:
             lab = lab.view(B, -1)
         self.labels = lab.contiguous() if lab.numel() else torch.zeros(B, 1, dtype=torch.int32, device=dev)
+        if self.on_gpu:
+            self.T_dev, self.S_dev = _lengths_on_device(input_lengths, label_lengths, self.T_host, self.S_host, dev)
+            if not labels.is_cuda:
+                _check_labels(labels, self.S_host, acts.size(-1))
         self.alignment = None
         if alignment is not None:
             al = alignment.detach().to(dev, torch.int32)
@@ -97,8 +126,9 @@ class _Prepared:
         p.max_shift = int(max_shift)
         p.T_host = self.T_host.ctypes.data
         p.S_host = self.S_host.ctypes.data
-        p.T_dev = self.T_dev.data_ptr()
-        p.S_dev = self.S_dev.data_ptr()
+        if self.on_gpu:
+            p.T_dev = self.T_dev.data_ptr()
+            p.S_dev = self.S_dev.data_ptr()
         p.acts = self.acts.data_ptr()
         p.labels = self.labels.data_ptr()
         p.label_stride = self.labels.size(1)
@@ -118,27 +148,54 @@ class _Prepared:
 
     def workspace(self) -> torch.Tensor:
         n = ctypes.c_size_t(0)
-        _L.check(_L.load().mrnnt_workspace_size(ctypes.byref(self.problem), ctypes.byref(n)), "workspace_size")
+        fn = _L.load().mrnnt_workspace_size if self.on_gpu else _L.load().mrnnt_cpu_workspace_size
+        _L.check(fn(ctypes.byref(self.problem), ctypes.byref(n)), "workspace_size")
         return torch.empty(max(1, n.value), dtype=torch.uint8, device=self.device)
 
     def stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
 
+def _check_labels(labels: torch.Tensor, S_host: np.ndarray, V: int) -> None:
+    """Host labels: every label inside the lattice (s < S_b) must be in [0, V). (Device labels are not read back;
+    the kernels never index past a row with them, and an out-of-range label yields a NaN cost.)"""
+    lab = labels.detach().to(torch.int32).numpy()
+    lab = lab.reshape(len(S_host), -1) if lab.size else lab.reshape(len(S_host), 0)
+    if lab.shape[1] < int(S_host.max(initial=0)):
+        return  # the stride check in the library reports this
+    mask = np.arange(lab.shape[1])[None, :] < S_host[:, None]
+    bad = mask & ((lab < 0) | (lab >= V))
+    if bad.any():
+        b, s = map(int, np.argwhere(bad)[0])
+        raise _L.MrnntError(_L.RNNT_STATUS_INVALID_VALUE, "monotonic_rnnt",
+                            f"label {int(lab[b, s])} at ({b}, {s}) outside [0, V = {V})")
+
+
 def _forward(prep: _Prepared, with_beta: bool):
+    lib = _L.load()
+    ws = prep.workspace()
+    costs = torch.empty(prep.problem.B, dtype=torch.float32, device=prep.device)
+    if not prep.on_gpu:
+        _L.check(lib.mrnnt_cpu_forward(ctypes.byref(prep.problem), _ptr(ws), ws.numel(), _ptr(costs),
+                                       1 if with_beta else 0, prep.num_threads), "mrnnt_cpu_forward")
+        return costs, ws
     with torch.cuda.device(prep.device):  # kernels go to this device's current stream
-        ws = prep.workspace()
-        costs = torch.empty(prep.problem.B, dtype=torch.float32, device=prep.device)
-        _L.check(_L.load().mrnnt_forward(ctypes.byref(prep.problem), _ptr(ws), ws.numel(), _ptr(costs),
-                                         1 if with_beta else 0, prep.stream()), "mrnnt_forward")
+        _L.check(lib.mrnnt_forward(ctypes.byref(prep.problem), _ptr(ws), ws.numel(), _ptr(costs),
+                                   1 if with_beta else 0, prep.stream()), "mrnnt_forward")
     return costs, ws
 
 
-def _backward(prep: _Prepared, ws: torch.Tensor, grad_scale: Optional[torch.Tensor]) -> torch.Tensor:
-    with torch.cuda.device(prep.device):
+def _backward(prep: _Prepared, ws: torch.Tensor, grad_scale: Optional[torch.Tensor],
+              grads: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if grads is None:
         grads = torch.empty_like(prep.acts)
-        if grad_scale is not None:
-            grad_scale = grad_scale.detach().to(prep.device, torch.float32).contiguous()
+    if grad_scale is not None:
+        grad_scale = grad_scale.detach().to(prep.device, torch.float32).contiguous()
+    if not prep.on_gpu:
+        _L.check(_L.load().mrnnt_cpu_backward(ctypes.byref(prep.problem), _ptr(ws), _ptr(grad_scale), _ptr(grads),
+                                              prep.num_threads), "mrnnt_cpu_backward")
+        return grads
+    with torch.cuda.device(prep.device):
         _L.check(_L.load().mrnnt_backward(ctypes.byref(prep.problem), _ptr(ws), _ptr(grad_scale), _ptr(grads),
                                           prep.stream()), "mrnnt_backward")
     return grads
@@ -156,19 +213,17 @@ class MonotonicRNNTFunction(torch.autograd.Function):
         need_grad = bool(ctx.needs_input_grad[0])
         costs, ws = _forward(prep, with_beta=need_grad)
         if need_grad:
-            # acts is re-read by the gradient kernel; saving it lets autograd catch in-place edits
-            ctx.save_for_backward(acts)
+            # acts is re-read by the gradient kernel (saving it lets autograd catch in-place edits); the workspace
+            # (den / lp / alpha / beta) is a saved tensor too, so autograd frees it after the last backward and
+            # keeps it for another one under retain_graph=True (the reference saves its grads, :92)
+            ctx.save_for_backward(acts, ws)
             ctx.prep = prep
-            ctx.ws = ws
         return costs
 
     @staticmethod
     def backward(ctx, grad_outputs):
-        (acts,) = ctx.saved_tensors
-        prep, ws = ctx.prep, ctx.ws
-        grads = _backward(prep, ws, grad_outputs)
-        ctx.prep = None
-        ctx.ws = None
+        _, ws = ctx.saved_tensors
+        grads = _backward(ctx.prep, ws, grad_outputs)
         return grads, None, None, None, None, None, None
 
 
@@ -178,9 +233,9 @@ def monotonic_rnnt_loss(acts: torch.Tensor, labels: torch.Tensor, input_lengths:
     """Computes the monotonic RNN-T loss between a sequence of activations and a ground truth labeling.
 
     Args (reference monotonic_rnnt_op.py:130-160):
-        acts:           packed 2-D float32 GPU tensor of logits, (sum_b T_b*(S_b+1), V), utterance b
+        acts:           packed 2-D float32 tensor of logits (GPU: HIP kernels; CPU: host implementation), (sum_b T_b*(S_b+1), V), utterance b
                         contiguous, then t-major, then s. Softmax is applied internally.
-                        Extensions: bfloat16 / float16 elements (fp32 math; grads in the same type), and
+                        Extensions (GPU): bfloat16 / float16 elements (fp32 math; grads in the same type), and
                         the padded 4-D joint-network layout [B, pad_T >= max T, pad_S1 >= max S + 1, V]
                         read in place (no packing copy; grads of padding rows are 0).
         labels:         2-D int tensor [B, max_b S_b] of padded label sequences.
@@ -218,42 +273,52 @@ class MonotonicRNNTLoss(torch.nn.Module):
 class _Ext:
     """The reference's pybind extension functions (monotonic_rnnt.cu:155-164), same argument order.
 
-    gpu_*: costs may live on any device (the reference takes a host tensor); grads [N, V] on the GPU
-    (an empty tensor = cost only). Return 0 (RNNT_STATUS_SUCCESS) or raise RuntimeError.
-    cpu_*: not available in this build (raises).
+    gpu_*: acts / labels / lengths on the GPU (the reference's TORCH_CHECKs, :85-88); costs may live on any
+    device (the reference takes a host tensor); grads [N, V] on the GPU, an empty tensor = cost only.
+    cpu_*: every tensor on the host (the reference's cpu_monotonic_rnnt, :16-77); num_threads > 0 sets the
+    thread count of the call. grads may also be acts itself (gradient written in place over the logits).
+    Return 0 (RNNT_STATUS_SUCCESS) or raise RuntimeError.
     """
 
     @staticmethod
-    def _run(acts, labels, input_lengths, label_lengths, alignment, k, costs, grads, blank_label):
-        prep = _Prepared(acts, labels, input_lengths, label_lengths, alignment, k, blank_label)
+    def _run(acts, labels, input_lengths, label_lengths, alignment, k, costs, grads, blank_label, num_threads,
+             want_gpu):
+        if acts.is_cuda != want_gpu or (want_gpu and not (labels.is_cuda and input_lengths.is_cuda
+                                                          and label_lengths.is_cuda)):
+            where = "GPU" if want_gpu else "CPU"
+            raise RuntimeError(f"{'gpu' if want_gpu else 'cpu'}_monotonic_rnnt: acts, labels and lengths must be "
+                               f"{where} tensors")
+        prep = _Prepared(acts, labels, input_lengths, label_lengths, alignment, k, blank_label, num_threads)
         want = grads is not None and grads.numel() > 0
-        c, ws = _forward(prep, with_beta=want)
         if want:
-            if not grads.is_cuda or grads.dtype != prep.acts.dtype or not grads.is_contiguous():
-                raise RuntimeError(f"grads must be a contiguous {prep.acts.dtype} GPU tensor")
+            if grads.device != prep.device or grads.dtype != prep.acts.dtype or not grads.is_contiguous():
+                raise RuntimeError(f"grads must be a contiguous {prep.acts.dtype} tensor on {prep.device}")
             if grads.shape != prep.acts.shape:
                 raise RuntimeError(f"grads must have the shape of acts {tuple(prep.acts.shape)}")
-            with torch.cuda.device(prep.device):
-                _L.check(_L.load().mrnnt_backward(ctypes.byref(prep.problem), _ptr(ws), None, _ptr(grads),
-                                                  prep.stream()), "mrnnt_backward")
+        c, ws = _forward(prep, with_beta=want)
+        if want:
+            _backward(prep, ws, None, grads)
         costs.copy_(c)
         return _L.RNNT_STATUS_SUCCESS
 
     def gpu_monotonic_rnnt(self, acts, labels, input_lengths, label_lengths, costs, grads, blank_label,
                            num_threads=0):
-        return self._run(acts, labels, input_lengths, label_lengths, None, 0, costs, grads, blank_label)
+        return self._run(acts, labels, input_lengths, label_lengths, None, 0, costs, grads, blank_label, 0, True)
 
     def gpu_monotonic_rnnt_align_restrict(self, acts, labels, input_lengths, label_lengths, alignment,
                                           max_distance_from_alignment, costs, grads, blank_label, num_threads=0):
         return self._run(acts, labels, input_lengths, label_lengths, alignment, max_distance_from_alignment,
-                         costs, grads, blank_label)
+                         costs, grads, blank_label, 0, True)
 
-    def cpu_monotonic_rnnt(self, *args, **kwargs):
-        raise RuntimeError("cpu_monotonic_rnnt: this is the MI355X (HIP) build; move tensors to the GPU")
+    def cpu_monotonic_rnnt(self, acts, labels, input_lengths, label_lengths, costs, grads, blank_label,
+                           num_threads=0):
+        return self._run(acts, labels, input_lengths, label_lengths, None, 0, costs, grads, blank_label,
+                         num_threads, False)
 
-    def cpu_monotonic_rnnt_align_restrict(self, *args, **kwargs):
-        raise RuntimeError("cpu_monotonic_rnnt_align_restrict: this is the MI355X (HIP) build; "
-                           "move tensors to the GPU")
+    def cpu_monotonic_rnnt_align_restrict(self, acts, labels, input_lengths, label_lengths, alignment,
+                                          max_distance_from_alignment, costs, grads, blank_label, num_threads=0):
+        return self._run(acts, labels, input_lengths, label_lengths, alignment, max_distance_from_alignment,
+                         costs, grads, blank_label, num_threads, False)
 
 
 monotonic_rnnt_cpp = _Ext()

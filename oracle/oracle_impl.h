@@ -65,8 +65,11 @@ static inline REAL SFX(den)(const SFX(utt_t) *u, int t, int s) { return u->denom
 static inline int SFX(maxi)(int a, int b) { return a > b ? a : b; }
 static inline int SFX(mini)(int a, int b) { return a < b ? a : b; }
 
-/* cpu_rnnt.h:98-115 -- per-row log-softmax denominator, sequential LSE over v (all rows). */
+/* cpu_rnnt.h:98-115 -- per-row log-softmax denominator, sequential LSE over v (all rows). Frames run in
+ * parallel when the utterance loop is not (one utterance per call): rows are independent, so this changes
+ * nothing but the wall time. */
 static void SFX(denoms)(SFX(utt_t) *u) {
+#pragma omp parallel for schedule(static)
     for (int t = 0; t < u->T; ++t) {
         for (int s = 0; s <= u->S; ++s) {
             REAL max_v = -(REAL)INFINITY;
@@ -113,9 +116,11 @@ static REAL SFX(betas)(SFX(utt_t) *u, int blank) {
     return SFX(get_beta)(u, 0, 0);
 }
 
-/* cpu_rnnt.h:216-236 -- gradient w.r.t. every logit of the utterance (out-of-band rows -> 0). */
+/* cpu_rnnt.h:216-236 -- gradient w.r.t. every logit of the utterance (out-of-band rows -> 0); frames in
+ * parallel as in denoms(). */
 static void SFX(grads)(const SFX(utt_t) *u, REAL ll, int blank, REAL *g) {
     const int T = u->T, S = u->S, V = u->V;
+#pragma omp parallel for schedule(static)
     for (int t = 0; t < T; ++t) {
         for (int s = 0; s <= S; ++s) {
             REAL a = SFX(get_alpha)(u, t - 1, s);
@@ -158,7 +163,9 @@ int SFX(mrnnt_oracle)(const float *acts, const int *labels, int64_t label_stride
     (void)num_threads;
 #endif
     int err = 0;
-#pragma omp parallel for schedule(dynamic, 1)
+    /* utterances in parallel; a single utterance instead parallelises its frames (the nested regions in
+     * denoms() / grads() are active only when this one is not) */
+#pragma omp parallel for schedule(dynamic, 1) if (B > 1)
     for (int b = 0; b < B; ++b) {
         const int Tb = T[b], Sb = S[b];
         const int64_t nrow = (int64_t)Tb * (Sb + 1);

@@ -43,7 +43,7 @@
 #undef SFX
 
 /* Counter-based synthetic generator, bit-identical to the device generator in
- * monotonic-rnnt_amd/csrc/synth.hip (integer hashing + one exact int->float conversion and one
+ * monotonic-rnnt_amd/devtools/mrnnt_devtools.hip (integer hashing + one exact int->float conversion and one
  * multiply, so no transcendental rounding can differ between host and device):
  *   h = SplitMix64(seed * K + index)
  *   uniform : U[0,1)   = (h >> 40) * 2^-24
@@ -56,6 +56,7 @@ static inline uint64_t mrnnt_splitmix(uint64_t x) {
 }
 
 void mrnnt_oracle_synth_acts(float *out, int64_t begin, int64_t count, uint64_t seed, int normal) {
+#pragma omp parallel for schedule(static) if (count > (1 << 22))
     for (int64_t i = 0; i < count; ++i) {
         uint64_t h = mrnnt_splitmix(seed * 0xD1B54A32D192ED03ull + (uint64_t)(begin + i));
         if (!normal) {

@@ -1,0 +1,20 @@
+"""bench.py's process-launch contract, checked without a GPU."""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_gpus_without_devices_fails_cleanly():
+    """`--gpus 2` over RCCL needs two visible GPUs; the launcher says so before any rank starts."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], capture_output=True,
+                       text=True, timeout=300, env=dict(os.environ, HIP_VISIBLE_DEVICES=""))
+    assert r.returncode == 2 and "needs 2 GPUs" in r.stderr
+
+
+def test_world_size_must_match_gpus():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1"], capture_output=True,
+                       text=True, timeout=300, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE=2 but --gpus 1" in r.stderr

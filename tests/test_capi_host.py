@@ -57,7 +57,16 @@ def test_library_exports_reference_cpp_classes(lib):
                    "GpuRNNTWorkspaceManager<float>::restrict_to_alignment(int const*, int, int)",
                    "GpuRNNTComputer<float>::cost_and_grad(float*, float*)",
                    "GpuRNNTComputer<float>::cost(float*)",
-                   "GpuRNNTComputer<float>::GpuRNNTComputer(GpuRNNTWorkspaceManager<float>&, int, ihipStream_t*)"]:
+                   "GpuRNNTComputer<float>::GpuRNNTComputer(GpuRNNTWorkspaceManager<float>&, int, ihipStream_t*)",
+                   "CpuRNNTWorkspaceManager<float>::CpuRNNTWorkspaceManager(float const*, int const*, int, int const*, int const*, int)",
+                   "CpuRNNTWorkspaceManager<float>::get_workspace_size(unsigned long*) const",
+                   "CpuRNNTWorkspaceManager<float>::set_workspace(void*)",
+                   "CpuRNNTWorkspaceManager<float>::create_workspace()",
+                   "CpuRNNTWorkspaceManager<float>::free_workspace()",
+                   "CpuRNNTWorkspaceManager<float>::restrict_to_alignment(int const*, int, int)",
+                   "CpuRNNTComputer<float>::cost_and_grad(float*, float*)",
+                   "CpuRNNTComputer<float>::cost(float*)",
+                   "CpuRNNTComputer<float>::CpuRNNTComputer(CpuRNNTWorkspaceManager<float>&, int, int)"]:
         assert method in exported, method
 
 
@@ -76,6 +85,7 @@ def _problem(T, S, V=8, blank=0, rows=-1):
     p = L.MrnntProblem()
     p.B, p.V, p.blank = len(T), V, blank
     p.T_host, p.S_host = T.ctypes.data, S.ctypes.data
+    p.label_stride = int(S.max(initial=0))
     p.num_rows = rows
     return p, (T, S)
 
@@ -115,14 +125,52 @@ def test_status_strings_match_reference_enum():
         assert re.search(rf"RNNT_STATUS_{name}\s*=\s*{val}", src)
 
 
-def test_torch_op_rejects_cpu_tensors():
+def test_torch_op_device_dispatch_checks():
+    """CPU tensors run the host implementation (tests/test_cpu_parity.py); the gpu_* extension functions keep
+    the reference's TORCH_CHECK that every input is a GPU tensor (monotonic_rnnt.cu:85-88)."""
     import torch
     import monotonic_rnnt_op as op
     acts = torch.zeros(12, 3)
+    lab, T, S = torch.tensor([[1, 2]], dtype=torch.int32), torch.tensor([4]), torch.tensor([2])
     with pytest.raises(RuntimeError, match="GPU"):
-        op.monotonic_rnnt_loss(acts, torch.tensor([[1, 2]], dtype=torch.int32), torch.tensor([4]), torch.tensor([2]))
-    with pytest.raises(RuntimeError):
+        op.monotonic_rnnt_cpp.gpu_monotonic_rnnt(acts, lab, T, S, torch.zeros(1), torch.zeros(0), 0, 0)
+    with pytest.raises(Exception):
         op.monotonic_rnnt_cpp.cpu_monotonic_rnnt(acts, None, None, None, None, None, 0, 0)
+    with pytest.raises(RuntimeError, match="float32"):
+        op.monotonic_rnnt_loss(acts.to(torch.bfloat16), lab, T, S)
+
+
+def test_product_library_has_no_development_hooks(lib):
+    """Launch knobs and bench helpers live in the development builds only (libmonotonic_rnnt_amd_dev.so,
+    libmrnnt_devtools.so); the product library exports neither."""
+    import _mrnnt_lib as L
+    exported = _exported()
+    for name in ("mrnnt_tune", "mrnnt_synth_acts", "mrnnt_copy_probe"):
+        assert not re.search(r"\s" + name + r"\b", exported), name
+    assert L.load_dev().mrnnt_tune(b"occ_skip", -1) == 1
+    assert L.devtools().mrnnt_synth_acts
+    with pytest.raises(RuntimeError, match="development build"):
+        L.tune("occ_skip")
+    with L.use(L.load_dev()):
+        assert L.tune("occ_skip") == 1
+
+
+def test_label_and_alignment_strides_validated(lib):
+    """A labels / alignment row narrower than max S / max T would make the kernels read past the row."""
+    import _mrnnt_lib as L
+    n = ctypes.c_size_t(0)
+    p, keep = _problem([4, 7], [2, 5])
+    p.label_stride = 4
+    assert lib.mrnnt_workspace_size(ctypes.byref(p), ctypes.byref(n)) == L.RNNT_STATUS_INVALID_VALUE
+    assert b"label row stride" in lib.mrnnt_last_error()
+    assert lib.mrnnt_cpu_workspace_size(ctypes.byref(p), ctypes.byref(n)) == L.RNNT_STATUS_INVALID_VALUE
+    p.label_stride = 5
+    al = np.zeros(2 * 6, np.int32)
+    p.alignment, p.align_stride = al.ctypes.data, 6
+    assert lib.mrnnt_workspace_size(ctypes.byref(p), ctypes.byref(n)) == L.RNNT_STATUS_INVALID_VALUE
+    assert b"alignment row stride" in lib.mrnnt_last_error()
+    p.align_stride = 7
+    assert lib.mrnnt_workspace_size(ctypes.byref(p), ctypes.byref(n)) == L.RNNT_STATUS_SUCCESS
 
 
 @pytest.mark.parametrize("cname,pyname", [("mrnnt_problem", "MrnntProblem"),
@@ -174,6 +222,7 @@ def test_joint_workspace_size_and_validation(lib):
     p.B, p.V, p.H, p.blank = 2, 64, 256, 0
     p.T_host, p.S_host = T.ctypes.data, S.ctypes.data
     p.enc_stride, p.pred_stride = 7 * 256, 6 * 256
+    p.label_stride = 5
     n = ctypes.c_size_t(0)
     assert lib.mrnnt_joint_workspace_size(ctypes.byref(p), ctypes.byref(n)) == L.RNNT_STATUS_SUCCESS
     assert n.value >= (4 * 3 + 7 * 6) * (4 + 4 * 8)

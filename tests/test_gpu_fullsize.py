@@ -29,8 +29,7 @@ def headline():
     rows_per = T * (S + 1)
     rows = B * rows_per
     acts = torch.empty((rows, V), dtype=torch.float32, device=dev)
-    L.check(L.load().mrnnt_synth_acts(ctypes.c_void_p(acts.data_ptr()), 0, rows * V, 0, 1,
-                                      ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)), "synth")
+    L.synth_acts(acts.data_ptr(), 0, rows * V, 0, 1, torch.cuda.current_stream().cuda_stream)
     labels_np = np.random.default_rng(1).integers(1, V, (B, S)).astype(np.int32)
     labels = torch.from_numpy(labels_np).to(dev)
     Tt = torch.full((B,), T, dtype=torch.int32)
@@ -137,8 +136,7 @@ def test_config_c5_large_vocab():
     rows = Bn * Tn * (Sn + 1)
     acts = torch.empty((rows, V), dtype=torch.float32, device=dev)
     import _mrnnt_lib as L
-    L.check(L.load().mrnnt_synth_acts(ctypes.c_void_p(acts.data_ptr()), 0, rows * V, 7, 1,
-                                      ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)), "synth")
+    L.synth_acts(acts.data_ptr(), 0, rows * V, 7, 1, torch.cuda.current_stream().cuda_stream)
     labels = np.random.default_rng(3).integers(1, V, (Bn, Sn)).astype(np.int32)
     c, g = _run(op, acts, labels, [Tn] * Bn, [Sn] * Bn, dev)
     assert np.all(np.isfinite(c))

@@ -13,6 +13,7 @@ import pytest
 import torch
 
 import oracle as O
+from _parity import knobs
 
 pytestmark = pytest.mark.gpu
 
@@ -26,12 +27,13 @@ T_EXTRA = int(os.environ.get("MRNNT_FUZZ_T_EXTRA", "40"))  # frames beyond the l
 @pytest.fixture(scope="module")
 def op():
     import monotonic_rnnt_op
-    import _mrnnt_lib as L
-    # long sweeps through another launch variant: MRNNT_FUZZ_TUNE="dp_halo=0,grad_variant=3"
-    for kv in filter(None, os.environ.get("MRNNT_FUZZ_TUNE", "").split(",")):
-        k, v = kv.split("=")
-        assert L.tune(k, int(v)) >= 0, k
-    return monotonic_rnnt_op
+    # long sweeps through another launch variant (development build): MRNNT_FUZZ_TUNE="dp_halo=0,grad_variant=3"
+    kv = dict(x.split("=") for x in filter(None, os.environ.get("MRNNT_FUZZ_TUNE", "").split(",")))
+    if not kv:
+        yield monotonic_rnnt_op
+        return
+    with knobs(**kv):
+        yield monotonic_rnnt_op
 
 
 @pytest.fixture(scope="module")
@@ -104,19 +106,12 @@ KNOB_SETS = [
 ]
 
 
-@pytest.mark.parametrize("knobs", range(len(KNOB_SETS)))
+@pytest.mark.parametrize("knob_set", range(len(KNOB_SETS)))
 @pytest.mark.parametrize("seed", range(1000, 1024))
-def test_random_case_other_kernels(op, dev, knobs, seed):
-    """The same sweep through the other launch variants (mrnnt_tune), 24 cases each."""
-    import _mrnnt_lib as L
-    saved = {k: L.tune(k) for k in KNOB_SETS[knobs]}
-    try:
-        for k, v in KNOB_SETS[knobs].items():
-            assert L.tune(k, v) >= 0, k
+def test_random_case_other_kernels(op, dev, knob_set, seed):
+    """The same sweep through the other launch variants (development build, mrnnt_tune), 24 cases each."""
+    with knobs(**KNOB_SETS[knob_set]):
         check_case(op, dev, make_case(seed))
-    finally:
-        for k, v in saved.items():
-            L.tune(k, v)
 
 
 @pytest.mark.parametrize("B,V,dtype", [(300, 16, "f32"), (1000, 33, "f32"), (257, 64, "bf16")])

@@ -18,6 +18,7 @@ import pytest
 import torch
 
 import oracle as O
+from _parity import knobs
 
 pytestmark = pytest.mark.gpu
 
@@ -25,12 +26,13 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture(scope="module")
 def jop():
     import monotonic_rnnt_joint
-    import _mrnnt_lib as L
-    # sweeps through another launch variant: MRNNT_FUZZ_TUNE="joint_nbuf=3,joint_reduce_sparse=2"
-    for kv in filter(None, os.environ.get("MRNNT_FUZZ_TUNE", "").split(",")):
-        k, v = kv.split("=")
-        assert L.tune(k, int(v)) >= 0, k
-    return monotonic_rnnt_joint
+    # sweeps through another launch variant (development build): MRNNT_FUZZ_TUNE="joint_nbuf=3,joint_reduce_sparse=2"
+    kv = dict(x.split("=") for x in filter(None, os.environ.get("MRNNT_FUZZ_TUNE", "").split(",")))
+    if not kv:
+        yield monotonic_rnnt_joint
+        return
+    with knobs(**kv):
+        yield monotonic_rnnt_joint
 
 
 @pytest.fixture(scope="module")

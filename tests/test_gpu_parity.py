@@ -13,6 +13,7 @@ import pytest
 import torch
 
 import oracle as O
+from _parity import knobs as knobs_ctx
 
 pytestmark = pytest.mark.gpu
 
@@ -279,8 +280,7 @@ def test_config_c2_vs_oracle(op, dev):
     labels = rng.integers(1, V, (B, Sn)).astype(np.int32)
     # the device generator must reproduce the host twin bit for bit (bench parity relies on it)
     d = torch.empty(rows * V, dtype=torch.float32, device=dev)
-    L.check(L.load().mrnnt_synth_acts(ctypes.c_void_p(d.data_ptr()), 0, rows * V, 0, 1,
-                                      ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)), "synth")
+    L.synth_acts(d.data_ptr(), 0, rows * V, 0, 1, torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     assert np.array_equal(d.cpu().numpy(), acts.reshape(-1))
     c, g = run_gpu(op, dev, acts, labels, T, S)
@@ -309,7 +309,7 @@ def test_accuracy_against_reference_fp32_noise(op, dev):
     assert ours[0] <= max(ref32[0], 1e-6) and ours[1] <= max(ref32[1], 1e-6), (ours, ref32)
 
 
-@pytest.mark.parametrize("knobs", [
+@pytest.mark.parametrize("knob_set", [
     {"softmax_variant": 0, "grad_variant": 0, "grid_per_cu": 8, "nt_store": 1},
     {"softmax_variant": 2, "grad_variant": 2, "grid_per_cu": 0, "nt_store": 0},
     {"softmax_variant": 0, "grad_variant": 0, "grid_per_cu": 3, "nt_store": 1},
@@ -330,14 +330,10 @@ def test_accuracy_against_reference_fp32_noise(op, dev):
     {"grad_variant": 5},
     {"grad_variant": 6, "grad_grid_per_cu": 3, "nt_load": 0, "nt_store": 0},
 ])
-def test_every_kernel_variant_matches_oracle(op, dev, knobs):
-    """All launch variants selectable through mrnnt_tune compute the same result (alignment included)."""
-    import _mrnnt_lib as L
-    saved = {k: L.tune(k) for k in ("softmax_variant", "grad_variant", "softmax_grid_per_cu",
-                                    "grad_grid_per_cu", "nt_store", "nt_load", "col_scatter", "dp_halo")}
-    try:
-        for k, v in knobs.items():
-            assert L.tune(k, v) >= 0
+def test_every_kernel_variant_matches_oracle(op, dev, knob_set):
+    """All launch variants selectable through mrnnt_tune (development build) compute the same result (alignment
+    included)."""
+    with knobs_ctx(**knob_set):
         rng = np.random.default_rng(77)
         for V, S_max, extra in ((1024, 40, 60), (260, 300, 60), (64, 12, 60), (32, 100, 200), (16, 200, 150)):
             acts, labels, T, S = random_problem(rng, 3, (S_max, S_max + extra), S_max, V, force={0: (S_max + extra, S_max)})
@@ -354,9 +350,6 @@ def test_every_kernel_variant_matches_oracle(op, dev, knobs):
             cr, gr = O.oracle_rnnt(acts, labels, T, S, alignment=al, max_shift=k)
             assert_costs(c, cr)
             assert_grads(g, gr)
-    finally:
-        for k, v in saved.items():
-            L.tune(k, v)
 
 
 @pytest.mark.parametrize("S_len,T_len,V", [(1100, 1200, 16), (64, 64, 8), (128, 300, 12), (511, 530, 8),
@@ -495,27 +488,22 @@ def test_occupancy_skip_is_bit_identical(op, dev, grad_variant):
     labels = rng.integers(1, V, (4, int(S.max()))).astype(np.int32)
     scale = np.array([1.0, -0.5, 2.0, 0.0], np.float32)
     n_band = int(np.sum((S.astype(np.int64) + 1) * (T - S + 1) - 1))
-    saved_skip, saved_var = L.tune("occ_skip"), L.tune("grad_variant")
-    try:
-        L.tune("grad_variant", grad_variant)
+    with knobs_ctx(grad_variant=grad_variant):
         out = {}
         for skip in (0, 1):
-            L.tune("occ_skip", skip)
-            out[skip] = run_gpu(op, dev, acts, labels, T, S, scale=scale)
-            live = _live_rows(op, dev, acts, labels, T, S)
-            if skip:
-                assert live < 0.9 * n_band, (live, n_band)
-            else:
-                assert live == n_band
+            with knobs_ctx(occ_skip=skip):
+                out[skip] = run_gpu(op, dev, acts, labels, T, S, scale=scale)
+                live = _live_rows(op, dev, acts, labels, T, S)
+                if skip:
+                    assert live < 0.9 * n_band, (live, n_band)
+                else:
+                    assert live == n_band
         assert np.array_equal(out[0][0], out[1][0])
         assert np.array_equal(out[0][1].view(np.uint32), out[1][1].view(np.uint32))  # signed zeros included
         cr, gr = O.oracle_rnnt(acts, labels, T, S, num_threads=4)
         gr = gr * np.repeat(scale.astype(np.float64), T * (S + 1))[:, None]
         assert_costs(out[1][0], cr)
         assert_grads(out[1][1], gr)
-    finally:
-        L.tune("occ_skip", saved_skip)
-        L.tune("grad_variant", saved_var)
 
 
 @pytest.mark.parametrize("grad_variant", [0, 5])
@@ -536,22 +524,17 @@ def test_alignment_window_with_and_without_occupancy_skip(op, dev, grad_variant)
         al[b, np.sort(rng.choice(T[b], S[b], replace=False))] = labels[b, : S[b]]
     scale = np.array([1.0, -2.0, 0.5], np.float32)
     k = 3
-    saved_skip, saved_var = L.tune("occ_skip"), L.tune("grad_variant")
-    try:
-        L.tune("grad_variant", grad_variant)
+    with knobs_ctx(grad_variant=grad_variant):
         out = {}
         for skip in (0, 1):
-            L.tune("occ_skip", skip)
-            out[skip] = run_gpu(op, dev, acts, labels, T, S, alignment=al, k=k, scale=scale)
+            with knobs_ctx(occ_skip=skip):
+                out[skip] = run_gpu(op, dev, acts, labels, T, S, alignment=al, k=k, scale=scale)
         assert np.array_equal(out[0][0], out[1][0])
         assert np.array_equal(out[0][1].view(np.uint32), out[1][1].view(np.uint32))
         cr, gr = O.oracle_rnnt(acts, labels, T, S, alignment=al, max_shift=k, num_threads=4)
         gr = gr * np.repeat(scale.astype(np.float64), T * (S + 1))[:, None]
         assert_costs(out[1][0], cr)
         assert_grads(out[1][1], gr)
-    finally:
-        L.tune("occ_skip", saved_skip)
-        L.tune("grad_variant", saved_var)
 
 
 @pytest.mark.parametrize("B,T,S,V", [(1, 150, 20, 50), (1, 150, 20, 5000), (16, 150, 20, 50), (16, 150, 20, 5000),

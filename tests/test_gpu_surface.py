@@ -1,0 +1,204 @@
+"""GPU tests of the round-2 surface items: per-row state read-out against the reference's own golden state,
+device-label safety, input validation, repeated backward, the HIP path against the library's CPU path, the
+configs[4] full-length utterance against the oracle, RCCL initialisation and the N-rank bench launcher."""
+import ctypes
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from _parity import FIXTURES, assert_costs, assert_grads, assert_state, random_problem, used_rows
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def op():
+    import monotonic_rnnt_op
+    return monotonic_rnnt_op
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    return torch.device("cuda:0")
+
+
+def _t(x, dev, dt=None):
+    t = torch.from_numpy(np.ascontiguousarray(x))
+    return t.to(dev) if dt is None else t.to(dev, dt)
+
+
+@pytest.mark.parametrize("path", FIXTURES, ids=[os.path.basename(p)[:-4] for p in FIXTURES])
+def test_golden_denominators_alpha_beta(op, dev, path):
+    """mrnnt_read_state after a forward against the reference's own get_denom / get_alpha / get_beta at double
+    precision (golden denom_f64 / alpha_f64 / beta_f64): the GPU's fp32 denominators and fp64 alpha / beta."""
+    import _mrnnt_lib as L
+    fx = dict(np.load(path))
+    al = None if "alignment" not in fx else _t(fx["alignment"], dev)
+    prep = op._Prepared(_t(fx["acts"], dev), _t(fx["labels"], dev), _t(fx["T"], dev), _t(fx["S"], dev), al,
+                        int(fx.get("max_shift", 0)), int(fx["blank"]))
+    _, ws = op._forward(prep, with_beta=True)
+    n = fx["acts"].shape[0]
+    den = torch.zeros(n, dtype=torch.float32, device=dev)
+    alpha = torch.zeros(n, dtype=torch.float64, device=dev)
+    beta = torch.zeros(n, dtype=torch.float64, device=dev)
+    L.check(L.load().mrnnt_read_state(ctypes.byref(prep.problem), ctypes.c_void_p(ws.data_ptr()),
+                                      ctypes.c_void_p(den.data_ptr()), ctypes.c_void_p(alpha.data_ptr()),
+                                      ctypes.c_void_p(beta.data_ptr()), prep.stream()), "read_state")
+    torch.cuda.synchronize()
+    assert_state(den.cpu().numpy(), alpha.cpu().numpy(), beta.cpu().numpy(), fx, window=used_rows(fx), rel=1e-4)
+
+
+@pytest.mark.parametrize("bad", [3, 7, -5, 1 << 30])
+def test_device_label_out_of_range_is_nan_not_a_fault(op, dev, bad):
+    """A device label outside [0, V) is not read back (no sync); the kernels read no logit with it and that
+    utterance's cost and gradient are NaN, the other utterances are exact (no write past the row)."""
+    rng = np.random.default_rng(abs(bad) % 97)
+    acts, labels, T, S = random_problem(rng, 3, (6, 14), 4, 3, force={0: (10, 3), 1: (9, 2), 2: (12, 4)})
+    labels = np.where(labels >= 3, 1, labels).astype(np.int32)
+    lab_bad = labels.copy()
+    lab_bad[1, 1] = bad
+    a = _t(acts, dev).requires_grad_(True)
+    costs = op.monotonic_rnnt_loss(a, _t(lab_bad, dev), _t(T, dev), _t(S, dev))
+    costs.sum().backward()
+    torch.cuda.synchronize()
+    c, g = costs.detach().cpu().numpy().astype(np.float64), a.grad.cpu().numpy()
+    assert np.isnan(c[1]) and np.isfinite(c[[0, 2]]).all()
+    cr, gr = O.oracle_rnnt(acts, labels, T, S)
+    r0, r1 = T[0] * (S[0] + 1), T[0] * (S[0] + 1) + T[1] * (S[1] + 1)
+    assert_costs(c[[0, 2]], cr[[0, 2]])
+    assert_grads(np.concatenate([g[:r0], g[r1:]]), np.concatenate([gr[:r0], gr[r1:]]))
+    assert not np.isfinite(g[r0:r1]).all()
+
+
+def test_host_labels_and_strides_validated(op, dev):
+    fx = dict(np.load(os.path.join(ROOT, "tests", "golden", "toy.npz")))
+    acts, T, S = _t(fx["acts"], dev), torch.from_numpy(fx["T"]), torch.from_numpy(fx["S"])
+    with pytest.raises(RuntimeError, match="outside"):
+        op.monotonic_rnnt_loss(acts, torch.tensor([[1, 3]], dtype=torch.int32), T, S)  # host labels, V = 3
+    with pytest.raises(RuntimeError, match="stride"):
+        op.monotonic_rnnt_loss(acts, torch.tensor([[1]], dtype=torch.int32, device=dev), T, S)
+    with pytest.raises(RuntimeError, match="stride"):
+        op.monotonic_rnnt_loss(acts, torch.tensor([[1, 2]], dtype=torch.int32, device=dev), T, S,
+                               torch.tensor([[0, 1, 0]], dtype=torch.int32, device=dev), 0)
+
+
+def test_backward_twice_with_retain_graph(op, dev):
+    rng = np.random.default_rng(3)
+    acts, labels, T, S = random_problem(rng, 3, (5, 40), 8, 64)
+    a = _t(acts, dev).requires_grad_(True)
+    costs = op.monotonic_rnnt_loss(a, _t(labels, dev), torch.from_numpy(T), torch.from_numpy(S))
+    (costs * 2).sum().backward(retain_graph=True)
+    g1 = a.grad.clone()
+    a.grad = None
+    (costs * 2).sum().backward()
+    assert torch.equal(a.grad, g1)
+    cr, gr = O.oracle_rnnt(acts, labels, T, S)
+    assert_grads(g1.cpu().numpy(), 2 * gr)
+
+
+def test_gpu_and_cpu_paths_agree(op, dev):
+    """The same inputs through the HIP kernels (GPU tensors) and the library's host implementation (CPU
+    tensors): both against the oracle, and against each other."""
+    rng = np.random.default_rng(21)
+    acts, labels, T, S = random_problem(rng, 6, (30, 160), 60, 300)
+    out = []
+    for d in (dev, torch.device("cpu")):
+        a = _t(acts, d).requires_grad_(True)
+        costs = op.monotonic_rnnt_loss(a, _t(labels, d), _t(T, d), _t(S, d))
+        costs.sum().backward()
+        out.append((costs.detach().cpu().numpy().astype(np.float64), a.grad.cpu().numpy()))
+    cr, gr = O.oracle_rnnt(acts, labels, T, S, num_threads=8)
+    for c, g in out:
+        assert_costs(c, cr)
+        assert_grads(g, gr)
+    assert_costs(out[0][0], out[1][0].astype(np.float64))
+    assert np.abs(out[0][1] - out[1][1]).max() <= 1e-4
+
+
+def test_configs4_full_utterance_vs_oracle(op, dev):
+    """configs[4] at full size for one utterance (T=1000, S=200, V=10000: 8 GB of logits) against the oracle on
+    every element: the large-vocabulary log-softmax and gradient at the benchmarked length."""
+    import _mrnnt_lib as L
+    T, S, V = 1000, 200, 10000
+    rows = T * (S + 1)
+    acts = torch.empty((rows, V), dtype=torch.float32, device=dev)
+    L.synth_acts(acts.data_ptr(), 0, rows * V, 0, True, torch.cuda.current_stream().cuda_stream)
+    labels = np.random.default_rng(1).integers(1, V, (1, S)).astype(np.int32)
+    acts.requires_grad_(True)
+    costs = op.monotonic_rnnt_loss(acts, _t(labels, dev), torch.tensor([T]), torch.tensor([S]))
+    costs.sum().backward()
+    torch.cuda.synchronize()
+    c = costs.detach().cpu().numpy().astype(np.float64)
+    g = acts.grad.cpu().numpy()
+    del acts
+    torch.cuda.empty_cache()
+    host = O.synth_acts(0, rows * V, seed=0).reshape(rows, V)
+    cr, gr = O.oracle_rnnt(host, labels, np.array([T]), np.array([S]), num_threads=16)
+    assert_costs(c, cr)
+    assert_grads(g, gr)
+
+
+def test_rccl_world1_sharded_loss(op, dev):
+    """torch.distributed over RCCL ("nccl" backend) at world size 1 on this GPU: shard_slice -> loss ->
+    allreduce_loss (the one collective of the path), checked against the oracle's summed cost."""
+    import torch.distributed as dist
+    from distributed import allreduce_loss, shard_slice
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
+    try:
+        assert dist.get_backend() == "nccl"
+        rng = np.random.default_rng(9)
+        acts, labels, T, S = random_problem(rng, 5, (20, 60), 10, 64)
+        a, lab, Ts, Ss, (lo, hi) = shard_slice(_t(acts, dev), _t(labels, dev), T, S, 0, 1)
+        assert (lo, hi) == (0, 5)
+        a = a.detach().requires_grad_(True)
+        costs = op.monotonic_rnnt_loss(a, lab, Ts, Ss)
+        tot = allreduce_loss(costs)
+        x = torch.ones(1, device=dev)
+        dist.all_reduce(x)  # an RCCL kernel really ran on this device
+        torch.cuda.synchronize()
+        assert float(x.item()) == 1.0
+        cr, _ = O.oracle_rnnt(acts, labels, T, S)
+        assert abs(float(tot.item()) - cr.sum()) <= 1e-4 * abs(cr.sum())
+    finally:
+        dist.destroy_process_group()
+
+
+def _bench(args, timeout=240):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                       timeout=timeout, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_launches_two_ranks():
+    """`bench.py --gpus 2` spawns two ranks itself (here both on this one GPU over gloo) and reports n_gpus 2 and
+    the whole-job batch."""
+    out = _bench(["--gpus", "2", "--dist-backend", "gloo", "--config", "c2", "--steps", "2", "--warmup", "1",
+                  "--no-cpu"])
+    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 32
+    assert out["scaling"] == "weak" and out["value"] > 0
+
+
+def test_bench_chunked_in_place_mode_matches_resident():
+    """The in-place / chunked memory modes (configs[3] at N <= 2, configs[4]) compute the same loss as the
+    resident autograd path on a small config forced into chunks by a tiny HBM budget."""
+    res = _bench(["--config", "c2", "--steps", "1", "--warmup", "1", "--no-cpu"])
+    chk = _bench(["--config", "c2", "--steps", "1", "--warmup", "1", "--no-cpu", "--hbm-budget-gb", "0.05"])
+    assert res["config"]["memory_mode"] == "resident" and chk["config"]["memory_mode"] == "inplace"
+    assert chk["config"]["chunks_per_step"] > 1
+    assert abs(res["loss_check"] - chk["loss_check"]) <= 1e-5 * abs(res["loss_check"])
+    assert res["roofline"]["live_rows"] == chk["roofline"]["live_rows"]
