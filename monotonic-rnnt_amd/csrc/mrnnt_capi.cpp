@@ -426,6 +426,11 @@ RNNTStatus make_joint_plan(const mrnnt_joint_problem *jp, JointPlan *jl) {
     const int H = jp->H;
     if (H != 128 && H != 256 && H != 384 && H != 512 && H != 640)
         return fail(RNNT_STATUS_INVALID_VALUE, "joint H must be 128, 256, 384, 512 or 640 (got " + std::to_string(H) + ")");
+    if (joint_min_lds_bytes(H, jp->V) > 160 * 1024)
+        return fail(RNNT_STATUS_INVALID_VALUE, "V = " + std::to_string(jp->V) + " is too large for the fused joint kernels at H = " +
+                                                   std::to_string(H) + " (weight tiles + bias need " +
+                                                   std::to_string(joint_min_lds_bytes(H, jp->V) / 1024) +
+                                                   " KiB of LDS, 160 KiB per CU); use the unfused loss");
     if (jp->enc_stride % 8 || jp->pred_stride % 8)
         return fail(RNNT_STATUS_INVALID_VALUE, "enc/pred utterance strides must be multiples of 8 elements");
     if (jp->hact_ld != 0 && (jp->hact_ld < H || jp->hact_ld % 8))

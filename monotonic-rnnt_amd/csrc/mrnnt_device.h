@@ -124,7 +124,9 @@ __device__ __forceinline__ void align_window(const DevProblem &p, int64_t c, int
 
 // Label of row s as the log-softmax kernels use it (has = s < S). Device labels are not range-checked on the
 // host (that would need a sync), so a label outside [0, V) reads no logit: it is returned as -1 (no capture)
-// and the row's label logit `ze` starts as NaN, so its lp -- hence the utterance's cost and gradient -- is NaN.
+// and the row's label logit `ze` starts as NaN: the transitions through that label carry NaN, which the
+// recursion turns into NaN or no probability, so the utterance's cost is not finite (NaN / +inf) and its
+// gradient non-finite.
 // A row without a label (s == S) returns -1 with ze = 0.
 __device__ __forceinline__ int checked_label(bool has, int l, int V, float &ze) {
     const bool bad = has && (unsigned)l >= (unsigned)V;
@@ -219,9 +221,11 @@ __device__ __forceinline__ double alpha_prev(const DevProblem &p, int t, int s, 
     return (t == 0) ? (s == 0 ? 0.0 : NEG_INF_D) : p.alpha[row - W];
 }
 
-// Value of a row whose gradient is not computed (out of band, or dead), times the upstream gradient: the
-// reference forms every row as exp(... - ll) (cpu_rnnt.h:221-231), i.e. 0 for a finite log-likelihood and NaN
-// for ll = -inf (no path survives, e.g. an alignment band that excludes them all) or NaN.
+// Value of a row whose gradient is not computed (out of band, or dead), times the upstream gradient: the CPU
+// reference -- the parity oracle -- forms every row as exp(... - ll) (cpu_rnnt.h:221-231), i.e. 0 for a finite
+// log-likelihood and NaN for ll = -inf (no path survives, e.g. an alignment band that excludes them all) or NaN.
+// The reference's GPU kernel writes a literal 0 to out-of-band rows instead (gpu_rnnt_kernel.h:266-271), so for
+// ll = -inf the two reference paths disagree on those rows; this build follows cpu_rnnt.h.
 __device__ __forceinline__ float zero_row_value(double ll, float sc) {
     return (ll > NEG_INF_D ? 0.0f : __builtin_nanf("")) * sc;
 }

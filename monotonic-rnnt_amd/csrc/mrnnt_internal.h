@@ -74,6 +74,8 @@ hipError_t launch_joint_backward(const DevProblem &p, const JointArgs &j, hipStr
 hipError_t launch_joint_reduce(const DevProblem &p, const JointArgs &j, const int64_t *off, int T_max, int S_max,
                                const unsigned short *dH, float *d_enc, float *d_pred, hipStream_t stream);
 hipError_t launch_zero(void *ptr, size_t bytes, hipStream_t stream);
+// LDS the fused joint kernels need at least (two weight-tile buffers + the bias row); at most 160 KiB per CU
+size_t joint_min_lds_bytes(int H, int V);
 
 // Launch-shape knobs (experiment hook: mrnnt_tune in mrnnt_capi.cpp). Defaults are the tuned values.
 struct Tuning {

@@ -60,11 +60,8 @@ __device__ __forceinline__ bool list_pred(const DevProblem &p, int mode, int t, 
 }
 
 template <bool WRITE>
-__global__ __launch_bounds__(256) void row_list_kernel(DevProblem p, int mode, int64_t *__restrict__ cnt,
-                                                       int *__restrict__ lcol, int *__restrict__ ls) {
-    const int lane = threadIdx.x & 63;
-    const int64_t col = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (col >= p.num_cols) return;
+__device__ __forceinline__ void row_list_column(const DevProblem &p, int mode, int64_t *__restrict__ cnt,
+                                                int *__restrict__ lcol, int *__restrict__ ls, int64_t col, int lane) {
     const int b = p.col_b[col];
     const int T = p.T[b], S = p.S[b], W = S + 1;
     const int t = (int)(col - p.col_off[b]);
@@ -87,6 +84,15 @@ __global__ __launch_bounds__(256) void row_list_kernel(DevProblem p, int mode, i
         n += __popcll(mask);
     }
     if (!WRITE && lane == 0) cnt[col] = n;
+}
+
+template <bool WRITE>
+__global__ __launch_bounds__(256) void row_list_kernel(DevProblem p, int mode, int64_t *__restrict__ cnt,
+                                                       int *__restrict__ lcol, int *__restrict__ ls) {
+    const int lane = threadIdx.x & 63;
+    // grid-stride over lattice columns (one per wave): the grid is capped, any number of columns works
+    for (int64_t col = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); col < p.num_cols; col += (int64_t)gridDim.x * 4)
+        row_list_column<WRITE>(p, mode, cnt, lcol, ls, col, lane);
 }
 
 // exclusive scan of a[0..n) in place, a[n] = total (one workgroup; n = lattice columns)
@@ -120,7 +126,7 @@ __global__ __launch_bounds__(1024) void scan_kernel(int64_t *__restrict__ a, int
 
 hipError_t launch_row_list(const DevProblem &p, int mode, int64_t *col_cnt, int *lcol, int *ls,
                            unsigned long long *total, hipStream_t stream) {
-    const int64_t blocks = (p.num_cols + 3) / 4;
+    const int64_t blocks = std::min<int64_t>((p.num_cols + 3) / 4, 1 << 20);
     row_list_kernel<false><<<(int)blocks, 256, 0, stream>>>(p, mode, col_cnt, lcol, ls);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -660,6 +666,7 @@ hipError_t launch_joint_reduce(const DevProblem &p, const JointArgs &j, const in
         const size_t lds = sizeof(float) * ((size_t)W * HS + 256 / (HS / 4) * HS);
         joint_reduce_kernel<HS><<<p.B * ntb * (j.H / HS), 256, lds, stream>>>(p, j, off, dH, d_enc, d_pred, ntb);
     };
+    if ((int64_t)p.B * ntb * (j.H / 4) > (1ll << 24)) return hipErrorInvalidValue;  // 32-bit dispatch size
     // LDS = W * HS + 4 KiB of fp32: about 30 KiB at the headline (several workgroups per CU), <= 64 KiB always
     if (W <= 448) go(std::integral_constant<int, 32>());
     else if (W <= 896) go(std::integral_constant<int, 16>());
@@ -671,6 +678,7 @@ hipError_t launch_joint_reduce(const DevProblem &p, const JointArgs &j, const in
 template <int KS, int NB, int NW>
 static hipError_t launch_knw(const DevProblem &p, const JointArgs &j, bool bwd, size_t lds, hipStream_t stream) {
     const int64_t blocks = (j.n + 32 * NW - 1) / (32 * NW);
+    if (blocks * 64 * NW > 0xffffffffll) return hipErrorInvalidValue;  // 32-bit dispatch size in work-items
     auto kern = bwd ? joint_bwd_kernel<KS, NB, NW> : joint_fwd_kernel<KS, NB, NW>;
     if (lds > 65536) {
         const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
@@ -691,6 +699,10 @@ static hipError_t launch_kh(const DevProblem &p, const JointArgs &j, bool bwd, h
         return launch_knw<KS, 3, 8>(p, j, bwd, 3 * tile + bias, stream);
     if (2 * tile + bias <= 160 * 1024) return launch_knw<KS, 2, 8>(p, j, bwd, 2 * tile + bias, stream);
     return hipErrorInvalidValue;
+}
+
+size_t joint_min_lds_bytes(int H, int V) {
+    return 2 * sizeof(unsigned short) * 32 * (size_t)H + sizeof(float) * (((size_t)V + 31) / 32 * 32);
 }
 
 static hipError_t launch_joint(const DevProblem &p, const JointArgs &j, bool bwd, hipStream_t stream) {

@@ -30,10 +30,10 @@ import torch
 
 try:
     from . import _mrnnt_lib as _L
-    from .monotonic_rnnt_op import _lengths_on_device
+    from .monotonic_rnnt_op import _check_labels, _lengths
 except ImportError:
     import _mrnnt_lib as _L
-    from monotonic_rnnt_op import _lengths_on_device
+    from monotonic_rnnt_op import _check_labels, _lengths
 
 _L.load()
 
@@ -66,20 +66,22 @@ class _JointPrepared:
         self.pred = pred.contiguous()
         self.weight = weight.contiguous()
         self.bias = None if bias is None else bias.detach().to(dev, torch.float32).contiguous()
-        self.T_host = np.ascontiguousarray(input_lengths.detach().to("cpu", torch.int32).numpy()).reshape(-1)
-        self.S_host = np.ascontiguousarray(label_lengths.detach().to("cpu", torch.int32).numpy()).reshape(-1)
+        ln = _lengths(input_lengths, label_lengths)
+        self.T_host, self.S_host = ln.T, ln.S
         if self.T_host.size != B or self.S_host.size != B:
             raise RuntimeError(f"monotonic_rnnt_joint: expected {B} input/label lengths")
         if B and (self.T_host.max() > enc.size(1) or self.S_host.max() + 1 > pred.size(1)):
             raise RuntimeError("monotonic_rnnt_joint: enc/pred have fewer frames/label positions than the lengths")
-        self.T_dev, self.S_dev = _lengths_on_device(input_lengths, label_lengths, self.T_host, self.S_host, dev)
+        self.T_dev, self.S_dev = ln.on(dev)
+        if not labels.is_cuda:
+            _check_labels(labels, self.S_host, V)
         lab = labels.detach().to(dev, torch.int32)
         if lab.dim() == 1:
             lab = lab.view(B, -1)
         self.labels = lab.contiguous() if lab.numel() else torch.zeros(B, 1, dtype=torch.int32, device=dev)
         p = _L.MrnntJointProblem()
         p.B, p.V, p.H, p.blank = B, V, H, int(blank_label)
-        p.T_host, p.S_host = self.T_host.ctypes.data, self.S_host.ctypes.data
+        p.T_host, p.S_host = ln.T_ptr, ln.S_ptr
         p.T_dev, p.S_dev = self.T_dev.data_ptr(), self.S_dev.data_ptr()
         p.labels, p.label_stride = self.labels.data_ptr(), self.labels.size(1)
         p.enc, p.enc_stride = self.enc.data_ptr(), self.enc.size(1) * H
@@ -179,19 +181,19 @@ class MonotonicRNNTJointFunction(torch.autograd.Function):
         need = any(ctx.needs_input_grad[:4])
         costs, ws = prep.forward(with_beta=need)
         if need:
-            ctx.save_for_backward(enc, pred, weight)
-            ctx.prep, ctx.ws = prep, ws
+            # the workspace is a saved tensor: freed after the last backward, kept under retain_graph=True
+            ctx.save_for_backward(enc, pred, weight, ws)
+            ctx.prep = prep
             ctx.bias_dtype = None if bias is None else bias.dtype
         return costs
 
     @staticmethod
     def backward(ctx, grad_costs):
-        prep, ws = ctx.prep, ctx.ws
+        prep, ws = ctx.prep, ctx.saved_tensors[3]
         need_b = ctx.bias_dtype is not None and ctx.needs_input_grad[3]
         # dbias rides on the dweight GEMM (a ones column in Hact); MRNNT_JOINT_BIAS_SUM=1: a separate G.sum (A/B)
         bias_col = need_b and ctx.needs_input_grad[2] and not _BIAS_SUM and prep.H in _HACT_LD
         G, Hact = prep.backward_rows(ws, grad_costs, bias_column=bias_col)
-        ctx.prep = ctx.ws = None
         d_enc = d_pred = d_w = d_b = None
         H = prep.H
         if ctx.needs_input_grad[2]:

@@ -29,6 +29,7 @@ Extensions beyond the reference: bf16/fp16 acts (costs
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 from typing import Optional
 
@@ -51,27 +52,37 @@ def _ptr(t: Optional[torch.Tensor]):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
-# Host lengths go up once per distinct (T, S) content and device: training loops repeat a handful of shapes, so
-# the pinned staging copy and its H2D transfer are paid once, not per call. Entries are never written after
-# creation (the kernels only read them).
+class _Lengths:
+    """int32 host copies of one (T, S) pair (the plan needs them on the host), their device copies per device,
+    and the workspace sizes of that shape. Cached by content: training loops repeat shapes, so the conversions,
+    the pinned staging copy and its H2D transfer are paid once per distinct shape, not per call. Entries are
+    never written after creation (the kernels only read them)."""
+
+    __slots__ = ("T", "S", "T_ptr", "S_ptr", "dev", "ws")
+
+    def __init__(self, T: np.ndarray, S: np.ndarray):
+        self.T, self.S = T, S
+        self.T_ptr, self.S_ptr = T.ctypes.data, S.ctypes.data
+        self.dev = {}
+        self.ws = {}
+
+    def on(self, dev: torch.device):
+        """Device copies, uploaded once as one pinned non-blocking copy on the current stream (no host wait); a
+        call on another stream waits for that upload through an event."""
+        hit = self.dev.get(dev)
+        stream = torch.cuda.current_stream(dev)
+        if hit is None:
+            ts = torch.from_numpy(np.stack([self.T, self.S])).pin_memory().to(dev, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            hit = self.dev[dev] = (ts[0], ts[1], ev, stream)
+        elif hit[3] != stream:
+            stream.wait_event(hit[2])
+        return hit[0], hit[1]
+
+
 _LEN_CACHE: "dict" = {}
 _LEN_CACHE_MAX = 64
-
-
-def _lengths_on_device(input_lengths, label_lengths, T_host, S_host, dev):
-    """Device int32 copies of the lengths: device inputs are converted in place on the GPU; host inputs go up
-    as one pinned, non-blocking copy (stream-ordered before the kernels, no host wait), cached by content."""
-    if input_lengths.is_cuda or label_lengths.is_cuda:
-        return (input_lengths.detach().to(dev, torch.int32).contiguous().view(-1),
-                label_lengths.detach().to(dev, torch.int32).contiguous().view(-1))
-    key = (dev, T_host.tobytes(), S_host.tobytes())
-    hit = _LEN_CACHE.get(key)
-    if hit is None:
-        ts = torch.from_numpy(np.stack([T_host, S_host])).pin_memory().to(dev, non_blocking=True)
-        if len(_LEN_CACHE) >= _LEN_CACHE_MAX:
-            _LEN_CACHE.pop(next(iter(_LEN_CACHE)))
-        hit = _LEN_CACHE[key] = (ts[0], ts[1])
-    return hit
 
 
 def _host_int32(t: torch.Tensor) -> np.ndarray:
@@ -79,6 +90,23 @@ def _host_int32(t: torch.Tensor) -> np.ndarray:
     if t.is_cuda:
         t = t.cpu()  # a sync, as the reference's cudaMemcpy of the lengths (gpu_workspace_manager.h:87-96)
     return np.ascontiguousarray(t.numpy() if t.dtype == torch.int32 else t.to(torch.int32).numpy()).reshape(-1)
+
+
+def _content(t: torch.Tensor) -> bytes:
+    if not t.is_cuda and t.dtype == torch.int32 and t.is_contiguous():
+        return ctypes.string_at(t.data_ptr(), t.numel() * 4)  # no numpy round trip for the common case
+    return _host_int32(t).tobytes()
+
+
+def _lengths(input_lengths: torch.Tensor, label_lengths: torch.Tensor) -> _Lengths:
+    key = (_content(input_lengths), _content(label_lengths))
+    hit = _LEN_CACHE.get(key)
+    if hit is None:
+        hit = _Lengths(np.frombuffer(key[0], np.int32).copy(), np.frombuffer(key[1], np.int32).copy())
+        if len(_LEN_CACHE) >= _LEN_CACHE_MAX:
+            _LEN_CACHE.pop(next(iter(_LEN_CACHE)))
+        _LEN_CACHE[key] = hit
+    return hit
 
 
 class _Prepared:
@@ -102,17 +130,19 @@ class _Prepared:
         self.acts = acts.contiguous()
         self.num_threads = int(num_threads)
         B = labels.size(0)
-        self.T_host = _host_int32(input_lengths)
-        self.S_host = _host_int32(label_lengths)
+        self.lengths = ln = _lengths(input_lengths, label_lengths)
+        self.T_host, self.S_host = ln.T, ln.S
         if self.T_host.size != B or self.S_host.size != B:
             raise RuntimeError(f"monotonic_rnnt: expected {B} input/label lengths, "
                                f"got {self.T_host.size}/{self.S_host.size}")
-        lab = labels.detach().to(dev, torch.int32)
+        lab = labels.detach()
+        if lab.device != dev or lab.dtype != torch.int32:
+            lab = lab.to(dev, torch.int32)
         if lab.dim() == 1:
             lab = lab.view(B, -1)
         self.labels = lab.contiguous() if lab.numel() else torch.zeros(B, 1, dtype=torch.int32, device=dev)
         if self.on_gpu:
-            self.T_dev, self.S_dev = _lengths_on_device(input_lengths, label_lengths, self.T_host, self.S_host, dev)
+            self.T_dev, self.S_dev = ln.on(dev)
             if not labels.is_cuda:
                 _check_labels(labels, self.S_host, acts.size(-1))
         self.alignment = None
@@ -124,8 +154,8 @@ class _Prepared:
         p.V = self.acts.size(-1)
         p.blank = int(blank_label)
         p.max_shift = int(max_shift)
-        p.T_host = self.T_host.ctypes.data
-        p.S_host = self.S_host.ctypes.data
+        p.T_host = ln.T_ptr
+        p.S_host = ln.S_ptr
         if self.on_gpu:
             p.T_dev = self.T_dev.data_ptr()
             p.S_dev = self.S_dev.data_ptr()
@@ -147,10 +177,14 @@ class _Prepared:
         self.device = dev
 
     def workspace(self) -> torch.Tensor:
-        n = ctypes.c_size_t(0)
-        fn = _L.load().mrnnt_workspace_size if self.on_gpu else _L.load().mrnnt_cpu_workspace_size
-        _L.check(fn(ctypes.byref(self.problem), ctypes.byref(n)), "workspace_size")
-        return torch.empty(max(1, n.value), dtype=torch.uint8, device=self.device)
+        key = (self.on_gpu, self.alignment is not None, _L.load())
+        n = self.lengths.ws.get(key)  # a function of the lengths and the alignment flag only
+        if n is None:
+            c = ctypes.c_size_t(0)
+            fn = _L.load().mrnnt_workspace_size if self.on_gpu else _L.load().mrnnt_cpu_workspace_size
+            _L.check(fn(ctypes.byref(self.problem), ctypes.byref(c)), "workspace_size")
+            n = self.lengths.ws[key] = max(1, c.value)
+        return torch.empty(n, dtype=torch.uint8, device=self.device)
 
     def stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
@@ -158,7 +192,7 @@ class _Prepared:
 
 def _check_labels(labels: torch.Tensor, S_host: np.ndarray, V: int) -> None:
     """Host labels: every label inside the lattice (s < S_b) must be in [0, V). (Device labels are not read back;
-    the kernels never index past a row with them, and an out-of-range label yields a NaN cost.)"""
+    the kernels never index past a row with them, and an out-of-range label yields a non-finite cost.)"""
     lab = labels.detach().to(torch.int32).numpy()
     lab = lab.reshape(len(S_host), -1) if lab.size else lab.reshape(len(S_host), 0)
     if lab.shape[1] < int(S_host.max(initial=0)):
@@ -171,6 +205,14 @@ def _check_labels(labels: torch.Tensor, S_host: np.ndarray, V: int) -> None:
                             f"label {int(lab[b, s])} at ({b}, {s}) outside [0, V = {V})")
 
 
+_NULL_CTX = contextlib.nullcontext()
+
+
+def _on_device(dev: torch.device):
+    """torch.cuda.device(dev) only when dev is not already current (the context manager costs microseconds)."""
+    return _NULL_CTX if torch.cuda.current_device() == dev.index else torch.cuda.device(dev)
+
+
 def _forward(prep: _Prepared, with_beta: bool):
     lib = _L.load()
     ws = prep.workspace()
@@ -179,7 +221,7 @@ def _forward(prep: _Prepared, with_beta: bool):
         _L.check(lib.mrnnt_cpu_forward(ctypes.byref(prep.problem), _ptr(ws), ws.numel(), _ptr(costs),
                                        1 if with_beta else 0, prep.num_threads), "mrnnt_cpu_forward")
         return costs, ws
-    with torch.cuda.device(prep.device):  # kernels go to this device's current stream
+    with _on_device(prep.device):  # kernels go to this device's current stream
         _L.check(lib.mrnnt_forward(ctypes.byref(prep.problem), _ptr(ws), ws.numel(), _ptr(costs),
                                    1 if with_beta else 0, prep.stream()), "mrnnt_forward")
     return costs, ws
@@ -195,7 +237,7 @@ def _backward(prep: _Prepared, ws: torch.Tensor, grad_scale: Optional[torch.Tens
         _L.check(_L.load().mrnnt_cpu_backward(ctypes.byref(prep.problem), _ptr(ws), _ptr(grad_scale), _ptr(grads),
                                               prep.num_threads), "mrnnt_cpu_backward")
         return grads
-    with torch.cuda.device(prep.device):
+    with _on_device(prep.device):
         _L.check(_L.load().mrnnt_backward(ctypes.byref(prep.problem), _ptr(ws), _ptr(grad_scale), _ptr(grads),
                                           prep.stream()), "mrnnt_backward")
     return grads
@@ -273,8 +315,9 @@ class MonotonicRNNTLoss(torch.nn.Module):
 class _Ext:
     """The reference's pybind extension functions (monotonic_rnnt.cu:155-164), same argument order.
 
-    gpu_*: acts / labels / lengths on the GPU (the reference's TORCH_CHECKs, :85-88); costs may live on any
-    device (the reference takes a host tensor); grads [N, V] on the GPU, an empty tensor = cost only.
+    gpu_*: acts on the GPU (the reference's TORCH_CHECK, :85; labels / lengths may be host or device tensors,
+    the reference requires device ones); costs may live on any device (the reference takes a host tensor);
+    grads [N, V] on the GPU, an empty tensor = cost only.
     cpu_*: every tensor on the host (the reference's cpu_monotonic_rnnt, :16-77); num_threads > 0 sets the
     thread count of the call. grads may also be acts itself (gradient written in place over the logits).
     Return 0 (RNNT_STATUS_SUCCESS) or raise RuntimeError.
@@ -283,11 +326,9 @@ class _Ext:
     @staticmethod
     def _run(acts, labels, input_lengths, label_lengths, alignment, k, costs, grads, blank_label, num_threads,
              want_gpu):
-        if acts.is_cuda != want_gpu or (want_gpu and not (labels.is_cuda and input_lengths.is_cuda
-                                                          and label_lengths.is_cuda)):
-            where = "GPU" if want_gpu else "CPU"
-            raise RuntimeError(f"{'gpu' if want_gpu else 'cpu'}_monotonic_rnnt: acts, labels and lengths must be "
-                               f"{where} tensors")
+        if acts.is_cuda != want_gpu:  # labels / lengths may live on either device (copied as needed)
+            raise RuntimeError(f"{'gpu' if want_gpu else 'cpu'}_monotonic_rnnt: acts must be a "
+                               f"{'GPU' if want_gpu else 'CPU'} tensor")
         prep = _Prepared(acts, labels, input_lengths, label_lengths, alignment, k, blank_label, num_threads)
         want = grads is not None and grads.numel() > 0
         if want:
