@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MRNNT_VERSION 3
+#define MRNNT_VERSION 4
 
 /* acts / grads element types */
 #define MRNNT_F32 0
@@ -58,11 +58,22 @@ typedef struct mrnnt_problem {
     int acts_dtype;          /* MRNNT_F32 / MRNNT_BF16 / MRNNT_F16 */
     int64_t pad_T;           /* padded layout: frames per utterance slot (>= max T_b) */
     int64_t pad_S1;          /* padded layout: label positions per frame (>= max S_b + 1); 0 = packed */
+    /* --- version 4 --- */
+    const void *lattice;     /* optional: device copy of mrnnt_lattice_host's output for these lengths. The lattice
+                                offsets then come from it and mrnnt_forward launches no setup kernel (a caller that
+                                repeats shapes uploads it once); NULL = built on the device in every forward */
 } mrnnt_problem;
 
 /* Validate lengths (reference semantics: B > 0, V > 0, T_b > 0, S_b >= 0, T_b >= S_b) and return the
  * device workspace bytes needed by mrnnt_forward / mrnnt_backward for this problem. Host-only. */
 RNNTStatus mrnnt_workspace_size(const mrnnt_problem *p, size_t *bytes);
+
+/* Lattice offsets of the problem's lengths, computed on the host from T_host / S_host: int64 row_off[B+1]
+ * (first lattice row of each utterance), int64 col_off[B+1] (first column), int32 col_b[sum_b T_b] (utterance
+ * of each column). mrnnt_lattice_bytes gives the size; mrnnt_lattice_host fills `host` (>= that many bytes).
+ * Upload it to device memory and pass it as mrnnt_problem.lattice. Host-only. */
+RNNTStatus mrnnt_lattice_bytes(const mrnnt_problem *p, size_t *bytes);
+RNNTStatus mrnnt_lattice_host(const mrnnt_problem *p, void *host, size_t bytes);
 
 /* Forward: log-softmax row reduce + alpha (and, if with_beta, beta) recursion.
  * Writes costs_dev[b] = -log p(labels_b | acts_b) (device fp32, may be NULL) and keeps the per-row

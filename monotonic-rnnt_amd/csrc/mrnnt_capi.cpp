@@ -153,9 +153,16 @@ DevProblem make_dev(const mrnnt_problem *p, const Plan &pl, const void *ws) {
     d.label_stride = p->label_stride;
     d.T = p->T_dev;
     d.S = p->S_dev;
-    d.row_off = reinterpret_cast<const int64_t *>(w + pl.off_row);
-    d.col_off = reinterpret_cast<const int64_t *>(w + pl.off_col);
-    d.col_b = reinterpret_cast<const int *>(w + pl.off_colb);
+    if (p->lattice) {  // caller-provided lattice offsets (mrnnt_lattice_host layout)
+        const int64_t *lat = static_cast<const int64_t *>(p->lattice);
+        d.row_off = lat;
+        d.col_off = lat + pl.B + 1;
+        d.col_b = reinterpret_cast<const int *>(lat + 2 * (pl.B + 1));
+    } else {
+        d.row_off = reinterpret_cast<const int64_t *>(w + pl.off_row);
+        d.col_off = reinterpret_cast<const int64_t *>(w + pl.off_col);
+        d.col_b = reinterpret_cast<const int *>(w + pl.off_colb);
+    }
     d.min_s = pl.align ? reinterpret_cast<const int *>(w + pl.off_min) : nullptr;
     d.max_s = pl.align ? reinterpret_cast<const int *>(w + pl.off_max) : nullptr;
     d.B = pl.B;
@@ -274,6 +281,36 @@ RNNTStatus mrnnt_workspace_size(const mrnnt_problem *p, size_t *bytes) {
     return RNNT_STATUS_SUCCESS;
 }
 
+RNNTStatus mrnnt_lattice_bytes(const mrnnt_problem *p, size_t *bytes) {
+    // needs only B, T_host and S_host
+    if (!bytes || !p) return fail(RNNT_STATUS_INVALID_VALUE, "null argument");
+    if (p->B <= 0 || !p->T_host || !p->S_host) return fail(RNNT_STATUS_INVALID_VALUE, "B > 0 and host lengths required");
+    int64_t cols = 0;
+    for (int b = 0; b < p->B; ++b) {
+        if (p->T_host[b] <= 0 || p->S_host[b] < 0 || p->T_host[b] < p->S_host[b])
+            return fail(RNNT_STATUS_INVALID_VALUE, "invalid lengths at utterance " + std::to_string(b));
+        cols += p->T_host[b];
+    }
+    *bytes = sizeof(int64_t) * 2 * ((size_t)p->B + 1) + sizeof(int) * (size_t)cols;
+    return RNNT_STATUS_SUCCESS;
+}
+
+RNNTStatus mrnnt_lattice_host(const mrnnt_problem *p, void *host, size_t bytes) {
+    size_t need = 0;
+    const RNNTStatus st = mrnnt_lattice_bytes(p, &need);
+    if (st != RNNT_STATUS_SUCCESS) return st;
+    if (!host || bytes < need) return fail(RNNT_STATUS_INVALID_VALUE, "lattice buffer too small: need " + std::to_string(need));
+    int64_t *row = static_cast<int64_t *>(host), *col = row + p->B + 1;
+    int *col_b = reinterpret_cast<int *>(col + p->B + 1);
+    row[0] = col[0] = 0;
+    for (int b = 0; b < p->B; ++b) {
+        row[b + 1] = row[b] + (int64_t)p->T_host[b] * (p->S_host[b] + 1);
+        col[b + 1] = col[b] + p->T_host[b];
+        for (int64_t c = col[b]; c < col[b + 1]; ++c) col_b[c] = b;
+    }
+    return RNNT_STATUS_SUCCESS;
+}
+
 RNNTStatus mrnnt_forward(const mrnnt_problem *p, void *ws, size_t ws_bytes, float *costs_dev, int with_beta,
                          hipStream_t stream) {
     Plan pl;
@@ -284,13 +321,15 @@ RNNTStatus mrnnt_forward(const mrnnt_problem *p, void *ws, size_t ws_bytes, floa
         return fail(RNNT_STATUS_INVALID_VALUE, "workspace too small: need " + std::to_string(pl.total) + " bytes");
     DevProblem d = make_dev(p, pl, ws);
     char *w = static_cast<char *>(ws);
-    hipError_t e;
-    e = timed(K_SETUP, stream, [&] {
-        return launch_setup(p->T_dev, p->S_dev, pl.B, reinterpret_cast<int64_t *>(w + pl.off_row),
-                            reinterpret_cast<int64_t *>(w + pl.off_col),
-                            reinterpret_cast<int *>(w + pl.off_colb), d.lpb, d.lpe, pl.N, stream);
-    });
-    if (e != hipSuccess) return fail_hip(e, "setup kernel");
+    hipError_t e = hipSuccess;
+    if (!p->lattice) {  // lattice offsets on the device (the log-softmax kernel zeroes the lp pads itself)
+        e = timed(K_SETUP, stream, [&] {
+            return launch_setup(p->T_dev, p->S_dev, pl.B, reinterpret_cast<int64_t *>(w + pl.off_row),
+                                reinterpret_cast<int64_t *>(w + pl.off_col),
+                                reinterpret_cast<int *>(w + pl.off_colb), nullptr, nullptr, 0, stream);
+        });
+        if (e != hipSuccess) return fail_hip(e, "setup kernel");
+    }
     if (pl.align) {
         e = timed(K_BAND, stream, [&] {
             return launch_align(d, p->alignment, p->align_stride, p->align_blank, p->max_shift,

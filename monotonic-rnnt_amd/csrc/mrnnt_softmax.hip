@@ -25,10 +25,24 @@ __device__ __forceinline__ void zero_fill_outside_band(const DevProblem &p, int6
         }
 }
 
+// The 64 lp entries either side of [0, N): the recursion's in-band cell s = 0 of utterance 0 adds lpe[-1] to its
+// -inf predecessor, and a NaN / +inf left in the (reused) workspace there would turn alpha(0, 0) into NaN (then
+// -inf through fmax in the next LSE: an infinite cost). Zeroed by the first workgroup of every log-softmax launch.
+__device__ __forceinline__ void zero_lp_pads(const DevProblem &p) {
+    if (blockIdx.x == 0 && threadIdx.x < 64) {
+        const int i = threadIdx.x;
+        p.lpb[i - 64] = 0.0;
+        p.lpe[i - 64] = 0.0;
+        p.lpb[p.num_rows + i] = 0.0;
+        p.lpe[p.num_rows + i] = 0.0;
+    }
+}
+
 // Vector path: V % E == 0, 16-byte aligned rows. U = vector loads per lane per chunk (a chunk covers
 // 64*U*E elements), R = rows a wave reduces at once (U*R vector loads in flight per lane).
 template <class IO, int U, int R, bool NTL>
 __global__ __launch_bounds__(256) void softmax_kernel(DevProblem p) {
+    zero_lp_pads(p);
     constexpr int NW = 4;
     constexpr int E = IO::E;
     typedef typename IO::V Vec;
@@ -132,6 +146,7 @@ __device__ __forceinline__ float lane_pick(const float (&x)[N], int k) {
 // (one fp64 log per R rows). FULL: V is a multiple of 64*U*E (no per-load bounds checks).
 template <class IO, int U, int R, bool NTL, bool FULL>
 __global__ __launch_bounds__(256) void softmax_lean_kernel(DevProblem p) {
+    zero_lp_pads(p);
     constexpr int E = IO::E;
     constexpr int CH = 64 * U;  // vectors per chunk
     typedef typename IO::V Vec;
@@ -246,6 +261,7 @@ __global__ __launch_bounds__(256) void softmax_lean_kernel(DevProblem p) {
 // Scalar path (any V, any alignment, any element type): one row per wave, lanes stride over v.
 template <class IO>
 __global__ __launch_bounds__(256) void softmax_scalar_kernel(DevProblem p) {
+    zero_lp_pads(p);
     typedef typename IO::S Sc;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

@@ -59,6 +59,8 @@ class MrnntProblem(ctypes.Structure):
         ("acts_dtype", ctypes.c_int),
         ("pad_T", ctypes.c_int64),
         ("pad_S1", ctypes.c_int64),
+        # version 4
+        ("lattice", ctypes.c_void_p),
     ]
 
 
@@ -112,6 +114,8 @@ def _bind(path: str, dev: bool = False) -> ctypes.CDLL:
     sig = {
         "mrnnt_workspace_size": (i, [P, ctypes.POINTER(sz)]),
         "mrnnt_forward": (i, [P, vp, sz, vp, i, vp]),
+        "mrnnt_lattice_bytes": (i, [P, ctypes.POINTER(sz)]),
+        "mrnnt_lattice_host": (i, [P, vp, sz]),
         "mrnnt_backward": (i, [P, vp, vp, vp, vp]),
         "mrnnt_cost_and_grad": (i, [P, vp, sz, vp, vp, vp, vp]),
         "mrnnt_read_loglik": (i, [P, vp, vp, vp, vp]),
@@ -137,8 +141,8 @@ def _bind(path: str, dev: bool = False) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.mrnnt_version() < 3:
-        raise ImportError(f"{path} is a stale build (ABI version {lib.mrnnt_version()} < 3); "
+    if lib.mrnnt_version() < 4:
+        raise ImportError(f"{path} is a stale build (ABI version {lib.mrnnt_version()} < 4); "
                           "rebuild with `make -C monotonic-rnnt_amd`")
     return lib
 
@@ -176,6 +180,13 @@ def use(lib: ctypes.CDLL):
         yield lib
     finally:
         _override = prev
+
+
+def select_dev() -> ctypes.CDLL:
+    """Route this whole process through the development build (A/B tools with launch knobs; never the product)."""
+    global _override
+    _override = load_dev()
+    return _override
 
 
 def devtools() -> ctypes.CDLL:

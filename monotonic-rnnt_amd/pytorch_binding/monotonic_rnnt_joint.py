@@ -72,7 +72,7 @@ class _JointPrepared:
             raise RuntimeError(f"monotonic_rnnt_joint: expected {B} input/label lengths")
         if B and (self.T_host.max() > enc.size(1) or self.S_host.max() + 1 > pred.size(1)):
             raise RuntimeError("monotonic_rnnt_joint: enc/pred have fewer frames/label positions than the lengths")
-        self.T_dev, self.S_dev = ln.on(dev)
+        self.T_dev, self.S_dev, _ = ln.on(dev)
         if not labels.is_cuda:
             _check_labels(labels, self.S_host, V)
         lab = labels.detach().to(dev, torch.int32)

@@ -67,18 +67,32 @@ class _Lengths:
         self.ws = {}
 
     def on(self, dev: torch.device):
-        """Device copies, uploaded once as one pinned non-blocking copy on the current stream (no host wait); a
-        call on another stream waits for that upload through an event."""
+        """Device copies of T, S and the lattice offsets (mrnnt_lattice_host: with them the forward launches no
+        setup kernel), uploaded once as one pinned non-blocking copy on the current stream (no host wait); a call
+        on another stream waits for that upload through an event. Returns (T_dev, S_dev, lattice_dev)."""
         hit = self.dev.get(dev)
         stream = torch.cuda.current_stream(dev)
         if hit is None:
-            ts = torch.from_numpy(np.stack([self.T, self.S])).pin_memory().to(dev, non_blocking=True)
+            B = self.T.size
+            p = _L.MrnntProblem()
+            p.B, p.T_host, p.S_host = B, self.T_ptr, self.S_ptr
+            n = ctypes.c_size_t(0)
+            _L.check(_L.load().mrnnt_lattice_bytes(ctypes.byref(p), ctypes.byref(n)), "lattice_bytes")
+            lat_off = 8 * ((2 * B * 4 + 7) // 8)
+            host = torch.empty(lat_off + n.value, dtype=torch.uint8).pin_memory()
+            hv = host.numpy()
+            hv[:B * 4] = self.T.view(np.uint8)
+            hv[B * 4:2 * B * 4] = self.S.view(np.uint8)
+            _L.check(_L.load().mrnnt_lattice_host(ctypes.byref(p), ctypes.c_void_p(host.data_ptr() + lat_off), n.value),
+                     "lattice_host")
+            d = host.to(dev, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(stream)
-            hit = self.dev[dev] = (ts[0], ts[1], ev, stream)
-        elif hit[3] != stream:
-            stream.wait_event(hit[2])
-        return hit[0], hit[1]
+            hit = self.dev[dev] = (d[:B * 4].view(torch.int32), d[B * 4:2 * B * 4].view(torch.int32), d[lat_off:],
+                                   ev, stream)
+        elif hit[4] != stream:
+            stream.wait_event(hit[3])
+        return hit[0], hit[1], hit[2]
 
 
 _LEN_CACHE: "dict" = {}
@@ -141,8 +155,9 @@ class _Prepared:
         if lab.dim() == 1:
             lab = lab.view(B, -1)
         self.labels = lab.contiguous() if lab.numel() else torch.zeros(B, 1, dtype=torch.int32, device=dev)
+        self.lattice = None
         if self.on_gpu:
-            self.T_dev, self.S_dev = ln.on(dev)
+            self.T_dev, self.S_dev, self.lattice = ln.on(dev)
             if not labels.is_cuda:
                 _check_labels(labels, self.S_host, acts.size(-1))
         self.alignment = None
@@ -159,6 +174,7 @@ class _Prepared:
         if self.on_gpu:
             p.T_dev = self.T_dev.data_ptr()
             p.S_dev = self.S_dev.data_ptr()
+            p.lattice = self.lattice.data_ptr()
         p.acts = self.acts.data_ptr()
         p.labels = self.labels.data_ptr()
         p.label_stride = self.labels.size(1)

@@ -9,6 +9,7 @@ import oracle as O
 import monotonic_rnnt_op as op
 import _mrnnt_lib as L
 
+L.select_dev()  # the dp_halo knob lives in the development build
 dev = torch.device("cuda:0")
 for (B, T, S, V, k) in [(2, 50, 10, 16, 2), (2, 200, 40, 64, 2), (2, 1000, 200, 64, 2), (1, 1000, 200, 1024, 2)]:
     rng = np.random.default_rng(0)

@@ -23,6 +23,8 @@ import monotonic_rnnt_op as op  # noqa: E402
 import _mrnnt_lib as L  # noqa: E402
 
 seeds = [int(s) for s in sys.argv[1].split(",")]
+if sys.argv[2:]:
+    L.select_dev()  # launch knobs live in the development build
 for kv in sys.argv[2:]:
     k, v = kv.split("=")
     assert L.tune(k, int(v)) >= 0, k

@@ -72,7 +72,7 @@ grads = torch.empty_like(acts)
 gp = ctypes.c_void_p(grads.data_ptr())
 timeit("mrnnt_backward (ctypes call only)", lambda: lib.mrnnt_backward(ctypes.byref(prep.problem), wsp, None, gp, st))
 timeit("torch.empty_like(acts)", lambda: torch.empty_like(acts))
-timeit("pinned lengths upload", lambda: op._lengths_on_device(T_t, S_t, Tn, Sn, dev))
+timeit("lengths cache lookup", lambda: op._lengths(T_t, S_t).on(dev))
 
 
 def ctx():

@@ -42,6 +42,8 @@ def main():
     import monotonic_rnnt_joint as J
     import monotonic_rnnt_op as op
 
+    if a.tune:
+        L.select_dev()  # launch knobs live in the development build
     for kv in a.tune:
         k, v = kv.split("=")
         assert L.tune(k, int(v)) >= 0, k

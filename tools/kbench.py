@@ -50,7 +50,7 @@ def main():
     import _mrnnt_lib as L
     from bench import lengths_for
 
-    lib = L.load()
+    lib = L.select_dev()  # launch knobs live in the development build
     DEFAULTS = {k: L.tune(k) for k in ("softmax_variant", "grad_variant", "softmax_grid_per_cu", "grad_grid_per_cu",
                                        "nt_store", "nt_load", "occ_skip", "col_scatter", "dp_halo")}
     dev = torch.device("cuda:0")
@@ -62,13 +62,13 @@ def main():
         del pieces
         torch.cuda.empty_cache()
     rk, wd = (int(x) for x in args.rank.split("/"))
-    T, S, V, workload = lengths_for(args.config, rk, wd)
+    T, S, V, workload = lengths_for(args.config, rk, wd)[:4]
     B = len(T)
     rows = int(np.sum(T.astype(np.int64) * (S + 1)))
     n_band = int(np.sum((S.astype(np.int64) + 1) * (T - S + 1) - 1))
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     acts = torch.empty((rows, V), dtype=torch.float32, device=dev)
-    L.check(lib.mrnnt_synth_acts(ctypes.c_void_p(acts.data_ptr()), 0, rows * V, 0, 1, stream), "synth")
+    L.synth_acts(acts.data_ptr(), 0, rows * V, 0, True, stream.value)
     MAX_OFF_KB = 1 << 20  # grads may be shifted by up to 1 GiB (variant knob "grads_offset_kb")
     if not args.ws_first:
         grads_store = torch.empty(rows * V + MAX_OFF_KB * 256, dtype=torch.float32, device=dev)

@@ -31,11 +31,11 @@ def main():
     from bench import lengths_for
     lib = L.load()
     dev = torch.device("cuda:0")
-    T, S, V, workload = lengths_for(a.config, 0, 1)
+    T, S, V, workload = lengths_for(a.config, 0, 1)[:4]
     rows = int(np.sum(T.astype(np.int64) * (S + 1)))
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     acts = torch.empty((rows, V), dtype=torch.float32, device=dev)
-    L.check(lib.mrnnt_synth_acts(ctypes.c_void_p(acts.data_ptr()), 0, rows * V, 0, 1, stream), "synth")
+    L.synth_acts(acts.data_ptr(), 0, rows * V, 0, True, stream.value)
     if a.acts_dtype != "f32":
         acts = acts.to(torch.bfloat16 if a.acts_dtype == "bf16" else torch.float16)
         torch.cuda.empty_cache()
