@@ -385,12 +385,20 @@ def run(args, world):
                 "grad": {"avg_ms": round(g_avg, 4) if g_avg else None, "gbps": round(achieved, 1) if achieved else None},
             },
             "cpu_baseline": cpu,
+            "grads_placement": placement_log(),
             "tune": args.tune or None,
             "loss_check": loss_val,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def placement_log():
+    """The gradient-buffer placement decisions of this process (pytorch_binding/_grads_placement.py): per decision
+    the fill rate of each candidate block and the one kept; None when no call was large enough."""
+    import _grads_placement as GP
+    return (GP.ARENA.log or None) if GP.enabled() else "disabled"
 
 
 def same_buffers_copy_gbps(L, dev, src_t, dst_t, gib=8, reps=5):

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MRNNT_VERSION 4
+#define MRNNT_VERSION 5
 
 /* acts / grads element types */
 #define MRNNT_F32 0
@@ -191,6 +191,11 @@ RNNTStatus mrnnt_joint_backward(const mrnnt_joint_problem *p, void *workspace, i
  * overwritten) and d_pred (fp32, pred's shape; added to: zero it first). Zero d_enc's padding rows yourself. */
 RNNTStatus mrnnt_joint_reduce(const mrnnt_joint_problem *p, void *workspace, int64_t n_live, const void *dH,
                               const void *Hact, float *d_enc, float *d_pred, hipStream_t stream);
+
+/* Nontemporal zero fill of `bytes` (a multiple of 16) at `dst` (16-byte aligned device memory), in the gradient
+ * pass's store pattern. The Python surface times it once over a newly allocated large grads buffer to pick a
+ * fast-writing physical placement; also usable as a plain fill. Asynchronous on `stream`. */
+RNNTStatus mrnnt_fill_zero(void *dst, size_t bytes, hipStream_t stream);
 
 int mrnnt_version(void);
 

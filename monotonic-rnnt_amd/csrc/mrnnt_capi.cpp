@@ -641,6 +641,15 @@ RNNTStatus mrnnt_joint_reduce(const mrnnt_joint_problem *jp, void *ws, int64_t n
     return RNNT_STATUS_SUCCESS;
 }
 
+RNNTStatus mrnnt_fill_zero(void *dst, size_t bytes, hipStream_t stream) {
+    if (bytes == 0) return RNNT_STATUS_SUCCESS;
+    if (!dst || (reinterpret_cast<uintptr_t>(dst) & 15) || (bytes & 15))
+        return fail(RNNT_STATUS_INVALID_VALUE, "fill_zero: null or not 16-byte aligned pointer / size");
+    const hipError_t e = launch_fill_zero(dst, bytes, streaming_grid((int64_t)1 << 40, 32), stream);
+    if (e != hipSuccess) return fail_hip(e, "zero fill kernel");
+    return RNNT_STATUS_SUCCESS;
+}
+
 void mrnnt_profile_enable(int enable) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
     for (auto &r : g_prof) {  // recycled: a record still pending is complete before the event is recorded again

@@ -427,4 +427,26 @@ hipError_t launch_pad_zero(const DevProblem &p, int elem, void *grads, hipStream
     return hipGetLastError();
 }
 
+// Nontemporal zero fill, each workgroup streaming contiguous slabs in turn: the gradient pass's store stream
+// without its loads. The Python surface times it once over a new large grads buffer (placement probe).
+typedef unsigned int fill_u4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void fill_zero_kernel(fill_u4 *__restrict__ dst, int64_t n, int64_t slab) {
+    const fill_u4 z = {0u, 0u, 0u, 0u};
+    for (int64_t c0 = (int64_t)blockIdx.x * slab; c0 < n; c0 += (int64_t)gridDim.x * slab) {
+        const int64_t end = min(c0 + slab, n);
+        for (int64_t i = c0 + threadIdx.x; i < end; i += 256) __builtin_nontemporal_store(z, &dst[i]);
+    }
+}
+
+hipError_t launch_fill_zero(void *dst, size_t bytes, int grid_max, hipStream_t stream) {
+    const int64_t n = (int64_t)(bytes / 16);
+    if (n <= 0) return hipSuccess;
+    // >= 8 slabs per workgroup (one slab each would time the launch tail); 16 KiB .. 800 KiB slabs
+    const int64_t slab = std::min<int64_t>(50 * 1024, std::max<int64_t>(1024, n / ((int64_t)grid_max * 8) / 1024 * 1024));
+    const int64_t blocks = std::min<int64_t>((n + slab - 1) / slab, grid_max);
+    fill_zero_kernel<<<(int)blocks, 256, 0, stream>>>(static_cast<fill_u4 *>(dst), n, slab);
+    return hipGetLastError();
+}
+
 }  // namespace mrnnt

@@ -113,6 +113,7 @@ hipError_t launch_dp(const DevProblem &p, int S_max, int with_beta, float *costs
 hipError_t launch_grad(const DevProblem &p, int elem, const float *scale, void *grads, int grid, hipStream_t stream);
 hipError_t launch_count_live(const DevProblem &p, unsigned long long *count, hipStream_t stream);
 hipError_t launch_pad_zero(const DevProblem &p, int elem, void *grads, hipStream_t stream);
+hipError_t launch_fill_zero(void *dst, size_t bytes, int grid_max, hipStream_t stream);
 
 // kDeadLogOcc (the exact-zero gradient-row threshold) is in mrnnt_host.h, shared with the CPU implementation.
 

@@ -64,6 +64,28 @@ __global__ __launch_bounds__(256) void copy_probe_kernel(const u4 *__restrict__ 
     }
 }
 
+// nontemporal stores only, same slab walk as the copy probe
+__global__ __launch_bounds__(256) void write_probe_kernel(u4 *__restrict__ b, int64_t n, int64_t slab) {
+    const u4 z = {0u, 0u, 0u, 0u};
+    for (int64_t c0 = (int64_t)blockIdx.x * slab; c0 < n; c0 += (int64_t)gridDim.x * slab) {
+        const int64_t end = min(c0 + slab, n);
+        for (int64_t i = c0 + threadIdx.x; i < end; i += 256) __builtin_nontemporal_store(z, &b[i]);
+    }
+}
+
+// slab size and grid of the probes: 32 workgroups per CU, each streaming >= 8 slabs in turn (a single pass
+// of one slab per workgroup measures the launch tail, not the memory); slabs of 16 KiB .. 800 KiB
+int probe_grid(int64_t n, int64_t *slab, int64_t *blocks) {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return 3;
+    const int64_t blocks_max = (int64_t)32 * cus;
+    *slab = std::min<int64_t>(50 * 1024, std::max<int64_t>(1024, n / (blocks_max * 8) / 1024 * 1024));
+    *blocks = std::min<int64_t>((n + *slab - 1) / *slab, blocks_max);
+    return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -80,16 +102,19 @@ int mrnnt_copy_probe(void *dst, const void *src, size_t bytes, hipStream_t strea
     if ((bytes & 15) || (reinterpret_cast<uintptr_t>(dst) & 15) || (reinterpret_cast<uintptr_t>(src) & 15)) return 2;
     const int64_t n = (int64_t)(bytes / 16);
     if (n <= 0) return 0;
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        return 3;
-    // 32 workgroups per CU, each streaming >= 8 slabs in turn (a single pass of one slab per workgroup
-    // measures the launch tail, not the memory); slabs of 16 KiB .. 800 KiB, whole 4 KiB workgroup steps
-    const int64_t blocks_max = (int64_t)32 * cus;
-    const int64_t slab = std::min<int64_t>(50 * 1024, std::max<int64_t>(1024, n / (blocks_max * 8) / 1024 * 1024));
-    const int64_t blocks = std::min<int64_t>((n + slab - 1) / slab, blocks_max);
+    int64_t slab = 0, blocks = 0;
+    if (probe_grid(n, &slab, &blocks)) return 3;
     copy_probe_kernel<<<(int)blocks, 256, 0, stream>>>(static_cast<const u4 *>(src), static_cast<u4 *>(dst), n, slab);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int mrnnt_write_probe(void *dst, size_t bytes, hipStream_t stream) {
+    if ((bytes & 15) || (reinterpret_cast<uintptr_t>(dst) & 15)) return 2;
+    const int64_t n = (int64_t)(bytes / 16);
+    if (n <= 0) return 0;
+    int64_t slab = 0, blocks = 0;
+    if (probe_grid(n, &slab, &blocks)) return 3;
+    write_probe_kernel<<<(int)blocks, 256, 0, stream>>>(static_cast<u4 *>(dst), n, slab);
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

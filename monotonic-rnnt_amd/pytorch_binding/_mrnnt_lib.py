@@ -132,6 +132,7 @@ def _bind(path: str, dev: bool = False) -> ctypes.CDLL:
         "mrnnt_joint_reduce": (i, [JP, vp, i64, vp, vp, vp, vp, vp]),
         "mrnnt_last_error": (ctypes.c_char_p, []),
         "mrnnt_version": (i, []),
+        "mrnnt_fill_zero": (i, [vp, sz, vp]),
         "mrnnt_profile_enable": (None, [i]),
         "mrnnt_profile_read": (i, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64), i]),
     }
@@ -141,8 +142,8 @@ def _bind(path: str, dev: bool = False) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.mrnnt_version() < 4:
-        raise ImportError(f"{path} is a stale build (ABI version {lib.mrnnt_version()} < 4); "
+    if lib.mrnnt_version() < 5:
+        raise ImportError(f"{path} is a stale build (ABI version {lib.mrnnt_version()} < 5); "
                           "rebuild with `make -C monotonic-rnnt_amd`")
     return lib
 
@@ -190,7 +191,7 @@ def select_dev() -> ctypes.CDLL:
 
 
 def devtools() -> ctypes.CDLL:
-    """libmrnnt_devtools.so: mrnnt_synth_acts / mrnnt_copy_probe (bench and tests only)."""
+    """libmrnnt_devtools.so: mrnnt_synth_acts / mrnnt_copy_probe / mrnnt_write_probe (bench and tests only)."""
     global _tools
     with _lock:
         if _tools is None:
@@ -202,6 +203,8 @@ def devtools() -> ctypes.CDLL:
                                            ctypes.c_int, ctypes.c_void_p]
             t.mrnnt_copy_probe.restype = ctypes.c_int
             t.mrnnt_copy_probe.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+            t.mrnnt_write_probe.restype = ctypes.c_int
+            t.mrnnt_write_probe.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
             _tools = t
         return _tools
 

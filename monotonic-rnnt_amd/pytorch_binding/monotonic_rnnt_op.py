@@ -38,8 +38,10 @@ import torch
 
 try:
     from . import _mrnnt_lib as _L
+    from . import _grads_placement as _GP
 except ImportError:  # imported with pytorch_binding/ on sys.path, like the reference's tests do
     import _mrnnt_lib as _L
+    import _grads_placement as _GP
 
 _L.load()  # fail loudly at import if the HIP library is missing
 
@@ -245,8 +247,8 @@ def _forward(prep: _Prepared, with_beta: bool):
 
 def _backward(prep: _Prepared, ws: torch.Tensor, grad_scale: Optional[torch.Tensor],
               grads: Optional[torch.Tensor] = None) -> torch.Tensor:
-    if grads is None:
-        grads = torch.empty_like(prep.acts)
+    if grads is None:  # large GPU gradients: a fast-writing buffer, kept across calls (_grads_placement)
+        grads = _GP.grads_like(prep.acts) if prep.on_gpu else torch.empty_like(prep.acts)
     if grad_scale is not None:
         grad_scale = grad_scale.detach().to(prep.device, torch.float32).contiguous()
     if not prep.on_gpu:

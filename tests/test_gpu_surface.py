@@ -203,3 +203,49 @@ def test_bench_chunked_in_place_mode_matches_resident():
     assert chk["config"]["chunks_per_step"] > 1
     assert abs(res["loss_check"] - chk["loss_check"]) <= 1e-5 * abs(res["loss_check"])
     assert res["roofline"]["live_rows"] == chk["roofline"]["live_rows"]
+
+
+def test_fill_zero(dev):
+    import _mrnnt_lib as L
+    buf = torch.ones((1 << 20) + 64, dtype=torch.float32, device=dev)
+    sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    L.check(L.load().mrnnt_fill_zero(ctypes.c_void_p(buf.data_ptr() + 256), 4 << 20, sp), "fill_zero")
+    torch.cuda.synchronize()
+    assert torch.all(buf[64:64 + (1 << 20)] == 0) and torch.all(buf[:64] == 1) and torch.all(buf[64 + (1 << 20):] == 1)
+    assert L.load().mrnnt_fill_zero(ctypes.c_void_p(buf.data_ptr() + 4), 64, sp) == L.RNNT_STATUS_INVALID_VALUE
+    assert L.load().mrnnt_fill_zero(ctypes.c_void_p(buf.data_ptr()), 60, sp) == L.RNNT_STATUS_INVALID_VALUE
+
+
+def test_grads_placement_arena_on_device(op, dev, monkeypatch):
+    """The placement-aware gradient buffer (threshold lowered so a small call takes it, real fill probe): the
+    kept buffer is reused once acts.grad is dropped, a held gradient is never overwritten, and the gradients
+    equal the plain-allocation path bit for bit."""
+    import _grads_placement as GP
+    ar = GP.GradsArena(min_bytes=1 << 16)
+    monkeypatch.setattr(GP, "ARENA", ar)
+    rng = np.random.default_rng(17)
+    acts, labels, T, S = random_problem(rng, 4, (40, 90), 20, 256)
+    a = _t(acts, dev).requires_grad_(True)
+    lab, Tt, St = _t(labels, dev), torch.from_numpy(T), torch.from_numpy(S)
+
+    def step():
+        op.monotonic_rnnt_loss(a, lab, Tt, St).sum().backward()
+        torch.cuda.synchronize()
+        return a.grad
+
+    g1 = step()
+    assert len(ar.log) == 1 and ar.log[0]["kept_gbps"] > 0
+    p1, ref = g1.data_ptr(), g1.clone()
+    a.grad = None
+    del g1
+    g2 = step()
+    assert g2.data_ptr() == p1 and torch.equal(g2, ref)  # reused
+    keep = a.grad
+    a.grad = None
+    g3 = step()  # `keep` still holds the kept buffer: a fresh one, `keep` untouched
+    assert g3.data_ptr() != p1 and torch.equal(keep, ref) and torch.equal(g3, ref)
+    monkeypatch.setenv("MRNNT_GRADS_PLACEMENT", "0")
+    a.grad = None
+    assert torch.equal(step(), ref)
+    cr, gr = O.oracle_rnnt(acts, labels, T, S)
+    assert_grads(ref.cpu().numpy(), gr)
