@@ -101,6 +101,9 @@ def parse():
                     help="nccl (= RCCL over xGMI, the real path) or gloo (rehearsal: several ranks may share one GPU)")
     ap.add_argument("--hbm-budget-gb", type=float, default=0.0,
                     help="cap the bytes a rank may allocate for acts (+ grads) (0 = free HBM minus a reserve)")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture forward + backward once in a HIP graph and time its replays (host-launch-bound "
+                         "sizes such as configs[1]); per-kernel times then come from eager steps after the timing")
     ap.add_argument("--cpu-worker", default=None, help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -231,6 +234,9 @@ def run(args, world):
         workload += f", alignment-restricted (k={args.align_k}, labels evenly spaced)"
 
     T_t, S_t = torch.from_numpy(T), torch.from_numpy(S)
+    prof_steps = min(args.steps, 100) if args.graph else args.steps  # steps the per-kernel times cover
+    if args.graph and mode != "resident":
+        raise SystemExit("--graph needs a resident config")
     if mode == "resident":
         acts = synth(0, B)
         if args.acts_dtype != "f32":
@@ -240,21 +246,48 @@ def run(args, world):
         acts.requires_grad_(True)
         torch.cuda.synchronize()
 
-        def step():
-            acts.grad = None
+        def loss_and_grad():
             costs = op.monotonic_rnnt_loss(acts, labels_dev, T_t, S_t, align, args.align_k or 0, blank_label=0)
             loss = costs.sum()
             loss.backward()
+            return loss
+
+        def reduce(loss):
             if world > 1:
                 tot = coll(loss.detach().clone())
                 dist.all_reduce(tot)  # the one RCCL exchange of the path: 4 bytes over xGMI
+
+        def eager_step():
+            acts.grad = None
+            loss = loss_and_grad()
+            reduce(loss)
             return loss
+
+        step = eager_step
+        if args.graph:
+            # forward + backward captured once in a HIP graph (torch.cuda.graph) and replayed: no host work per
+            # step beyond one graph launch; acts.grad lives in the graph's pool and is rewritten by every replay
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                for _ in range(3):
+                    eager_step()
+            torch.cuda.current_stream(dev).wait_stream(side)
+            acts.grad = None
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                g_loss = loss_and_grad()
+
+            def step():
+                graph.replay()
+                reduce(g_loss)
+                return g_loss
 
         for _ in range(args.warmup):
             step()
         torch.cuda.synchronize()
         barrier()
-        L.profile_enable(True)
+        L.profile_enable(not args.graph)
         torch.cuda.synchronize()
         barrier()
         t0 = time.perf_counter()
@@ -264,6 +297,11 @@ def run(args, world):
         barrier()
         elapsed = time.perf_counter() - t0
         loss_val = float(loss.item())
+        if args.graph:  # replays launch no kernels from the host: per-kernel times from eager steps after timing
+            L.profile_enable(True)
+            for _ in range(prof_steps):
+                eager_step()
+            torch.cuda.synchronize()
     else:
         costs_c = torch.zeros(B, dtype=torch.float32, device=dev)
         T_d, S_d = T_t.to(dev), S_t.to(dev)
@@ -325,7 +363,7 @@ def run(args, world):
     s_ms, s_n = tot_ms("log_softmax")
     d_ms, d_n = tot_ms("alpha_beta")
     # the bytes of all gradient launches of the timed steps over their summed duration
-    achieved = grad_bytes * args.steps / (g_ms * 1e-3) / 1e9 if g_ms else None
+    achieved = grad_bytes * prof_steps / (g_ms * 1e-3) / 1e9 if g_ms else None
     g_avg = g_ms / g_n if g_ms else None
 
     traffic = None
@@ -364,6 +402,7 @@ def run(args, world):
             "config": {"workload": workload, "utterances_per_gpu": B, "global_batch": total_utts,
                        "rows_per_gpu": rows, "inband_rows_per_gpu": n_band, "V": V,
                        "memory_mode": mode, "chunks_per_step": n_chunks,
+                       "execution": "hip_graph_replay" if args.graph else "eager",
                        **({"window_rows_per_gpu": n_window} if n_window is not None else {}),
                        "parallelism": f"dp{world} (batch-sharded, one 4-byte "
                                       f"{'gloo (rehearsal)' if gloo else 'RCCL'} loss all-reduce)"},
@@ -375,12 +414,12 @@ def run(args, world):
                          "avg_launch_ms": round(g_avg, 4) if g_avg else None,
                          "live_rows": live, "inband_rows": n_band,
                          "formula_bytes_per_launch": formula_grad_bytes // n_chunks,
-                         "formula_gbps": round(formula_grad_bytes * args.steps / (g_ms * 1e-3) / 1e9, 1) if g_ms else None,
+                         "formula_gbps": round(formula_grad_bytes * prof_steps / (g_ms * 1e-3) / 1e9, 1) if g_ms else None,
                          "copy_gbps_same_buffers": copy_gbps,
                          "frac_of_copy_same_buffers": round(achieved / copy_gbps, 4) if achieved and copy_gbps else None},
             "kernels": {
                 "log_softmax": {"avg_ms": round(s_ms / s_n, 4) if s_ms else None,
-                                "gbps": round(softmax_bytes * args.steps / (s_ms * 1e-3) / 1e9, 1) if s_ms else None},
+                                "gbps": round(softmax_bytes * prof_steps / (s_ms * 1e-3) / 1e9, 1) if s_ms else None},
                 "alpha_beta": {"avg_ms": round(d_ms / d_n, 4) if d_ms else None},
                 "grad": {"avg_ms": round(g_avg, 4) if g_avg else None, "gbps": round(achieved, 1) if achieved else None},
             },

@@ -389,7 +389,7 @@ static void launch_io(const DevProblem &p, const float *scale, void *grads, int 
         grad_scalar_kernel<IO><<<grid, 256, 0, stream>>>(p, scale, grads);
         return;
     }
-    const bool ntl = tuning().nt_load != 0, nts = tuning().nt_store != 0;
+    const bool ntl = nt_acts_loads(p, sizeof(typename IO::S)), nts = tuning().nt_store != 0;
     if (ntl && nts) launch_vec<IO, true, true>(p, scale, grads, grid, stream);
     else if (ntl) launch_vec<IO, true, false>(p, scale, grads, grid, stream);
     else if (nts) launch_vec<IO, false, true>(p, scale, grads, grid, stream);

@@ -87,7 +87,8 @@ struct Tuning {
     int softmax_grid_per_cu = 0;  // workgroups (of 4 waves) per CU; 0 = one workgroup per lattice column
     int grad_grid_per_cu = 32;    // same for the gradient kernel
     int nt_store = 1;             // nontemporal stores of grads
-    int nt_load = 1;              // nontemporal loads of acts (both streaming kernels)
+    int nt_load = 2;              // loads of acts in both streaming kernels: 1 nontemporal, 0 default policy,
+                                  // 2 by size (nt_acts_loads)
     int occ_skip = 1;             // gradient: no acts read for rows with log-occupancy < kDeadLogOcc
     int joint_nbuf = 2;           // fused joint kernels: LDS buffers for the weight chunks (2 or 3)
     int joint_reduce_sparse = 0;  // joint d_enc/d_pred reduce: 0 row-parallel kernel below 4 live rows per column,
@@ -98,6 +99,18 @@ struct Tuning {
                                   // bit 1 gradient
 };
 Tuning &tuning();
+
+// Acts tensors up to this size stay in the 256 MiB Infinity Cache between the log-softmax pass and the gradient
+// pass's re-read when both load them with the default policy (MI355X_MICROARCH.md, Infinity Cache residency:
+// table + every byte streamed in between <= ~256 MiB); larger ones stream with nontemporal loads.
+constexpr int64_t kCachedActsBytes = 160ll << 20;
+
+inline bool nt_acts_loads(const DevProblem &p, int elem_bytes) {
+    const int k = tuning().nt_load;
+    if (k != 2) return k != 0;
+    const int64_t rows = p.pad_S1 ? (int64_t)p.B * p.pad_T * p.pad_S1 : p.num_rows;
+    return rows * (int64_t)p.V * elem_bytes > kCachedActsBytes;
+}
 
 // Kernel-family ids for the profiling counters (mrnnt_profile_read order).
 enum KernelId { K_BAND = 0, K_SOFTMAX = 1, K_DP = 2, K_GRAD = 3, K_SETUP = 4, K_JOINT_FWD = 5, K_JOINT_BWD = 6,

@@ -343,7 +343,7 @@ static void launch_io(const DevProblem &p, int grid, hipStream_t stream) {
     const bool vec = (p.V % IO::E) == 0 && (reinterpret_cast<uintptr_t>(p.acts) % 16) == 0;
     if (!vec)
         softmax_scalar_kernel<IO><<<grid, 256, 0, stream>>>(p);
-    else if (tuning().nt_load)
+    else if (nt_acts_loads(p, sizeof(typename IO::S)))
         launch_vec<IO, true>(p, grid, stream);
     else
         launch_vec<IO, false>(p, grid, stream);

@@ -11,6 +11,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdio>
 
 #pragma GCC visibility push(default)
 #include "mrnnt_devtools.h"
@@ -86,6 +87,16 @@ int probe_grid(int64_t n, int64_t *slab, int64_t *blocks) {
     return 0;
 }
 
+// a launch's status: an error left by an earlier call on this thread is reported (not blamed on this launch)
+int launch_status(const char *what, hipError_t stale) {
+    if (stale != hipSuccess)
+        std::fprintf(stderr, "mrnnt_devtools: error pending before %s: %s\n", what, hipGetErrorString(stale));
+    const hipError_t e = hipGetLastError();
+    if (e == hipSuccess) return 0;
+    std::fprintf(stderr, "mrnnt_devtools: %s launch failed: %s\n", what, hipGetErrorString(e));
+    return 3;
+}
+
 }  // namespace
 
 extern "C" {
@@ -94,8 +105,9 @@ int mrnnt_synth_acts(float *out, int64_t begin, int64_t count, uint64_t seed, in
     if (count <= 0) return 0;
     if (!out) return 2;
     const int64_t blocks = std::min<int64_t>((count + 255) / 256, 65536);
+    const hipError_t stale = hipGetLastError();
     synth_kernel<<<(int)blocks, 256, 0, stream>>>(out, begin, count, seed, normal);
-    return hipGetLastError() == hipSuccess ? 0 : 3;
+    return launch_status("synth", stale);
 }
 
 int mrnnt_copy_probe(void *dst, const void *src, size_t bytes, hipStream_t stream) {
@@ -104,8 +116,9 @@ int mrnnt_copy_probe(void *dst, const void *src, size_t bytes, hipStream_t strea
     if (n <= 0) return 0;
     int64_t slab = 0, blocks = 0;
     if (probe_grid(n, &slab, &blocks)) return 3;
+    const hipError_t stale = hipGetLastError();
     copy_probe_kernel<<<(int)blocks, 256, 0, stream>>>(static_cast<const u4 *>(src), static_cast<u4 *>(dst), n, slab);
-    return hipGetLastError() == hipSuccess ? 0 : 3;
+    return launch_status("copy probe", stale);
 }
 
 int mrnnt_write_probe(void *dst, size_t bytes, hipStream_t stream) {
@@ -114,8 +127,9 @@ int mrnnt_write_probe(void *dst, size_t bytes, hipStream_t stream) {
     if (n <= 0) return 0;
     int64_t slab = 0, blocks = 0;
     if (probe_grid(n, &slab, &blocks)) return 3;
+    const hipError_t stale = hipGetLastError();
     write_probe_kernel<<<(int)blocks, 256, 0, stream>>>(static_cast<u4 *>(dst), n, slab);
-    return hipGetLastError() == hipSuccess ? 0 : 3;
+    return launch_status("write probe", stale);
 }
 
 }  // extern "C"

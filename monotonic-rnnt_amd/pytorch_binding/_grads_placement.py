@@ -14,7 +14,8 @@ allocated while the earlier ones are still held (so it is a different block), up
 runs short, and the fastest is kept (the others go back to the caching allocator). Later calls get a view of the
 kept buffer whenever nothing else holds it (storage use count 1: e.g. the previous step's acts.grad was
 dropped), and a plain allocation otherwise, so a caller that keeps gradients across calls never sees them
-overwritten. MRNNT_GRADS_PLACEMENT=0 turns this off (plain torch.empty_like); release() drops the kept buffers.
+overwritten. Under HIP-graph capture the graph's memory pool serves gradients as usual. MRNNT_GRADS_PLACEMENT=0
+turns this off (plain torch.empty_like); release() drops the kept buffers.
 """
 from __future__ import annotations
 
@@ -85,7 +86,7 @@ class GradsArena:
     def like(self, acts: torch.Tensor) -> torch.Tensor:
         """A contiguous uninitialised tensor of acts' shape, dtype and device."""
         nbytes = acts.numel() * acts.element_size()
-        if nbytes < self.min_bytes or (self.require_cuda and not acts.is_cuda):
+        if nbytes < self.min_bytes or (self.require_cuda and not acts.is_cuda) or _capturing(acts):
             return torch.empty_like(acts, memory_format=torch.contiguous_format)
         key = (acts.device, acts.dtype)
         with self._lock:
@@ -118,6 +119,11 @@ class GradsArena:
     def release(self) -> None:
         with self._lock:
             self._kept.clear()
+
+
+def _capturing(acts: torch.Tensor) -> bool:
+    """Inside HIP-graph capture the probe cannot synchronise: the graph's own pool serves the gradient."""
+    return acts.is_cuda and torch.cuda.is_current_stream_capturing()
 
 
 def _contiguous_strides(shape) -> Tuple[int, ...]:

@@ -16,6 +16,11 @@ import ctypes
 import os
 import threading
 
+# One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64.so, and a library of ours loaded before
+# torch would bind the system copy first, leaving torch's device calls on a second runtime ("no ROCm-capable
+# device is detected" in whichever loses). Importing torch first makes every library here share torch's.
+import torch  # noqa: F401
+
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_DIR, "libmonotonic_rnnt_amd.so")
 DEV_PATH = os.path.join(PKG_DIR, "libmonotonic_rnnt_amd_dev.so")

@@ -92,7 +92,9 @@ class _Lengths:
             ev.record(stream)
             hit = self.dev[dev] = (d[:B * 4].view(torch.int32), d[B * 4:2 * B * 4].view(torch.int32), d[lat_off:],
                                    ev, stream)
-        elif hit[4] != stream:
+        elif hit[4] != stream and not torch.cuda.is_current_stream_capturing():
+            # (under HIP-graph capture the wait is skipped: torch.cuda.graph synchronises the device before
+            # capture begins, so an upload issued before it has landed)
             stream.wait_event(hit[3])
         return hit[0], hit[1], hit[2]
 

@@ -249,3 +249,57 @@ def test_grads_placement_arena_on_device(op, dev, monkeypatch):
     assert torch.equal(step(), ref)
     cr, gr = O.oracle_rnnt(acts, labels, T, S)
     assert_grads(ref.cpu().numpy(), gr)
+
+
+@pytest.mark.parametrize("aligned", [False, True])
+def test_hip_graph_capture_replay(op, dev, aligned):
+    """Forward + backward captured once in a HIP graph (torch.cuda.graph) and replayed on new logits written
+    into the captured input: costs and gradients equal an eager call on the same logits and the oracle (the
+    op makes no host synchronisation and allocates only through torch, so it is capture-safe)."""
+    rng = np.random.default_rng(40 + aligned)
+    acts1, labels, T, S = random_problem(rng, 5, (30, 120), 25, 128)
+    acts2 = rng.standard_normal(acts1.shape).astype(np.float32) * 2
+    al = None
+    if aligned:
+        al_np = np.zeros((len(T), int(T.max())), np.int32)
+        for b in range(len(T)):
+            fr = ((np.arange(S[b]) + 0.5) * T[b] / max(S[b], 1)).astype(np.int64)
+            al_np[b, fr] = labels[b, :S[b]]
+        al = _t(al_np, dev)
+    a = _t(acts1, dev).requires_grad_(True)
+    lab, Tt, St = _t(labels, dev), torch.from_numpy(T), torch.from_numpy(S)
+    k = 3 if aligned else 0
+
+    def fwd_bwd():
+        costs = op.monotonic_rnnt_loss(a, lab, Tt, St, al, k)
+        (costs * torch.arange(1, len(T) + 1, device=dev)).sum().backward()
+        return costs
+
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        for _ in range(2):
+            a.grad = None
+            fwd_bwd()
+    torch.cuda.current_stream(dev).wait_stream(side)
+    a.grad = None
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        c_static = fwd_bwd()
+    with torch.no_grad():
+        a.copy_(_t(acts2, dev))
+    g.replay()
+    torch.cuda.synchronize()
+    c_graph, g_graph = c_static.detach().clone(), a.grad.detach().clone()
+    g.replay()  # idempotent
+    torch.cuda.synchronize()
+    assert torch.equal(c_static, c_graph) and torch.equal(a.grad, g_graph)
+    b = _t(acts2, dev).requires_grad_(True)
+    ce = op.monotonic_rnnt_loss(b, lab, Tt, St, al, k)
+    (ce * torch.arange(1, len(T) + 1, device=dev)).sum().backward()
+    assert torch.equal(ce.detach(), c_graph) and torch.equal(b.grad, g_graph)
+    if not aligned:
+        cr, gr = O.oracle_rnnt(acts2, labels, T, S)
+        assert_costs(c_graph.cpu().numpy().astype(np.float64), cr)
+        w = np.repeat(np.arange(1, len(T) + 1), T * (S + 1))[:, None]
+        assert_grads(g_graph.cpu().numpy(), gr * w)
