@@ -104,6 +104,9 @@ def parse():
     ap.add_argument("--graph", action="store_true",
                     help="capture forward + backward once in a HIP graph and time its replays (host-launch-bound "
                          "sizes such as configs[1]); per-kernel times then come from eager steps after the timing")
+    ap.add_argument("--shard", default=None, metavar="R/N",
+                    help="time only shard R of the N-way sharded config in this one process (strong-scaling "
+                         "emulation on one GPU: the sharded path has no data-path collective; tools/shard_scaling.py)")
     ap.add_argument("--cpu-worker", default=None, help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -177,7 +180,12 @@ def run(args, world):
         if world > 1:
             dist.barrier()
 
-    T, S, V, workload, scaling = lengths_for(args.config, rank, world)
+    cfg_rank, cfg_world = (rank, world) if not args.shard else tuple(int(x) for x in args.shard.split("/"))
+    T, S, V, workload, scaling = lengths_for(args.config, cfg_rank, cfg_world)
+    if args.shard:
+        if world != 1 or not 0 <= cfg_rank < cfg_world:
+            raise SystemExit("--shard R/N runs one shard in one process (0 <= R < N)")
+        workload += f"; shard {cfg_rank} of {cfg_world} timed alone on this GPU"
     B = len(T)
     elem = {"f32": 4, "bf16": 2, "f16": 2}[args.acts_dtype]
     rows_u = T.astype(np.int64) * (S + 1)
@@ -191,6 +199,9 @@ def run(args, world):
         dist.all_gather(g, t)
         all_rows = [int(x.item()) for x in g]
     row0 = sum(all_rows[:rank])
+    if args.shard:  # the global row offset of shard R: every shard streams its own part of the synthetic batch
+        row0 = sum(int(np.sum(lengths_for(args.config, i, cfg_world)[0].astype(np.int64) *
+                              (lengths_for(args.config, i, cfg_world)[1] + 1))) for i in range(cfg_rank))
 
     # memory plan: acts + grads resident (autograd path), else grads in place, else chunks of utterances
     free, _ = torch.cuda.mem_get_info(dev)
