@@ -99,6 +99,7 @@ def test_random_case_vs_oracle(op, dev, seed):
 
 KNOB_SETS = [
     {"dp_halo": 0},                                  # per-step-barrier recursion at every S
+    {"dp_halo": 2},                                  # log-domain halo recursion
     {"softmax_variant": 0, "grad_variant": 2},       # first log-softmax, per-row gradient
     {"grad_variant": 3, "nt_load": 0, "nt_store": 0},  # row-sweep gradient, plain loads / stores
     {"softmax_variant": 14, "grad_variant": 6, "col_scatter": 0},

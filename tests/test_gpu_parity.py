@@ -325,6 +325,7 @@ def test_accuracy_against_reference_fp32_noise(op, dev):
     {"col_scatter": 3},
     {"dp_halo": 0},
     {"dp_halo": 1},
+    {"dp_halo": 2},
     {"col_scatter": 0, "grad_variant": 6},
     {"col_scatter": 3, "grad_grid_per_cu": 0, "softmax_grid_per_cu": 4},
     {"grad_variant": 5},
