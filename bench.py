@@ -143,6 +143,16 @@ def main():
     world = int(env_world or 1)
     if world != args.gpus:
         raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
+    if args.shard:  # checked before anything touches the GPU
+        try:
+            r, n = (int(x) for x in args.shard.split("/"))
+        except ValueError:
+            raise SystemExit(f"bench.py: --shard wants R/N, got {args.shard!r}")
+        if world != 1 or not 0 <= r < n:
+            raise SystemExit("bench.py: --shard R/N times one shard in one process (0 <= R < N, --gpus 1)")
+        args.shard = (r, n)
+    if args.graph and args.config in ("ragged", "c5"):
+        raise SystemExit("bench.py: --graph needs a resident config (headline, c2, ragged64)")
     import _mrnnt_lib as L
     if args.tune:
         with L.use(L.load_dev()):
@@ -180,11 +190,9 @@ def run(args, world):
         if world > 1:
             dist.barrier()
 
-    cfg_rank, cfg_world = (rank, world) if not args.shard else tuple(int(x) for x in args.shard.split("/"))
+    cfg_rank, cfg_world = (rank, world) if not args.shard else args.shard
     T, S, V, workload, scaling = lengths_for(args.config, cfg_rank, cfg_world)
     if args.shard:
-        if world != 1 or not 0 <= cfg_rank < cfg_world:
-            raise SystemExit("--shard R/N runs one shard in one process (0 <= R < N)")
         workload += f"; shard {cfg_rank} of {cfg_world} timed alone on this GPU"
     B = len(T)
     elem = {"f32": 4, "bf16": 2, "f16": 2}[args.acts_dtype]

@@ -32,8 +32,13 @@ MAX_CANDIDATES = 3
 HBM_RESERVE = 4 << 30      # free device memory left untouched when trying a further candidate
 
 
+# storage use count (private torch API, present in 2.x): without it a kept buffer could not be proven unshared,
+# so the module falls back to plain allocations
+_use_count = getattr(torch._C, "_storage_Use_Count", None)
+
+
 def enabled() -> bool:
-    return os.environ.get("MRNNT_GRADS_PLACEMENT", "1") != "0"
+    return _use_count is not None and os.environ.get("MRNNT_GRADS_PLACEMENT", "1") != "0"
 
 
 class _Kept:
@@ -91,7 +96,7 @@ class GradsArena:
         key = (acts.device, acts.dtype)
         with self._lock:
             kept = self._kept.get(key)
-            if kept is not None and torch._C._storage_Use_Count(kept.storage._cdata) > 1:
+            if kept is not None and _use_count(kept.storage._cdata) > 1:
                 return torch.empty_like(acts, memory_format=torch.contiguous_format)  # still held by the caller
             if kept is None or kept.nbytes < nbytes:
                 if kept is not None:

@@ -3,6 +3,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -18,3 +20,11 @@ def test_world_size_must_match_gpus():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1"], capture_output=True,
                        text=True, timeout=300, env=env)
     assert r.returncode != 0 and "WORLD_SIZE=2 but --gpus 1" in r.stderr
+
+
+@pytest.mark.parametrize("args,msg", [(["--shard", "2/2"], "--shard R/N"), (["--shard", "x"], "wants R/N"),
+                                      (["--config", "c5", "--graph"], "--graph needs")])
+def test_bad_options_fail_before_the_gpu(args, msg):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode != 0 and msg in r.stderr, r.stderr[-2000:]
