@@ -73,11 +73,29 @@ def lengths_for(config, rank, world):
         return Tg[:64], Sg[:64], 1024, "first 64 utterances of configs[3] (ragged T, S), V=1024", "weak"
     if config == "ragged":  # configs[3], sharded over ranks
         Tg, Sg = ragged_lengths()
-        from distributed import shard_bounds
-        lo, hi = shard_bounds(Tg.astype(np.int64) * (Sg + 1), world)[rank]
+        lo, hi = ragged_slice(rank, world)
         return (Tg[lo:hi], Sg[lo:hi], 1024,
                 f"B=512 ragged (T~U[200,1600], S~U[20,min(300,T)]), V=1024, sharded over {world}", "strong")
     raise SystemExit(f"unknown config {config}")
+
+
+def ragged_slice(rank, world):
+    """Utterances [lo, hi) of configs[3] owned by `rank` (contiguous prefix split balanced by rows, §8e)."""
+    from distributed import shard_bounds
+    Tg, Sg = ragged_lengths()
+    return shard_bounds(Tg.astype(np.int64) * (Sg + 1), world)[rank]
+
+
+def labels_for(config, scaling, rank, world, B, S_max, V):
+    """Synthetic labels U[1, V-1]: weak-scaled configs draw each rank's own batch (seed 1 + rank); the strong-scaled
+    configs[3] draws the global batch (seed 1) and each rank takes its slice, so every world size computes the
+    same 512 utterances."""
+    if scaling != "strong":
+        return np.random.default_rng(1 + rank).integers(1, V, (B, S_max)).astype(np.int32)
+    Tg, Sg = ragged_lengths()
+    lo, hi = ragged_slice(rank, world)
+    glob = np.random.default_rng(1).integers(1, V, (len(Tg), max(1, int(Sg.max())))).astype(np.int32)
+    return np.ascontiguousarray(glob[lo:hi, :S_max])
 
 
 def parse():
@@ -235,8 +253,7 @@ def run(args, world):
 
     stream_h = torch.cuda.current_stream(dev).cuda_stream
     acts_buf = torch.empty((max_chunk_rows, V), dtype=torch.float32, device=dev)
-    rng = np.random.default_rng(1 + rank)
-    labels_all = rng.integers(1, V, (B, max(1, int(S.max())))).astype(np.int32)
+    labels_all = labels_for(args.config, scaling, cfg_rank, cfg_world, B, max(1, int(S.max())), V)
     labels_dev = torch.from_numpy(labels_all).to(dev)
 
     def synth(lo, hi):
@@ -315,7 +332,7 @@ def run(args, world):
         torch.cuda.synchronize()
         barrier()
         elapsed = time.perf_counter() - t0
-        loss_val = float(loss.item())
+        loss_val = loss.detach().reshape(1).double()
         if args.graph:  # replays launch no kernels from the host: per-kernel times from eager steps after timing
             L.profile_enable(True)
             for _ in range(prof_steps):
@@ -348,8 +365,13 @@ def run(args, world):
         for _ in range(args.steps):
             for lo, hi in chunks:
                 elapsed += chunk_step(lo, hi)
-        loss_val = float(costs_c.sum().item())
+        loss_val = costs_c.double().sum().reshape(1)
         acts = None
+    # the whole batch's summed loss (every rank's share, the same all-reduce the step performs), for checks
+    loss_val = coll(loss_val)
+    if world > 1:
+        dist.all_reduce(loss_val)
+    loss_val = float(loss_val.item())
     prof = L.profile_read()
     L.profile_enable(False)
     el = coll(torch.tensor([elapsed], dtype=torch.float64, device=dev))
@@ -417,7 +439,7 @@ def run(args, world):
             "scaling": scaling,
             "vs_baseline": None,
             "dtype": args.acts_dtype,
-            "data": "synthetic: counter-hash N(0,1)-like acts (seed 0), labels U[1,V-1] (seed 1+rank); inputs resident in HBM",
+            "data": "synthetic: counter-hash N(0,1)-like acts (seed 0), labels U[1,V-1] (seed 1+rank; configs[3]: seed 1 over the global batch); inputs resident in HBM",
             "config": {"workload": workload, "utterances_per_gpu": B, "global_batch": total_utts,
                        "rows_per_gpu": rows, "inband_rows_per_gpu": n_band, "V": V,
                        "memory_mode": mode, "chunks_per_step": n_chunks,

@@ -303,3 +303,23 @@ def test_hip_graph_capture_replay(op, dev, aligned):
         assert_costs(c_graph.cpu().numpy().astype(np.float64), cr)
         w = np.repeat(np.arange(1, len(T) + 1), T * (S + 1))[:, None]
         assert_grads(g_graph.cpu().numpy(), gr * w)
+
+
+def test_bench_graph_mode_matches_eager():
+    """`bench.py --graph` (forward + backward replayed from a HIP graph) computes the loss of the eager step."""
+    eager = _bench(["--config", "c2", "--steps", "5", "--warmup", "2", "--no-cpu"])
+    graph = _bench(["--config", "c2", "--steps", "20", "--warmup", "3", "--no-cpu", "--graph"])
+    assert graph["config"]["execution"] == "hip_graph_replay" and eager["config"]["execution"] == "eager"
+    assert abs(graph["loss_check"] - eager["loss_check"]) <= 1e-6 * abs(eager["loss_check"])
+    assert graph["kernels"]["grad"]["avg_ms"] > 0 and graph["ms_per_step"] > 0
+
+
+def test_bench_ragged_sharded_two_ranks_equals_one():
+    """configs[3] strong-scaled over 2 ranks (gloo, both on this GPU, in-place chunks under a small HBM budget):
+    the all-reduced loss of the sharded batch equals the one-rank run over the whole batch."""
+    one = _bench(["--config", "ragged", "--steps", "1", "--warmup", "0", "--no-cpu", "--hbm-budget-gb", "30"], 400)
+    two = _bench(["--gpus", "2", "--dist-backend", "gloo", "--config", "ragged", "--steps", "1", "--warmup", "0",
+                  "--no-cpu", "--hbm-budget-gb", "30"], 400)
+    assert one["config"]["memory_mode"] == "inplace" and two["n_gpus"] == 2 and two["scaling"] == "strong"
+    assert one["config"]["global_batch"] == two["config"]["global_batch"] == 512
+    assert abs(one["loss_check"] - two["loss_check"]) <= 1e-6 * abs(one["loss_check"])
