@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MRNNT_VERSION 5
+#define MRNNT_VERSION 6
 
 /* acts / grads element types */
 #define MRNNT_F32 0
@@ -62,6 +62,9 @@ typedef struct mrnnt_problem {
     const void *lattice;     /* optional: device copy of mrnnt_lattice_host's output for these lengths. The lattice
                                 offsets then come from it and mrnnt_forward launches no setup kernel (a caller that
                                 repeats shapes uploads it once); NULL = built on the device in every forward */
+    /* --- version 6 --- */
+    int grad_scale_broadcast; /* 1: grad_scale[0] scales every utterance (a stride-0 upstream gradient, e.g. the
+                                backward of costs.sum(): no copy into a [B] vector); 0: grad_scale[b] */
 } mrnnt_problem;
 
 /* Validate lengths (reference semantics: B > 0, V > 0, T_b > 0, S_b >= 0, T_b >= S_b) and return the
@@ -83,7 +86,8 @@ RNNTStatus mrnnt_forward(const mrnnt_problem *p, void *workspace, size_t workspa
 
 /* Backward: grads[r, v] = grad_scale[b(r)] * dcost_b / dacts[r, v] for every row (out-of-band rows
  * are written with 0 * grad_scale, padding rows of the padded layout with 0; no pre-zeroing needed).
- * grads has the layout and element type of acts. grad_scale (device fp32 [B]) may be NULL (= 1).
+ * grads has the layout and element type of acts. grad_scale (device fp32 [B], or [1] with
+ * grad_scale_broadcast) may be NULL (= 1).
  * Requires a preceding mrnnt_forward(with_beta=1) on the same workspace and inputs. */
 RNNTStatus mrnnt_backward(const mrnnt_problem *p, const void *workspace, const float *grad_scale, void *grads,
                           hipStream_t stream);

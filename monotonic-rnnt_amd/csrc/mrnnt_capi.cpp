@@ -173,6 +173,7 @@ DevProblem make_dev(const mrnnt_problem *p, const Plan &pl, const void *ws) {
     d.num_rows = pl.N;
     d.pad_T = pl.pad_T;
     d.pad_S1 = pl.pad_S1;
+    d.scale_stride = p->grad_scale_broadcast ? 0 : 1;
     d.col_mul = 0;  // set per pass by mrnnt_forward / mrnnt_backward (tuning().col_scatter)
     d.den = reinterpret_cast<float *>(w + pl.off_den);
     d.lpb = reinterpret_cast<double *>(w + pl.off_lpb) + kLpPad;

@@ -389,7 +389,7 @@ void grad_column(const mrnnt_problem *p, const CpuPlan &pl, const Views &w, cons
     const int T = p->T_host[b], S = p->S_host[b], W = S + 1, V = pl.V, blank = p->blank;
     const int *lab = p->labels ? p->labels + (int64_t)b * p->label_stride : nullptr;
     const float *acts = static_cast<const float *>(p->acts);
-    const float sc = scale ? scale[b] : 1.0f;
+    const float sc = scale ? scale[p->grad_scale_broadcast ? 0 : b] : 1.0f;
     const double ll = w.ll[b];
     const float zero = (ll > kNegInf ? 0.0f : std::numeric_limits<float>::quiet_NaN()) * sc;
     const int64_t r0 = pl.row_off[b] + (int64_t)t * W, a0 = acts_row(pl, b, t, W);

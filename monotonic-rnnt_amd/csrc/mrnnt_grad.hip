@@ -57,7 +57,7 @@ __global__ __launch_bounds__(256) void grad_kernel(DevProblem p, const float *__
         const int lo = max(0, t - (T - S));
         const int hi = min(t, S);
         const double ll = p.ll[b];
-        const float sc = scale ? scale[b] : 1.0f;
+        const float sc = scale ? scale[b * p.scale_stride] : 1.0f;
         const Vec zv = splat<IO>(zero_row_value(ll, sc));
         const int *__restrict__ lab_b = p.labels + (int64_t)b * p.label_stride;
 
@@ -135,7 +135,7 @@ __global__ __launch_bounds__(256) void grad_staged_kernel(DevProblem p, const fl
         const int lo = max(0, t - (T - S));
         const int hi = min(t, S);
         const double ll = p.ll[b];
-        const float sc = scale ? scale[b] : 1.0f;
+        const float sc = scale ? scale[b * p.scale_stride] : 1.0f;
         const Vec zv = splat<IO>(zero_row_value(ll, sc));
         const int *__restrict__ lab_b = p.labels + (int64_t)b * p.label_stride;
 
@@ -215,7 +215,7 @@ __global__ __launch_bounds__(256) void grad_rows_kernel(DevProblem p, const floa
         const int t = (int)(loc / (unsigned)(S + 1));
         const int s = (int)(loc - (unsigned)t * (unsigned)(S + 1));
         const bool inb = s <= t && (S - s) <= (T - t);
-        const float sc = scale ? scale[b] : 1.0f;
+        const float sc = scale ? scale[b * p.scale_stride] : 1.0f;
         Vec *__restrict__ out = gv + row * (int64_t)VL;
         RowCoef rc;
         if (inb) rc = row_coef(p, t, T, S, s, row, p.ll[b], p.labels + (int64_t)b * p.label_stride);
@@ -263,7 +263,7 @@ __global__ __launch_bounds__(256) void grad_scalar_kernel(DevProblem p, const fl
         const int lo = max(0, t - (T - S));
         const int hi = min(t, S);
         const double ll = p.ll[b];
-        const float sc = scale ? scale[b] : 1.0f;
+        const float sc = scale ? scale[b * p.scale_stride] : 1.0f;
         const Sc zs = IO::from_f(zero_row_value(ll, sc));
         const int *__restrict__ lab_b = p.labels + (int64_t)b * p.label_stride;
         for (int s = wave; s <= S; s += 4) {

@@ -32,6 +32,7 @@ struct DevProblem {
     int64_t num_cols;           // sum_b T_b
     int64_t num_rows;           // N = sum_b T_b (S_b + 1)
     int64_t pad_T, pad_S1;      // padded acts layout (pad_S1 == 0: packed)
+    int64_t scale_stride;       // upstream-gradient stride: grad_scale[b * scale_stride] (0 = one value for all)
     int64_t col_mul;            // column visiting order of the streaming kernels: the i-th column visited is
                                 // (i * col_mul) % num_cols (0 = in order; col_mul coprime with num_cols)
     float *den;                 // [N]  log-softmax denominator  -max - log sum exp(z - max)

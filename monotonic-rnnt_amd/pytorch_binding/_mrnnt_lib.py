@@ -66,6 +66,8 @@ class MrnntProblem(ctypes.Structure):
         ("pad_S1", ctypes.c_int64),
         # version 4
         ("lattice", ctypes.c_void_p),
+        # version 6
+        ("grad_scale_broadcast", ctypes.c_int),
     ]
 
 
@@ -147,8 +149,8 @@ def _bind(path: str, dev: bool = False) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.mrnnt_version() < 5:
-        raise ImportError(f"{path} is a stale build (ABI version {lib.mrnnt_version()} < 5); "
+    if lib.mrnnt_version() < 6:
+        raise ImportError(f"{path} is a stale build (ABI version {lib.mrnnt_version()} < 6); "
                           "rebuild with `make -C monotonic-rnnt_amd`")
     return lib
 

@@ -251,8 +251,16 @@ def _backward(prep: _Prepared, ws: torch.Tensor, grad_scale: Optional[torch.Tens
               grads: Optional[torch.Tensor] = None) -> torch.Tensor:
     if grads is None:  # large GPU gradients: a fast-writing buffer, kept across calls (_grads_placement)
         grads = _GP.grads_like(prep.acts) if prep.on_gpu else torch.empty_like(prep.acts)
+    prep.problem.grad_scale_broadcast = 0
     if grad_scale is not None:
-        grad_scale = grad_scale.detach().to(prep.device, torch.float32).contiguous()
+        grad_scale = grad_scale.detach()
+        if (grad_scale.dim() == 1 and grad_scale.numel() > 1 and grad_scale.stride(0) == 0
+                and grad_scale.dtype == torch.float32 and grad_scale.device == prep.device):
+            # the backward of costs.sum() / .mean(): one value expanded over B -- read it in place (ABI v6)
+            # instead of materialising the [B] vector (a copy kernel per step)
+            prep.problem.grad_scale_broadcast = 1
+        else:
+            grad_scale = grad_scale.to(prep.device, torch.float32).contiguous()
     if not prep.on_gpu:
         _L.check(_L.load().mrnnt_cpu_backward(ctypes.byref(prep.problem), _ptr(ws), _ptr(grad_scale), _ptr(grads),
                                               prep.num_threads), "mrnnt_cpu_backward")

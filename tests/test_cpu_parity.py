@@ -210,6 +210,21 @@ def test_backward_twice_with_retain_graph():
         costs.sum().backward()  # the saved workspace was freed by the last backward
 
 
+def test_broadcast_upstream_gradient():
+    """costs.sum() / costs.mean() hand backward a stride-0 [B] gradient, read in place (grad_scale_broadcast, ABI
+    v6): bit-identical to the same scale as a materialised [B] vector, and against the oracle."""
+    rng = np.random.default_rng(5)
+    acts, labels, T, S = random_problem(rng, 4, (5, 20), 6, 16)
+    out = []
+    for reduce in (lambda c: c.sum(), lambda c: c.mean(), lambda c: (c * torch.full_like(c, 1.0 / 4)).sum()):
+        a = torch.from_numpy(acts).requires_grad_(True)
+        reduce(op.monotonic_rnnt_loss(a, torch.from_numpy(labels), torch.from_numpy(T), torch.from_numpy(S))).backward()
+        out.append(a.grad)
+    assert torch.equal(out[1], out[2])
+    cr, gr = O.oracle_rnnt(acts, labels, T, S)
+    assert_grads(out[0].numpy(), gr)
+
+
 def test_padded_layout_equals_packed():
     rng = np.random.default_rng(11)
     acts, labels, T, S = random_problem(rng, 3, (4, 15), 5, 9)

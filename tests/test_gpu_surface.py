@@ -106,6 +106,21 @@ def test_backward_twice_with_retain_graph(op, dev):
     assert_grads(g1.cpu().numpy(), 2 * gr)
 
 
+def test_broadcast_upstream_gradient(op, dev):
+    """costs.sum() / costs.mean() hand backward a stride-0 [B] gradient, which the gradient kernel reads in place
+    (grad_scale_broadcast, ABI v6: no copy kernel): bit-identical to the same scale as a materialised [B] vector."""
+    rng = np.random.default_rng(6)
+    acts, labels, T, S = random_problem(rng, 5, (5, 60), 20, 64)
+    out = []
+    for reduce in (lambda c: c.sum(), lambda c: c.mean(), lambda c: (c * torch.full_like(c, 1.0 / 5)).sum()):
+        a = _t(acts, dev).requires_grad_(True)
+        reduce(op.monotonic_rnnt_loss(a, _t(labels, dev), torch.from_numpy(T), torch.from_numpy(S))).backward()
+        out.append(a.grad)
+    assert torch.equal(out[1], out[2])
+    cr, gr = O.oracle_rnnt(acts, labels, T, S)
+    assert_grads(out[0].cpu().numpy(), gr)
+
+
 def test_gpu_and_cpu_paths_agree(op, dev):
     """The same inputs through the HIP kernels (GPU tensors) and the library's host implementation (CPU
     tensors): both against the oracle, and against each other."""
