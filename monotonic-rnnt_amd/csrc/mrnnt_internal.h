@@ -82,8 +82,9 @@ size_t joint_min_lds_bytes(int H, int V);
 struct Tuning {
     int softmax_variant = 13;     // log-softmax kernel: 13/14/15 -> lean kernel with 2 (4 for rows of < 96
                                   // vectors) / 1 / 4 rows per wave; 0/2 -> first kernel (shuffle butterflies), 1/2 rows
-    int grad_variant = 5;         // gradient kernel: 5 -> staged coefficients (1 / 2 rows per wave for rows of
-                                  // >= 192 / >= 96 vectors; shorter rows: per-row kernel, 4 rows), 6 -> staged, 2 rows;
+    int grad_variant = 5;         // gradient kernel: 5 -> staged coefficients (1 / 2 / 4 rows per wave for rows of
+                                  // >= 192 / >= 96 / fewer vectors; short rows loaded nontemporally: per-row
+                                  // kernel, 2 rows), 6 -> staged, 2 rows;
                                   // 0 / 2 -> per-row coefficients, default / 2 rows; 3 -> row-stride sweep (packed)
     int softmax_grid_per_cu = 0;  // workgroups (of 4 waves) per CU; 0 = one workgroup per lattice column
     int grad_grid_per_cu = 32;    // same for the gradient kernel
