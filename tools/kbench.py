@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--buffers", type=int, default=1,
                     help="allocate this many acts and grads buffers (variant knobs acts_buf / grads_buf pick one): "
                          "does the gradient kernel's speed depend on where a buffer sits?")
+    ap.add_argument("--acts-dtype", default="f32", choices=["f32", "bf16", "f16"],
+                    help="element type of acts / grads (the kernels' IoBF16 / IoF16 paths)")
     ap.add_argument("--ws-first", action="store_true",
                     help="allocate the workspace before grads (the order the autograd surface produces)")
     args = ap.parse_args()
@@ -69,9 +71,14 @@ def main():
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     acts = torch.empty((rows, V), dtype=torch.float32, device=dev)
     L.synth_acts(acts.data_ptr(), 0, rows * V, 0, True, stream.value)
+    tdt = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}[args.acts_dtype]
+    elem = torch.empty(0, dtype=tdt).element_size()
+    if tdt != torch.float32:
+        acts = acts.to(tdt)
+        torch.cuda.empty_cache()
     MAX_OFF_KB = 1 << 20  # grads may be shifted by up to 1 GiB (variant knob "grads_offset_kb")
     if not args.ws_first:
-        grads_store = torch.empty(rows * V + MAX_OFF_KB * 256, dtype=torch.float32, device=dev)
+        grads_store = torch.empty(rows * V + MAX_OFF_KB * 256, dtype=tdt, device=dev)
     labels = torch.from_numpy(np.random.default_rng(1).integers(1, V, (B, int(S.max()))).astype(np.int32)).to(dev)
     T_dev = torch.from_numpy(T).to(dev)
     S_dev = torch.from_numpy(S).to(dev)
@@ -82,16 +89,17 @@ def main():
     p.T_dev, p.S_dev = T_dev.data_ptr(), S_dev.data_ptr()
     p.acts, p.labels, p.label_stride = acts.data_ptr(), labels.data_ptr(), labels.size(1)
     p.alignment, p.align_stride, p.align_blank, p.num_rows = None, 0, 0, rows
+    p.acts_dtype = {"f32": L.MRNNT_F32, "bf16": L.MRNNT_BF16, "f16": L.MRNNT_F16}[args.acts_dtype]
     n = ctypes.c_size_t(0)
     L.check(lib.mrnnt_workspace_size(ctypes.byref(p), ctypes.byref(n)), "ws")
     ws = torch.empty(n.value, dtype=torch.uint8, device=dev)
     if args.ws_first:
-        grads_store = torch.empty(rows * V + MAX_OFF_KB * 256, dtype=torch.float32, device=dev)
+        grads_store = torch.empty(rows * V + MAX_OFF_KB * 256, dtype=tdt, device=dev)
     grads_holder = {"t": grads_store[: rows * V].view(rows, V)}
     acts_list, grads_list = [acts], [grads_store]
     for _ in range(args.buffers - 1):
         acts_list.append(acts.clone())
-        grads_list.append(torch.empty(rows * V, dtype=torch.float32, device=dev))
+        grads_list.append(torch.empty(rows * V, dtype=tdt, device=dev))
     out_alloc = {"acts": acts.data_ptr(), "grads": grads_store.data_ptr(), "ws": ws.data_ptr()}
 
     def run_once():
@@ -132,9 +140,9 @@ def main():
                 times[i][k].append(prof[k][0])
     out_alloc["acts_bufs"] = [t.data_ptr() for t in acts_list]
     out_alloc["grads_bufs"] = [t.data_ptr() for t in grads_list]
-    out = {"alloc": out_alloc, "fragment": {"gb": args.fragment_gb, "mib": args.fragment_mib, "held": len(keep)}, "workload": workload, "rows": rows, "inband_rows": n_band, "V": V, "variants": []}
-    gb = (n_band + rows) * V * 4 / 1e9
-    sb = n_band * V * 4 / 1e9
+    out = {"alloc": out_alloc, "fragment": {"gb": args.fragment_gb, "mib": args.fragment_mib, "held": len(keep)}, "workload": workload, "acts_dtype": args.acts_dtype, "rows": rows, "inband_rows": n_band, "V": V, "variants": []}
+    gb = (n_band + rows) * V * elem / 1e9
+    sb = n_band * V * elem / 1e9
     for v, t in zip(variants, times):
         med = {k: float(np.median(x)) for k, x in t.items()}
         out["variants"].append({"knobs": v, "median_ms": med, "min_ms": {k: float(np.min(x)) for k, x in t.items()},
