@@ -418,9 +418,10 @@ def run(args, world):
         except Exception:
             traffic = None
 
-    copy_gbps = None
+    copy_gbps = acts_read_gbps = None
     if mode == "resident" and acts.grad is not None:
         copy_gbps = same_buffers_copy_gbps(L, dev, acts.detach(), acts.grad)
+        acts_read_gbps = acts_read_probe_gbps(L, dev, acts.detach())
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_sample > 0 and args.acts_dtype == "f32":
@@ -460,7 +461,11 @@ def run(args, world):
                          "frac_of_copy_same_buffers": round(achieved / copy_gbps, 4) if achieved and copy_gbps else None},
             "kernels": {
                 "log_softmax": {"avg_ms": round(s_ms / s_n, 4) if s_ms else None,
-                                "gbps": round(softmax_bytes * prof_steps / (s_ms * 1e-3) / 1e9, 1) if s_ms else None},
+                                "gbps": round(softmax_bytes * prof_steps / (s_ms * 1e-3) / 1e9, 1) if s_ms else None,
+                                "acts_read_probe_gbps": acts_read_gbps,
+                                "frac_of_acts_read_probe": round(softmax_bytes * prof_steps / (s_ms * 1e-3) / 1e9 /
+                                                                 acts_read_gbps, 4)
+                                if s_ms and acts_read_gbps else None},
                 "alpha_beta": {"avg_ms": round(d_ms / d_n, 4) if d_ms else None},
                 "grad": {"avg_ms": round(g_avg, 4) if g_avg else None, "gbps": round(achieved, 1) if achieved else None},
             },
@@ -508,6 +513,35 @@ def same_buffers_copy_gbps(L, dev, src_t, dst_t, gib=8, reps=5):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
     return round(2 * n / (ms * 1e-3) / 1e9, 1)
+
+
+def acts_read_probe_gbps(L, dev, acts_t, reps=3):
+    """Nontemporal read rate of THIS run's whole acts buffer (mrnnt_read_probe, the log-softmax pass's load stream,
+    HIP events on the stream it runs on), after the timed region: like a grads buffer, an acts
+    allocation reads at a rate set by its physical placement, which the caller -- not the library -- chose, so
+    the log-softmax kernel is also reported against the rate of its own input. None below 1 GiB."""
+    import torch
+    n = acts_t.numel() * acts_t.element_size()
+    n -= n % 16
+    if n < (1 << 30):
+        return None
+    stream = torch.cuda.current_stream(dev)
+    sp = ctypes.c_void_p(stream.cuda_stream)
+    sink = torch.zeros(4, dtype=torch.uint8, device=dev)
+    tools = L.devtools()
+
+    def run():
+        if tools.mrnnt_read_probe(ctypes.c_void_p(acts_t.data_ptr()), n, ctypes.c_void_p(sink.data_ptr()), sp):
+            raise RuntimeError("read probe failed")
+
+    run()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        run()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return round(n / (e0.elapsed_time(e1) / reps * 1e-3) / 1e9, 1)
 
 
 def synthetic_alignment(labels, T, S, k):

@@ -19,6 +19,10 @@ int mrnnt_synth_acts(float *out, int64_t begin, int64_t count, uint64_t seed, in
  * access pattern (contiguous slabs per workgroup). */
 int mrnnt_copy_probe(void *dst, const void *src, size_t bytes, hipStream_t stream);
 
+/* Nontemporal read of `bytes` (multiple of 16, 16-byte aligned) in the same slab walk (the log-softmax pass's load
+ * stream); `sink` is 4 bytes of device memory the kernel may write. */
+int mrnnt_read_probe(const void *src, size_t bytes, void *sink, hipStream_t stream);
+
 /* Nontemporal zero fill of `bytes` (multiple of 16, 16-byte aligned) in the same slab walk: the write half of
  * the copy probe alone. */
 int mrnnt_write_probe(void *dst, size_t bytes, hipStream_t stream);

@@ -198,7 +198,7 @@ def select_dev() -> ctypes.CDLL:
 
 
 def devtools() -> ctypes.CDLL:
-    """libmrnnt_devtools.so: mrnnt_synth_acts / mrnnt_copy_probe / mrnnt_write_probe (bench and tests only)."""
+    """libmrnnt_devtools.so: mrnnt_synth_acts / mrnnt_copy_probe / mrnnt_read_probe / mrnnt_write_probe (bench and tests only)."""
     global _tools
     with _lock:
         if _tools is None:
@@ -212,6 +212,8 @@ def devtools() -> ctypes.CDLL:
             t.mrnnt_copy_probe.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
             t.mrnnt_write_probe.restype = ctypes.c_int
             t.mrnnt_write_probe.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+            t.mrnnt_read_probe.restype = ctypes.c_int
+            t.mrnnt_read_probe.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
             _tools = t
         return _tools
 
