@@ -136,6 +136,30 @@ def _run(op, acts, labels_np, T, S, dev):
     return costs.detach().cpu().numpy().astype(np.float64), g
 
 
+def test_config_c4_ragged_extremes():
+    """configs[3]'s extreme utterances at full length against the oracle: the most lattice rows (T=1549, S=297),
+    the longest labels (S=300), the most frames (T=1597) and the fewest frames (T=203) -- 5.5 GB of logits."""
+    import monotonic_rnnt_op as op
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(0)
+    Tg = rng.integers(200, 1601, 512).astype(np.int32)
+    Sg = np.array([rng.integers(20, min(300, t) + 1) for t in Tg], np.int32)
+    rows_g = Tg.astype(np.int64) * (Sg + 1)
+    pick = sorted({int(np.argmax(rows_g)), int(np.argmax(Sg)), int(np.argmax(Tg)), int(np.argmin(Tg))})
+    T, S, V = Tg[pick], Sg[pick], 1024
+    rows = int(np.sum(T.astype(np.int64) * (S + 1)))
+    host = O.synth_acts(0, rows * V, seed=6).reshape(rows, V)
+    labels = np.random.default_rng(7).integers(1, V, (len(pick), int(S.max()))).astype(np.int32)
+    c, g = _run(op, torch.from_numpy(host).to(dev), labels, T, S, dev)
+    cr, gr = O.oracle_rnnt(host, labels, T, S, precision="f64", num_threads=len(pick))
+    assert np.max(np.abs(c - cr) / np.abs(cr)) <= 1e-4
+    r0 = 0
+    for T_b, S_b in zip(T, S):  # per utterance: no full-size temporary of the difference
+        r1 = r0 + int(T_b) * (int(S_b) + 1)
+        assert np.abs(g[r0:r1].cpu().numpy() - gr[r0:r1]).max() <= 1e-4
+        r0 = r1
+
+
 def test_config_c4_ragged_subset():
     """configs[3] lengths (T~U[200,1600], S~U[20,min(300,T)], V=1024, seed 0): the first 6 utterances of the
     512-utterance batch, full lengths, against the oracle."""
