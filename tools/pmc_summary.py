@@ -58,10 +58,15 @@ def main():
     ap.add_argument("--bench", required=True)
     ap.add_argument("--tag", required=True)
     ap.add_argument("--config", default="headline")
+    ap.add_argument("--dtype", default="f32", help="acts dtype of the profiled bench (f32 / bf16 / f16)")
     a = ap.parse_args()
+    # the headline f32 run feeds bench.py's `traffic` (profiles/pmc_grad_traffic.json); other runs keep their own files
+    main_run = a.config == "headline" and a.dtype == "f32"
+    sfx = "" if main_run else f"_{a.config}_{a.dtype}"
+    elem = {"f32": 4, "bf16": 2, "f16": 2}[a.dtype]
     out_dir = os.path.join(ROOT, "profiles", a.tag)
     os.makedirs(out_dir, exist_ok=True)
-    shutil.copy(os.path.join(a.stats, "run_kernel_stats.csv"), os.path.join(out_dir, f"kernel_stats_{a.config}.csv"))
+    shutil.copy(os.path.join(a.stats, "run_kernel_stats.csv"), os.path.join(out_dir, f"kernel_stats_{a.config}{'' if a.dtype == 'f32' else '_' + a.dtype}.csv"))
     bench = json.loads(open(a.bench).read().strip().splitlines()[-1])
 
     stats = {}
@@ -82,7 +87,7 @@ def main():
                                                    None)}
     json.dump({"units": "KiB per launch as reported by rocprofv3 (separate --pmc passes); "
                         "hbm_bytes_corrected = FETCH_SIZE*2 + WRITE_SIZE (gfx950 correction)",
-               "kernels": per}, open(os.path.join(out_dir, "pmc_per_launch.json"), "w"), indent=1)
+               "kernels": per}, open(os.path.join(out_dir, f"pmc_per_launch{sfx}.json"), "w"), indent=1)
 
     grad = [k for k in per if family(k) in ("grad_staged_kernel", "grad_kernel", "grad_rows_kernel")]
     soft = [k for k in per if family(k) in ("softmax_lean_kernel", "softmax_kernel")]
@@ -91,6 +96,7 @@ def main():
     alg = bench["roofline"]["algorithmic_bytes_per_launch"]
     res = {
         "config": a.config,
+        "dtype": a.dtype,
         "kernel": grad[0],
         "hbm_bytes_per_launch": int(round(g["hbm_bytes_corrected"])),
         "read_bytes_corrected": int(round(g["FETCH_SIZE_KiB"] * 2048)),
@@ -99,15 +105,17 @@ def main():
         "traffic_over_algorithmic": round(g["hbm_bytes_corrected"] / alg, 4),
         "softmax_kernel": soft[0],
         "softmax_read_bytes_corrected": int(round(s["FETCH_SIZE_KiB"] * 2048)),
-        "softmax_algorithmic_bytes": bench["config"]["inband_rows_per_gpu"] * bench["config"]["V"] * 4,
+        "softmax_algorithmic_bytes": bench["config"]["inband_rows_per_gpu"] * bench["config"]["V"] * elem,
         "rocprof_avg_ms": {"grad": g["rocprof_avg_ms"], "log_softmax": s["rocprof_avg_ms"]},
         "bench_hip_event_avg_ms": {"grad": bench["kernels"]["grad"]["avg_ms"],
                                    "log_softmax": bench["kernels"]["log_softmax"]["avg_ms"]},
         "correction": "FETCH_SIZE(KiB)*1024*2 (gfx950 half-count of 16-B/lane streaming reads) + WRITE_SIZE(KiB)*1024",
-        "source": f"profiles/{a.tag}/pmc_per_launch.json (rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, "
-                  f"python3 bench.py --config {a.config} --steps 3 --warmup 1 --no-cpu)",
+        "source": f"profiles/{a.tag}/pmc_per_launch{sfx}.json (rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, "
+                  f"python3 bench.py --config {a.config} --acts-dtype {a.dtype} --steps 3 --warmup 1 --no-cpu)",
     }
-    json.dump(res, open(os.path.join(ROOT, "profiles", "pmc_grad_traffic.json"), "w"), indent=1)
+    out = os.path.join(ROOT, "profiles", "pmc_grad_traffic.json") if main_run else \
+        os.path.join(out_dir, f"pmc_grad_traffic{sfx}.json")
+    json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
 
