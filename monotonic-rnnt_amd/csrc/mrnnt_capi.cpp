@@ -407,6 +407,8 @@ RNNTStatus mrnnt_read_state(const mrnnt_problem *p, const void *ws, float *den_d
         return fail(RNNT_STATUS_MEMOPS_FAILED, "copy alpha");
     if (beta_dev && hipMemcpyAsync(beta_dev, d.beta, sizeof(double) * pl.N, hipMemcpyDeviceToDevice, stream) != hipSuccess)
         return fail(RNNT_STATUS_MEMOPS_FAILED, "copy beta");
+    if ((alpha_dev || beta_dev) && launch_mask_state(d, alpha_dev, beta_dev, stream) != hipSuccess)
+        return fail(RNNT_STATUS_EXECUTION_FAILED, "mask state");
     return RNNT_STATUS_SUCCESS;
 }
 
@@ -701,6 +703,7 @@ __attribute__((visibility("default"))) int mrnnt_tune(const char *key, int value
     else if (!std::strcmp(key, "grad_variant")) slot = &t.grad_variant;
     else if (!std::strcmp(key, "col_scatter")) slot = &t.col_scatter;
     else if (!std::strcmp(key, "dp_halo")) slot = &t.dp_halo;
+    else if (!std::strcmp(key, "dp_lean")) slot = &t.dp_lean;
     else if (!std::strcmp(key, "joint_reduce_sparse")) slot = &t.joint_reduce_sparse;
     else if (!std::strcmp(key, "softmax_grid_per_cu")) slot = &t.softmax_grid_per_cu;
     else if (!std::strcmp(key, "grad_grid_per_cu")) slot = &t.grad_grid_per_cu;

@@ -134,8 +134,21 @@ __device__ __forceinline__ int checked_label(bool has, int l, int V, float &ze) 
     return (has && !bad) ? l : -1;
 }
 
+// ln(s) of a row's fp32 exp-sum (s in [1, V] for a finite row) without the fp64 log routine: s = m * 2^e with the
+// exponent exact in fp64 and m in [sqrt(1/2), sqrt(2)), whose |log2 m| <= 1/2 the fp32 v_log_f32 resolves to ~3e-8
+// absolute -- below the fp32 rounding of s itself. 0 -> -inf, inf / NaN propagate as in log().
+__device__ __forceinline__ double log_row_sum(float s) {
+    int e = __builtin_amdgcn_frexp_expf(s);
+    float m = __builtin_amdgcn_frexp_mantf(s);  // [0.5, 1)
+    if (m < 0.70710678f) {
+        m *= 2.0f;
+        e -= 1;
+    }
+    return ((double)e + (double)fast_log2(m)) * 0.69314718055994530942;
+}
+
 __device__ __forceinline__ void write_row(const DevProblem &p, int64_t row, float m, float sum, float zb, float ze) {
-    const double den = -(double)m - log((double)sum);
+    const double den = -(double)m - log_row_sum(sum);
     p.den[row] = (float)den;
     p.lpb[row] = (double)zb + den;
     p.lpe[row] = (double)ze + den;

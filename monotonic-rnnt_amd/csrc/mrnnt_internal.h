@@ -97,6 +97,8 @@ struct Tuning {
                                   // 1 always frame by frame, 2 always row-parallel
     int dp_halo = 2;              // alpha/beta: halo recursion (one barrier per 8 steps, 8 / 16-step prefetch
                                   // blocks: 1 / 2) for S+1 <= 448; 0: one barrier per step
+    int dp_lean = 1;              // halo recursion without an alignment: 1 -> the lean step (uniform-row-pointer
+                                  // addressing, bound-ctrl DPP shifts, no band mask); 0 -> the masked step
     int col_scatter = 2;          // visit columns in a scattered order (DevProblem::col_mul): bit 0 log-softmax,
                                   // bit 1 gradient
 };
@@ -124,6 +126,8 @@ hipError_t launch_setup(const int *T, const int *S, int B, int64_t *row_off, int
 hipError_t launch_align(const DevProblem &p, const int *alignment, int64_t align_stride, int align_blank,
                         int max_shift, int *mtmp, int *min_s, int *max_s, hipStream_t stream);
 hipError_t launch_softmax(const DevProblem &p, int elem, int grid, hipStream_t stream);
+// mrnnt_read_state: alpha / beta cells outside the compute band set to -inf (either may be null)
+hipError_t launch_mask_state(const DevProblem &p, double *alpha, double *beta, hipStream_t stream);
 hipError_t launch_dp(const DevProblem &p, int S_max, int with_beta, float *costs, hipStream_t stream);
 hipError_t launch_grad(const DevProblem &p, int elem, const float *scale, void *grads, int grid, hipStream_t stream);
 hipError_t launch_count_live(const DevProblem &p, unsigned long long *count, hipStream_t stream);

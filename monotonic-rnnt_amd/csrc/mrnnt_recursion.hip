@@ -31,6 +31,19 @@ __device__ __forceinline__ double dpp_shl1(double v) {  // lane i <- lane i+1 (l
     return __hiloint2double(hi, lo);
 }
 
+// Shifts with bound_ctrl: the lane without a source reads 0 (no "old" operand to initialise).
+__device__ __forceinline__ double dpp_shr1_bc(double v) {
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x138, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x138, 0xf, 0xf, true);
+    return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ double dpp_shl1_bc(double v) {
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x130, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x130, 0xf, 0xf, true);
+    return __hiloint2double(hi, lo);
+}
+
 template <int K, int D, int NW, bool BAND>
 __device__ __forceinline__ void alpha_pass(const DevProblem &p, int b, float *__restrict__ costs, double (*xb)[8]) {
     const int lane = threadIdx.x & 63;
@@ -203,7 +216,7 @@ __global__ __launch_bounds__(64 * NW) void recursion_kernel(DevProblem p, int wi
 // neighbouring wave owns (alpha: the cells below, beta: the cells above). Those halo lanes lose one valid lane
 // per step (their outer neighbour is not in the wave), so the own cells stay exact for HL steps; then the
 // neighbour's HL boundary cells are copied in through LDS (one barrier per HL steps instead of one per step).
-template <int D, int NW, int HL, bool BAND>
+template <int D, int NW, int HL, bool BAND, int LEAN>
 __device__ __forceinline__ void alpha_pass_halo(const DevProblem &p, int b, float *__restrict__ costs,
                                                 double (*xh)[8][HL > 0 ? HL : 1]) {
     static_assert((HL == 0 ? NW == 1 : D % HL == 0) && NW <= 8,
@@ -216,6 +229,9 @@ __device__ __forceinline__ void alpha_pass_halo(const DevProblem &p, int b, floa
     const int64_t r0 = p.row_off[b], c0 = p.col_off[b];
     const int s0 = wave * C - HL + lane;  // negative for the halo lanes of wave 0 (always out of band)
     const bool own = lane >= HL && s0 < W;
+    // LEAN: every row access is a uniform row pointer (SGPRs) + an unsigned lane offset; the halo lanes of wave 0
+    // (s0 < 0, never in band) read cell 0
+    const unsigned sl = (unsigned)max(s0, 0);
 
     double a = (s0 == 0) ? 0.0 : NEG_INF_D;
     double pb[D], pe[D];
@@ -223,12 +239,43 @@ __device__ __forceinline__ void alpha_pass_halo(const DevProblem &p, int b, floa
 #pragma unroll
     for (int d = 0; d < D; ++d) {
         const int tt = min(d, T - 1);
-        pb[d] = p.lpb[r0 + (int64_t)tt * W + s0];
-        pe[d] = p.lpe[r0 + (int64_t)tt * W + s0 - 1];
+        if (LEAN) {
+            pb[d] = (p.lpb + (r0 + (int64_t)tt * W))[sl];
+            pe[d] = (p.lpe + (r0 + (int64_t)tt * W - 1))[sl];
+        } else {
+            pb[d] = p.lpb[r0 + (int64_t)tt * W + s0];
+            pe[d] = p.lpe[r0 + (int64_t)tt * W + s0 - 1];
+        }
         mn[d] = BAND ? p.min_s[c0 + tt] : 0;
         mx[d] = BAND ? p.max_s[c0 + tt] : S;
     }
+    auto step_lean = [&](int t, int d) {
+        // unrestricted: no band mask -- a cell above the band only ever sees -inf predecessors (so it is -inf), a
+        // cell below it only feeds cells below it and is never read (mrnnt_read_state masks it for inspection);
+        // halo lanes are garbage between refreshes exactly as in the masked step (they only feed halo lanes)
+        double carry = dpp_shr1_bc(a);
+        if (HL == 0 && lane == 0) carry = NEG_INF_D;
+        const double v = lse2(a + pb[d], carry + pe[d]);
+        if (BAND) {
+            const int lo = max(max(t - (T - 1 - S), mn[d]), 0);
+            const int hi = min(min(t + 1, S), mx[d]);
+            a = (s0 >= lo && s0 <= hi) ? v : NEG_INF_D;
+        } else {
+            // the halo lanes of wave 0 stand for cells s < 0 and feed cell 0: they stay -inf
+            a = (HL > 0 && s0 < 0) ? NEG_INF_D : v;
+        }
+        if (own) (p.alpha + (r0 + (int64_t)t * W))[sl] = a;
+        const int tn = min(t + D, T - 1);
+        pb[d] = (p.lpb + (r0 + (int64_t)tn * W))[sl];
+        pe[d] = (p.lpe + (r0 + (int64_t)tn * W - 1))[sl];
+        mn[d] = BAND ? p.min_s[c0 + tn] : 0;
+        mx[d] = BAND ? p.max_s[c0 + tn] : S;
+    };
     auto step = [&](int t, int d) {
+        if (LEAN) {
+            step_lean(t, d);
+            return;
+        }
         const int lo = max(max(t - (T - 1 - S), mn[d]), 0);
         const int hi = min(min(t + 1, S), mx[d]);
         double carry = dpp_shr1(a);  // lane 0: garbage that only ever feeds halo lanes ...
@@ -274,7 +321,7 @@ __device__ __forceinline__ void alpha_pass_halo(const DevProblem &p, int b, floa
     }
 }
 
-template <int D, int NW, int HL, bool BAND>
+template <int D, int NW, int HL, bool BAND, int LEAN>
 __device__ __forceinline__ void beta_pass_halo(const DevProblem &p, int b, double (*xh)[8][HL > 0 ? HL : 1]) {
     static_assert((HL == 0 ? NW == 1 : D % HL == 0) && NW <= 8,
                   "halo refreshes at prefetch-block positions (HL = 0: one wave, no halo); xh sized for <= 8 waves");
@@ -286,6 +333,7 @@ __device__ __forceinline__ void beta_pass_halo(const DevProblem &p, int b, doubl
     const int64_t r0 = p.row_off[b], c0 = p.col_off[b];
     const int s0 = wave * C + lane;  // lanes >= C: halo, the first HL cells of the wave above
     const bool own = lane < C && s0 < W;
+    const unsigned sl = (unsigned)s0;
 
     double bn = (s0 == S) ? 0.0 : NEG_INF_D;  // beta(T, s)
     double pb[D], pe[D];
@@ -293,12 +341,41 @@ __device__ __forceinline__ void beta_pass_halo(const DevProblem &p, int b, doubl
 #pragma unroll
     for (int d = 0; d < D; ++d) {
         const int tt = max(T - 1 - d, 0);
-        pb[d] = p.lpb[r0 + (int64_t)tt * W + s0];
-        pe[d] = p.lpe[r0 + (int64_t)tt * W + s0];
+        pb[d] = (p.lpb + (r0 + (int64_t)tt * W))[sl];
+        pe[d] = (p.lpe + (r0 + (int64_t)tt * W))[sl];
         mn[d] = (BAND && tt > 0) ? p.min_s[c0 + tt - 1] : 0;
         mx[d] = (BAND && tt > 0) ? p.max_s[c0 + tt - 1] : S;
     }
+    auto step_lean = [&](int t, int d) {
+        // unrestricted: no band mask -- a cell below the band only sees -inf successors, one above it (s > t) only
+        // feeds cells above it and is never read (mrnnt_read_state masks it for inspection)
+        double carry = dpp_shl1_bc(bn);
+        if (HL == 0 && lane == 63) carry = NEG_INF_D;
+        const double v = lse2(bn + pb[d], carry + pe[d]);
+        if (BAND) {
+            int lo = 0, hi = 0;
+            if (t > 0) {
+                lo = max(max(t - (T - S), mn[d]), 0);
+                hi = min(min(t, S), mx[d]);
+            }
+            bn = (s0 >= lo && s0 <= hi) ? v : NEG_INF_D;
+        } else {
+            // lanes past S (halo lanes of the top wave) feed cell S from above: they stay -inf (with one wave, lane
+            // 63's successor is -inf and so are they)
+            bn = (HL > 0 && s0 > S) ? NEG_INF_D : v;
+        }
+        if (own) (p.beta + (r0 + (int64_t)t * W))[sl] = bn;
+        const int tn = max(t - D, 0);
+        pb[d] = (p.lpb + (r0 + (int64_t)tn * W))[sl];
+        pe[d] = (p.lpe + (r0 + (int64_t)tn * W))[sl];
+        mn[d] = (BAND && tn > 0) ? p.min_s[c0 + tn - 1] : 0;
+        mx[d] = (BAND && tn > 0) ? p.max_s[c0 + tn - 1] : S;
+    };
     auto step = [&](int t, int d) {
+        if (LEAN) {
+            step_lean(t, d);
+            return;
+        }
         int lo, hi;
         if (t == 0) {
             lo = 0;
@@ -345,21 +422,25 @@ __device__ __forceinline__ void beta_pass_halo(const DevProblem &p, int b, doubl
     if (threadIdx.x == 0) p.llb[b] = bn;
 }
 
-template <int D, int NW, int HL, bool BAND>
+template <int D, int NW, int HL, bool BAND, int LEAN = 0>
 __global__ __launch_bounds__(64 * NW) void recursion_halo_kernel(DevProblem p, int with_beta,
                                                                  float *__restrict__ costs) {
     __shared__ double xh[2][8][HL > 0 ? HL : 1];
     const int b = with_beta ? (int)(blockIdx.x >> 1) : (int)blockIdx.x;
     const bool bwd = with_beta && (blockIdx.x & 1);
     if (bwd)
-        beta_pass_halo<D, NW, HL, BAND>(p, b, xh);
+        beta_pass_halo<D, NW, HL, BAND, LEAN>(p, b, xh);
     else
-        alpha_pass_halo<D, NW, HL, BAND>(p, b, costs, xh);
+        alpha_pass_halo<D, NW, HL, BAND, LEAN>(p, b, costs, xh);
 }
 
 template <int NW, int HL = 8>
 static void launch_halo(const DevProblem &p, int with_beta, float *costs, hipStream_t stream) {
     const int blocks = with_beta ? 2 * p.B : p.B;
+    if (tuning().dp_lean && tuning().dp_halo == 2 && !p.min_s) {  // unrestricted: the lean step
+        recursion_halo_kernel<16, NW, HL, false, 1><<<blocks, 64 * NW, 0, stream>>>(p, with_beta, costs);
+        return;
+    }
     if (tuning().dp_halo == 2) {  // 16-step prefetch blocks
         if (p.min_s)
             recursion_halo_kernel<16, NW, HL, true><<<blocks, 64 * NW, 0, stream>>>(p, with_beta, costs);

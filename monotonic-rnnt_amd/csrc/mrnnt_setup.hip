@@ -118,4 +118,28 @@ hipError_t launch_align(const DevProblem &p, const int *alignment, int64_t align
     return hipGetLastError();
 }
 
+// mrnnt_read_state: cells outside the compute band as -inf (the reference getters' values). Without an alignment
+// the lean recursion step (mrnnt_recursion.hip) leaves finite values in cells that no in-band cell and no gradient
+// row reads.
+__global__ __launch_bounds__(64) void mask_state_kernel(DevProblem p, double *__restrict__ alpha,
+                                                        double *__restrict__ beta) {
+    for (int64_t c = blockIdx.x; c < p.num_cols; c += gridDim.x) {
+        const int b = p.col_b[c];
+        const int T = p.T[b], S = p.S[b];
+        const int t = (int)(c - p.col_off[b]);
+        const int64_t rowc = p.row_off[b] + (int64_t)t * (S + 1);
+        for (int s = threadIdx.x; s <= S; s += 64) {
+            if (alpha && (s > min(t + 1, S) || s < t - (T - 1 - S))) alpha[rowc + s] = -__builtin_huge_val();
+            const bool bin = t == 0 ? s == 0 : (s <= t && s >= t - (T - S));
+            if (beta && !bin) beta[rowc + s] = -__builtin_huge_val();
+        }
+    }
+}
+
+hipError_t launch_mask_state(const DevProblem &p, double *alpha, double *beta, hipStream_t stream) {
+    const int grid = (int)(p.num_cols < (1 << 16) ? p.num_cols : (1 << 16));
+    mask_state_kernel<<<grid > 0 ? grid : 1, 64, 0, stream>>>(p, alpha, beta);
+    return hipGetLastError();
+}
+
 }  // namespace mrnnt

@@ -224,7 +224,8 @@ __global__ __launch_bounds__(256) void softmax_lean_kernel(DevProblem p) {
                     const float mn = fmaxf(m[r], cm);
                     const float mr = (mn == NEG_INF_F) ? 0.0f : mn;
                     const float off = -mr * kLog2e;
-                    float acc = sum[r] * fast_exp2(fmaf(m[r], kLog2e, off));
+                    float acc = 0.0f;  // the first chunk has no running sum to rescale
+                    if (base > 0) acc = sum[r] * fast_exp2(fmaf(m[r], kLog2e, off));
 #pragma unroll
                     for (int k = 0; k < U * E; ++k) acc += fast_exp2(fmaf(xf[k], kLog2e, off));
                     sum[r] = acc;
@@ -249,7 +250,7 @@ __global__ __launch_bounds__(256) void softmax_lean_kernel(DevProblem p) {
             }
             if (lane < nrow) {
                 const int64_t row = rowc + s + lane;
-                const double den = -(double)em - log((double)es);
+                const double den = -(double)em - log_row_sum(es);
                 p.den[row] = (float)den;
                 p.lpb[row] = (double)ezb + den;
                 p.lpe[row] = (double)eze + den;

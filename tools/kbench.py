@@ -53,8 +53,14 @@ def main():
     from bench import lengths_for
 
     lib = L.select_dev()  # launch knobs live in the development build
-    DEFAULTS = {k: L.tune(k) for k in ("softmax_variant", "grad_variant", "softmax_grid_per_cu", "grad_grid_per_cu",
-                                       "nt_store", "nt_load", "occ_skip", "col_scatter", "dp_halo")}
+    # every knob any variant sets is restored to its default before each variant (a knob left set by the previous
+    # variant would otherwise carry over into the next one, round after round)
+    SPECIAL = ("grads_buf", "acts_buf", "grads_offset_kb")
+    keys = {"softmax_variant", "grad_variant", "softmax_grid_per_cu", "grad_grid_per_cu", "nt_store", "nt_load",
+            "occ_skip", "col_scatter", "dp_halo"} | {k for v in variants for k in v if k not in SPECIAL}
+    DEFAULTS = {k: L.tune(k) for k in sorted(keys)}
+    bad = [k for k, v in DEFAULTS.items() if v < 0]
+    assert not bad, f"unknown knobs {bad}"
     dev = torch.device("cuda:0")
     keep = []
     if args.fragment_gb > 0:
