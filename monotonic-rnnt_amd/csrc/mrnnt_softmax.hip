@@ -144,7 +144,10 @@ __device__ __forceinline__ float lane_pick(const float (&x)[N], int k) {
 // exp per lane instead of two per step), blank / label logits read with a uniform indexed move + v_readlane
 // (no LDS spill of the row slice), and den / lpb / lpe of the R rows formed in parallel by lanes 0..R-1
 // (one fp64 log per R rows). FULL: V is a multiple of 64*U*E (no per-load bounds checks).
-template <class IO, int U, int R, bool NTL, bool FULL>
+// ONE: the row is a single chunk (VL <= 64 U, every configuration up to V = 1024): the wave max is reduced first and
+// every lane's exps are taken against it, so there is no per-lane running max, no rescale of lane partial sums
+// before the wave sum (one exp and its bookkeeping per row fewer), and the R rows' DPP chains interleave.
+template <class IO, int U, int R, bool NTL, bool FULL, bool ONE = false>
 __global__ __launch_bounds__(256) void softmax_lean_kernel(DevProblem p) {
     zero_lp_pads(p);
     constexpr int E = IO::E;
@@ -169,6 +172,71 @@ __global__ __launch_bounds__(256) void softmax_lean_kernel(DevProblem p) {
         const int *__restrict__ lab_b = p.labels + (int64_t)b * p.label_stride;
         zero_fill_outside_band(p, rowc, S, lo, hi);
 
+        if constexpr (ONE) {
+            for (int s = lo + wave * R; s <= hi; s += 4 * R) {
+                const int nrow = __builtin_amdgcn_readfirstlane(min(R, hi - s + 1));
+                Vec x[R][U];
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const int j = lane + 64 * u;
+                        x[r][u] = (r < nrow && (FULL || j < VL)) ? vload<NTL>(&av[(arow + s + r) * (int64_t)VL + j])
+                                                                 : ninf;
+                    }
+                float xf[R][U * E], M[R], zb[R], ze[R];
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const bool has = r < nrow && s + r < S;
+                    const int lab = checked_label(has, has ? __builtin_amdgcn_readfirstlane(lab_b[s + r]) : 0, p.V,
+                                                  ze[r]);
+                    float cm = NEG_INF_F;
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        float t4[E];
+                        IO::unpack(x[r][u], t4);
+#pragma unroll
+                        for (int i = 0; i < E; ++i) {
+                            xf[r][u * E + i] = t4[i];
+                            cm = fmaxf(cm, t4[i]);
+                        }
+                    }
+                    const int jb = blank / E;
+                    zb[r] = __int_as_float(__builtin_amdgcn_readlane(
+                        __float_as_int(lane_pick<U * E>(xf[r], (jb >> 6) * E + blank % E)), jb & 63));
+                    if (lab >= 0) {
+                        const int je = lab / E;
+                        ze[r] = __int_as_float(__builtin_amdgcn_readlane(
+                            __float_as_int(lane_pick<U * E>(xf[r], (je >> 6) * E + lab % E)), je & 63));
+                    }
+                    M[r] = wave_max_uniform(cm);
+                }
+                float em = 0.0f, es = 1.0f, ezb = 0.0f, eze = 0.0f;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    if (r >= nrow) break;
+                    const float off = -((M[r] == NEG_INF_F) ? 0.0f : M[r]) * kLog2e;
+                    float acc = 0.0f;
+#pragma unroll
+                    for (int k = 0; k < U * E; ++k) acc += fast_exp2(fmaf(xf[r][k], kLog2e, off));
+                    const float Ssum = wave_sum_uniform(acc);
+                    if (lane == r) {
+                        em = M[r];
+                        es = Ssum;
+                        ezb = zb[r];
+                        eze = ze[r];
+                    }
+                }
+                if (lane < nrow) {
+                    const int64_t row = rowc + s + lane;
+                    const double den = -(double)em - log_row_sum(es);
+                    p.den[row] = (float)den;
+                    p.lpb[row] = (double)ezb + den;
+                    p.lpe[row] = (double)eze + den;
+                }
+            }
+            continue;
+        }
         for (int s = lo + wave * R; s <= hi; s += 4 * R) {
             const int nrow = __builtin_amdgcn_readfirstlane(min(R, hi - s + 1));
             float m[R], sum[R], zb[R], ze[R];
@@ -319,8 +387,15 @@ static void launch_u(const DevProblem &p, int grid, hipStream_t stream) {
         else softmax_kernel<IO, U, 2, NTL><<<grid, 256, 0, stream>>>(p);
         return;
     }
-    // lean kernel: 13 -> 2 rows per wave (4 for rows of < 96 vectors), 14 -> 1, 15 -> 4
-    const int R = v == 14 ? 1 : (v == 15 || (v == 13 && U == 1)) ? 4 : 2;
+    if (v == 13 && VL <= 64 * U) {  // single-chunk rows (the default): wave max first, 4 / 2 rows per wave
+        constexpr int RO = U == 1 ? 4 : 2;
+        if (full) softmax_lean_kernel<IO, U, RO, NTL, true, true><<<grid, 256, 0, stream>>>(p);
+        else softmax_lean_kernel<IO, U, RO, NTL, false, true><<<grid, 256, 0, stream>>>(p);
+        return;
+    }
+    // running-max lean kernel: 13 (rows of several chunks) / 16 (any row) -> 2 rows per wave (4 for rows of < 96
+    // vectors), 14 -> 1, 15 -> 4
+    const int R = v == 14 ? 1 : (v == 15 || ((v == 13 || v == 16) && U == 1)) ? 4 : 2;
 #define MRNNT_LEAN(RR)                                                                              \
     (full ? softmax_lean_kernel<IO, U, RR, NTL, true><<<grid, 256, 0, stream>>>(p)                 \
           : softmax_lean_kernel<IO, U, RR, NTL, false><<<grid, 256, 0, stream>>>(p))
