@@ -98,8 +98,8 @@ struct Tuning {
                                   // 1 always frame by frame, 2 always row-parallel
     int dp_halo = 2;              // alpha/beta: halo recursion (one barrier per 8 steps, 8 / 16-step prefetch
                                   // blocks: 1 / 2) for S+1 <= 448; 0: one barrier per step
-    int dp_lean = 1;              // halo recursion without an alignment: 1 -> the lean step (uniform-row-pointer
-                                  // addressing, bound-ctrl DPP shifts, no band mask); 0 -> the masked step
+    int dp_lean = 1;              // halo recursion without an alignment: 1 -> the lean step (row pointers advanced
+                                  // per frame + lane offsets, bound-ctrl DPP shifts, no band mask); 0 -> masked step
     int col_scatter = 2;          // visit columns in a scattered order (DevProblem::col_mul): bit 0 log-softmax,
                                   // bit 1 gradient
 };

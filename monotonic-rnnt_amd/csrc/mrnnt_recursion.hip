@@ -249,6 +249,9 @@ __device__ __forceinline__ void alpha_pass_halo(const DevProblem &p, int b, floa
         mn[d] = BAND ? p.min_s[c0 + tt] : 0;
         mx[d] = BAND ? p.max_s[c0 + tt] : S;
     }
+    double *ap = p.alpha + r0;                                           // alpha row of the next frame
+    const double *pbp = p.lpb + r0 + (int64_t)min(D, T - 1) * W;         // lp rows of the next prefetch
+    const double *pep = p.lpe + r0 + (int64_t)min(D, T - 1) * W - 1;
     auto step_lean = [&](int t, int d) {
         // unrestricted: no band mask -- a cell above the band only ever sees -inf predecessors (so it is -inf), a
         // cell below it only feeds cells below it and is never read (mrnnt_read_state masks it for inspection);
@@ -264,12 +267,20 @@ __device__ __forceinline__ void alpha_pass_halo(const DevProblem &p, int b, floa
             // the halo lanes of wave 0 stand for cells s < 0 and feed cell 0: they stay -inf
             a = (HL > 0 && s0 < 0) ? NEG_INF_D : v;
         }
-        if (own) (p.alpha + (r0 + (int64_t)t * W))[sl] = a;
-        const int tn = min(t + D, T - 1);
-        pb[d] = (p.lpb + (r0 + (int64_t)tn * W))[sl];
-        pe[d] = (p.lpe + (r0 + (int64_t)tn * W - 1))[sl];
-        mn[d] = BAND ? p.min_s[c0 + tn] : 0;
-        mx[d] = BAND ? p.max_s[c0 + tn] : S;
+        // row pointers advance by W per frame (no per-frame 64-bit multiply on the scalar unit)
+        if (own) ap[sl] = a;
+        ap += W;
+        pb[d] = pbp[sl];
+        pe[d] = pep[sl];
+        if (t + D < T - 1) {
+            pbp += W;
+            pep += W;
+        }
+        if (BAND) {
+            const int tn = min(t + D, T - 1);
+            mn[d] = p.min_s[c0 + tn];
+            mx[d] = p.max_s[c0 + tn];
+        }
     };
     auto step = [&](int t, int d) {
         if (LEAN) {
@@ -346,6 +357,9 @@ __device__ __forceinline__ void beta_pass_halo(const DevProblem &p, int b, doubl
         mn[d] = (BAND && tt > 0) ? p.min_s[c0 + tt - 1] : 0;
         mx[d] = (BAND && tt > 0) ? p.max_s[c0 + tt - 1] : S;
     }
+    double *bp_ = p.beta + r0 + (int64_t)(T - 1) * W;                   // beta row of the next frame (downwards)
+    const double *pbp = p.lpb + r0 + (int64_t)max(T - 1 - D, 0) * W;     // lp rows of the next prefetch
+    const double *pep = p.lpe + r0 + (int64_t)max(T - 1 - D, 0) * W;
     auto step_lean = [&](int t, int d) {
         // unrestricted: no band mask -- a cell below the band only sees -inf successors, one above it (s > t) only
         // feeds cells above it and is never read (mrnnt_read_state masks it for inspection)
@@ -364,12 +378,19 @@ __device__ __forceinline__ void beta_pass_halo(const DevProblem &p, int b, doubl
             // 63's successor is -inf and so are they)
             bn = (HL > 0 && s0 > S) ? NEG_INF_D : v;
         }
-        if (own) (p.beta + (r0 + (int64_t)t * W))[sl] = bn;
-        const int tn = max(t - D, 0);
-        pb[d] = (p.lpb + (r0 + (int64_t)tn * W))[sl];
-        pe[d] = (p.lpe + (r0 + (int64_t)tn * W))[sl];
-        mn[d] = (BAND && tn > 0) ? p.min_s[c0 + tn - 1] : 0;
-        mx[d] = (BAND && tn > 0) ? p.max_s[c0 + tn - 1] : S;
+        if (own) bp_[sl] = bn;
+        bp_ -= W;
+        pb[d] = pbp[sl];
+        pe[d] = pep[sl];
+        if (t - D > 0) {
+            pbp -= W;
+            pep -= W;
+        }
+        if (BAND) {
+            const int tn = max(t - D, 0);
+            mn[d] = tn > 0 ? p.min_s[c0 + tn - 1] : 0;
+            mx[d] = tn > 0 ? p.max_s[c0 + tn - 1] : S;
+        }
     };
     auto step = [&](int t, int d) {
         if (LEAN) {
