@@ -80,8 +80,9 @@ size_t joint_min_lds_bytes(int H, int V);
 
 // Launch-shape knobs (experiment hook: mrnnt_tune in mrnnt_capi.cpp). Defaults are the tuned values.
 struct Tuning {
-    int softmax_variant = 13;     // log-softmax kernel: 13 -> lean kernel, 2 (4 for rows of < 96 vectors) rows per
-                                  // wave, wave max first for single-chunk rows; 16 -> the same with a running max for
+    int softmax_variant = 13;     // log-softmax kernel: 13 -> rows of <= 64 vectors on 16-lane groups (4 rows per
+                                  // wave), longer single-chunk rows per wave with the wave max first, longer rows with
+                                  // a running max, 2 rows per wave; 21 -> no 16-lane groups; 16 -> running max for
                                   // every row; 14 / 15 -> running max, 1 / 4 rows; 0/2 -> first kernel, 1/2 rows
     int grad_variant = 5;         // gradient kernel: 5 -> staged coefficients (1 / 2 / 4 rows per wave for rows of
                                   // >= 192 / >= 96 / fewer vectors; short rows loaded nontemporally: per-row

@@ -327,6 +327,108 @@ __global__ __launch_bounds__(256) void softmax_lean_kernel(DevProblem p) {
     }
 }
 
+// 16-lane rows (the default for rows of <= 64 vectors: f32 V <= 256, bf16 / fp16 V <= 512; softmax_variant 13 /
+// 22, 23 = two rows per group per pass; configs[1]: 23.7 -> 19.4 us against one wave per row, wave max first). A wave reduces
+// four rows at once, one per 16-lane DPP row, so the max and sum reductions are four DPP steps inside the
+// hardware row (quad_perm x2, half-row mirror, row mirror) serving all four rows per instruction -- against six
+// DPP steps + a readlane per row and reduction when a whole wave holds one row. The blank / label logits (4-byte
+// loads issued with the row) and den / lpb / lpe stay per row in lane 0 of each 16-lane group. NR: rows per lane
+// group per pass (NR * 4 rows per wave in flight).
+template <int CTRL>
+__device__ __forceinline__ float dpp16(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+
+template <class IO, int NR, bool NTL>
+__global__ __launch_bounds__(256) void softmax_row16_kernel(DevProblem p) {
+    zero_lp_pads(p);
+    constexpr int E = IO::E;
+    typedef typename IO::V Vec;
+    typedef typename IO::S Sc;
+    const int lane = threadIdx.x & 63;
+    const int g = lane >> 4, l16 = lane & 15;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int VL = p.V / E;  // <= 64: up to 4 vectors per lane of a group
+    const Vec *__restrict__ av = reinterpret_cast<const Vec *>(p.acts);
+    const Sc *__restrict__ as = reinterpret_cast<const Sc *>(p.acts);
+    const int blank = p.blank;
+    const Vec ninf = splat<IO>(NEG_INF_F);
+
+    for (int64_t ci = blockIdx.x; ci < p.num_cols; ci += gridDim.x) {
+        const int64_t c = p.col_mul ? (ci * p.col_mul) % p.num_cols : ci;
+        const int b = p.col_b[c];
+        const int T = p.T[b], S = p.S[b];
+        const int t = (int)(c - p.col_off[b]);
+        const int64_t rowc = p.row_off[b] + (int64_t)t * (S + 1);
+        const int64_t arow = acts_col_base(p, b, t, rowc);
+        int lo = max(0, t - (T - S)), hi = min(t, S);
+        align_window(p, c, t, lo, hi);
+        const int *__restrict__ lab_b = p.labels + (int64_t)b * p.label_stride;
+        zero_fill_outside_band(p, rowc, S, lo, hi);
+
+        // wave w, pass k: rows lo + 16 k + 4 NR w + 4 r + g (r < NR) -- a row per 16-lane group
+        for (int s0 = lo + wave * 4 * NR; s0 <= hi; s0 += 16 * NR) {
+            Vec x[NR][4];
+            float zb[NR], ze[NR];
+            bool ok[NR];
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const int s = s0 + 4 * r + g;
+                ok[r] = s <= hi;
+                const int64_t ar = (arow + s) * (int64_t)VL;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int j = l16 + 16 * u;
+                    x[r][u] = (ok[r] && j < VL) ? vload<NTL>(&av[ar + j]) : ninf;
+                }
+                zb[r] = 0.0f;
+                ze[r] = 0.0f;
+                if (ok[r] && l16 == 0) {  // the two logits the recursion needs, loaded with the row
+                    const int64_t ae = (arow + s) * (int64_t)p.V;
+                    zb[r] = IO::to_f(as[ae + blank]);
+                    const bool has = s < S;
+                    const int lab = checked_label(has, has ? lab_b[s] : 0, p.V, ze[r]);
+                    if (lab >= 0) ze[r] = IO::to_f(as[ae + lab]);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                float xf[4 * E];
+                float m = NEG_INF_F;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    float t4[E];
+                    IO::unpack(x[r][u], t4);
+#pragma unroll
+                    for (int i = 0; i < E; ++i) {
+                        xf[u * E + i] = t4[i];
+                        m = fmaxf(m, t4[i]);
+                    }
+                }
+                m = fmaxf(m, dpp16<0xB1>(m));   // quad_perm [1,0,3,2]
+                m = fmaxf(m, dpp16<0x4E>(m));   // quad_perm [2,3,0,1]
+                m = fmaxf(m, dpp16<0x141>(m));  // row_half_mirror
+                m = fmaxf(m, dpp16<0x140>(m));  // row_mirror: every lane of the 16-lane row holds its max
+                const float off = -((m == NEG_INF_F) ? 0.0f : m) * kLog2e;
+                float acc = 0.0f;
+#pragma unroll
+                for (int k = 0; k < 4 * E; ++k) acc += fast_exp2(fmaf(xf[k], kLog2e, off));
+                acc += dpp16<0xB1>(acc);
+                acc += dpp16<0x4E>(acc);
+                acc += dpp16<0x141>(acc);
+                acc += dpp16<0x140>(acc);
+                if (ok[r] && l16 == 0) {
+                    const int64_t row = rowc + s0 + 4 * r + g;
+                    const double den = -(double)m - log_row_sum(acc);
+                    p.den[row] = (float)den;
+                    p.lpb[row] = (double)zb[r] + den;
+                    p.lpe[row] = (double)ze[r] + den;
+                }
+            }
+        }
+    }
+}
+
 // Scalar path (any V, any alignment, any element type): one row per wave, lanes stride over v.
 template <class IO>
 __global__ __launch_bounds__(256) void softmax_scalar_kernel(DevProblem p) {
@@ -387,7 +489,12 @@ static void launch_u(const DevProblem &p, int grid, hipStream_t stream) {
         else softmax_kernel<IO, U, 2, NTL><<<grid, 256, 0, stream>>>(p);
         return;
     }
-    if (v == 13 && VL <= 64 * U) {  // single-chunk rows (the default): wave max first, 4 / 2 rows per wave
+    if ((v == 13 || v == 22 || v == 23) && VL <= 64) {  // 16-lane rows (the default), 1 / 2 rows per group per pass
+        if (v != 23) softmax_row16_kernel<IO, 1, NTL><<<grid, 256, 0, stream>>>(p);
+        else softmax_row16_kernel<IO, 2, NTL><<<grid, 256, 0, stream>>>(p);
+        return;
+    }
+    if ((v == 13 || v == 21) && VL <= 64 * U) {  // single-chunk rows (the default): wave max first, 4 / 2 rows per wave
         constexpr int RO = U == 1 ? 4 : 2;
         if (full) softmax_lean_kernel<IO, U, RO, NTL, true, true><<<grid, 256, 0, stream>>>(p);
         else softmax_lean_kernel<IO, U, RO, NTL, false, true><<<grid, 256, 0, stream>>>(p);
