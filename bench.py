@@ -413,7 +413,11 @@ def run(args, world):
         try:
             pm = json.load(open(pmc_path))
             ek = {"f32": "IoF32", "bf16": "IoBF16", "f16": "IoF16"}[args.acts_dtype]
-            if pm.get("config") == args.config and pm.get("kernel", "").startswith(f"grad_staged_kernel<{ek}"):
+            # the counter record belongs to this exact workload only: same config and acts dtype, and the same
+            # live-row bytes per launch (an alignment band, a shard or chunking all change those)
+            if (pm.get("config") == args.config and pm.get("dtype") == args.acts_dtype
+                    and pm.get("kernel", "").startswith(f"grad_staged_kernel<{ek}")
+                    and pm.get("algorithmic_bytes_per_launch") == grad_bytes // n_chunks):
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
