@@ -251,3 +251,4 @@ def test_headline_alignment_restricted(headline):
     assert np.abs(g[:rows_per].cpu().numpy() - gr).max() <= 1e-4
     del g
     torch.cuda.empty_cache()
+
