@@ -340,7 +340,7 @@ RNNTStatus mrnnt_forward(const mrnnt_problem *p, void *ws, size_t ws_bytes, floa
         if (e != hipSuccess) return fail_hip(e, "alignment band kernels");
     }
     const int grid = streaming_grid(pl.cols, tuning().softmax_grid_per_cu);
-    d.col_mul = (tuning().col_scatter & 1) ? scatter_mul(pl.cols) : 0;
+    d.col_mul = (tuning().col_xcd & 1) ? -1 : (tuning().col_scatter & 1) ? scatter_mul(pl.cols) : 0;
     e = timed(K_SOFTMAX, stream, [&] { return launch_softmax(d, pl.elem, grid, stream); });
     if (e != hipSuccess) return fail_hip(e, "log-softmax kernel");
     e = timed(K_DP, stream, [&] { return launch_dp(d, pl.S_max, with_beta ? 1 : 0, costs_dev, stream); });
@@ -357,7 +357,7 @@ RNNTStatus mrnnt_backward(const mrnnt_problem *p, const void *ws, const float *g
     if (!ws) return fail(RNNT_STATUS_INVALID_VALUE, "workspace is null");
     if (!grads) return fail(RNNT_STATUS_INVALID_VALUE, "grads is null");
     DevProblem d = make_dev(p, pl, ws);
-    d.col_mul = (tuning().col_scatter & 2) ? scatter_mul(pl.cols) : 0;
+    d.col_mul = (tuning().col_xcd & 2) ? -1 : (tuning().col_scatter & 2) ? scatter_mul(pl.cols) : 0;
     // grad_variant 3 sweeps rows (packed layout only), the others walk lattice columns
     const int grid = (tuning().grad_variant == 3 && pl.pad_S1 == 0)
                          ? streaming_grid(pl.N, std::max(1, tuning().grad_grid_per_cu))
@@ -702,6 +702,7 @@ __attribute__((visibility("default"))) int mrnnt_tune(const char *key, int value
     if (!std::strcmp(key, "softmax_variant")) slot = &t.softmax_variant;
     else if (!std::strcmp(key, "grad_variant")) slot = &t.grad_variant;
     else if (!std::strcmp(key, "col_scatter")) slot = &t.col_scatter;
+    else if (!std::strcmp(key, "col_xcd")) slot = &t.col_xcd;
     else if (!std::strcmp(key, "dp_halo")) slot = &t.dp_halo;
     else if (!std::strcmp(key, "dp_lean")) slot = &t.dp_lean;
     else if (!std::strcmp(key, "joint_reduce_sparse")) slot = &t.joint_reduce_sparse;

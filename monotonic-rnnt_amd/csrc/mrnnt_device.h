@@ -97,6 +97,18 @@ struct Cursor {
     }
 };
 
+// Column taken at visit ci of a streaming kernel's column walk. col_mul == 0: in order; > 0: scattered,
+// (ci * col_mul) % num_cols; < 0: XCD-chunked -- workgroups are dispatched round-robin over the 8 XCDs, so visit
+// ci runs on XCD ci % 8 (every grid is a multiple of 8 or one workgroup per column), and XCD x walks its own
+// contiguous eighth of the columns in order, x * q + min(x, r) + ci / 8 (q, r = num_cols / 8, % 8): the window of
+// acts an XCD's L2 and address-translation caches see at once is one region, not all eight XCDs' interleaved.
+__device__ __forceinline__ int64_t visit_col(const DevProblem &p, int64_t ci) {
+    if (p.col_mul == 0) return ci;
+    if (p.col_mul > 0) return (ci * p.col_mul) % p.num_cols;
+    const int64_t n = p.num_cols, q = n >> 3, r = n & 7, x = ci & 7;
+    return x * q + (x < r ? x : r) + (ci >> 3);
+}
+
 // First acts/grads row of lattice column (b, t): packed layout (reference contract) = the internal
 // row rowc; padded [B, pad_T, pad_S1, V] layout = (b * pad_T + t) * pad_S1.
 __device__ __forceinline__ int64_t acts_col_base(const DevProblem &p, int b, int t, int64_t rowc) {

@@ -124,7 +124,7 @@ __global__ __launch_bounds__(256) void grad_staged_kernel(DevProblem p, const fl
     cur.b = blockIdx.x < p.num_cols ? p.col_b[blockIdx.x] : 0;
     int buf = 0;
     for (int64_t ci = blockIdx.x; ci < p.num_cols; ci += gridDim.x) {
-        const int64_t c = p.col_mul ? (ci * p.col_mul) % p.num_cols : ci;
+        const int64_t c = visit_col(p, ci);
         if (p.col_mul) cur.b = p.col_b[c];
         else cur.advance(p.col_off, c);
         const int b = cur.b;

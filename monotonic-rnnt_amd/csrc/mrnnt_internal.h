@@ -33,8 +33,8 @@ struct DevProblem {
     int64_t num_rows;           // N = sum_b T_b (S_b + 1)
     int64_t pad_T, pad_S1;      // padded acts layout (pad_S1 == 0: packed)
     int64_t scale_stride;       // upstream-gradient stride: grad_scale[b * scale_stride] (0 = one value for all)
-    int64_t col_mul;            // column visiting order of the streaming kernels: the i-th column visited is
-                                // (i * col_mul) % num_cols (0 = in order; col_mul coprime with num_cols)
+    int64_t col_mul;            // column visiting order of the streaming kernels (visit_col): 0 in order, > 0 the
+                                // i-th column visited is (i * col_mul) % num_cols (coprime), < 0 XCD-chunked
     float *den;                 // [N]  log-softmax denominator  -max - log sum exp(z - max)
     double *lpb;                // [N]  z[r, blank] + den[r]
     double *lpe;                // [N]  z[r, label(s)] + den[r]   (s < S)
@@ -103,6 +103,8 @@ struct Tuning {
                                   // per frame + lane offsets, bound-ctrl DPP shifts, no band mask); 0 -> masked step
     int col_scatter = 2;          // visit columns in a scattered order (DevProblem::col_mul): bit 0 log-softmax,
                                   // bit 1 gradient
+    int col_xcd = 0;              // XCD-chunked column order (visit_col, col_mul < 0; overrides col_scatter): bit 0
+                                  // log-softmax, bit 1 gradient
 };
 Tuning &tuning();
 

@@ -161,7 +161,7 @@ __global__ __launch_bounds__(256) void softmax_lean_kernel(DevProblem p) {
     const Vec ninf = splat<IO>(NEG_INF_F);
 
     for (int64_t ci = blockIdx.x; ci < p.num_cols; ci += gridDim.x) {
-        const int64_t c = p.col_mul ? (ci * p.col_mul) % p.num_cols : ci;
+        const int64_t c = visit_col(p, ci);
         const int b = p.col_b[c];
         const int T = p.T[b], S = p.S[b];
         const int t = (int)(c - p.col_off[b]);
@@ -355,7 +355,7 @@ __global__ __launch_bounds__(256) void softmax_row16_kernel(DevProblem p) {
     const Vec ninf = splat<IO>(NEG_INF_F);
 
     for (int64_t ci = blockIdx.x; ci < p.num_cols; ci += gridDim.x) {
-        const int64_t c = p.col_mul ? (ci * p.col_mul) % p.num_cols : ci;
+        const int64_t c = visit_col(p, ci);
         const int b = p.col_b[c];
         const int T = p.T[b], S = p.S[b];
         const int t = (int)(c - p.col_off[b]);

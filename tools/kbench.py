@@ -57,7 +57,7 @@ def main():
     # variant would otherwise carry over into the next one, round after round)
     SPECIAL = ("grads_buf", "acts_buf", "grads_offset_kb")
     keys = {"softmax_variant", "grad_variant", "softmax_grid_per_cu", "grad_grid_per_cu", "nt_store", "nt_load",
-            "occ_skip", "col_scatter", "dp_halo"} | {k for v in variants for k in v if k not in SPECIAL}
+            "occ_skip", "col_scatter", "col_xcd", "dp_halo"} | {k for v in variants for k in v if k not in SPECIAL}
     DEFAULTS = {k: L.tune(k) for k in sorted(keys)}
     bad = [k for k, v in DEFAULTS.items() if v < 0]
     assert not bad, f"unknown knobs {bad}"
