@@ -122,6 +122,9 @@ def parse():
     ap.add_argument("--graph", action="store_true",
                     help="capture forward + backward once in a HIP graph and time its replays (host-launch-bound "
                          "sizes such as configs[1]); per-kernel times then come from eager steps after the timing")
+    ap.add_argument("--device-lengths", action="store_true",
+                    help="pass input / label lengths as GPU tensors (the reference's calling convention, "
+                         "monotonic_rnnt.cu:85-88): planned without reading them back, lattice built on the device")
     ap.add_argument("--shard", default=None, metavar="R/N",
                     help="time only shard R of the N-way sharded config in this one process (strong-scaling "
                          "emulation on one GPU: the sharded path has no data-path collective; tools/shard_scaling.py)")
@@ -270,6 +273,9 @@ def run(args, world):
         workload += f", alignment-restricted (k={args.align_k}, labels evenly spaced)"
 
     T_t, S_t = torch.from_numpy(T), torch.from_numpy(S)
+    if args.device_lengths:
+        T_t, S_t = T_t.to(dev), S_t.to(dev)
+        workload += ", device-resident lengths"
     prof_steps = min(args.steps, 100) if args.graph else args.steps  # steps the per-kernel times cover
     if args.graph and mode != "resident":
         raise SystemExit("--graph needs a resident config")
@@ -449,6 +455,7 @@ def run(args, world):
                        "rows_per_gpu": rows, "inband_rows_per_gpu": n_band, "V": V,
                        "memory_mode": mode, "chunks_per_step": n_chunks,
                        "execution": "hip_graph_replay" if args.graph else "eager",
+                       "lengths": "device" if (args.device_lengths or mode != "resident") else "host",
                        **({"window_rows_per_gpu": n_window} if n_window is not None else {}),
                        "parallelism": f"dp{world} (batch-sharded, one 4-byte "
                                       f"{'gloo (rehearsal)' if gloo else 'RCCL'} loss all-reduce)"},

@@ -1,16 +1,23 @@
 // gpu_workspace_manager.h -- GpuRNNTWorkspaceManager<float>, the workspace object the reference's C
-// entry point takes (reference include/gpu_workspace_manager.h:15-346). Same constructor and public
-// methods; the implementation lives in libmonotonic_rnnt_amd.so (only the float instantiation exists,
-// which is the only one the reference's entry point accepts: src/rnnt_entrypoint.cpp:34).
+// entry point takes (reference include/gpu_workspace_manager.h:15-346). The reference's constructor and public
+// methods, including its host-side inspection getters (:87-190); the implementation lives in
+// libmonotonic_rnnt_amd.so (only the float instantiation exists, which is the only one the reference's entry point
+// accepts: src/rnnt_entrypoint.cpp:34).
 //
-// Pointer conventions follow the reference: acts, labels, T, S and alignments are DEVICE pointers.
-// Like the reference, the manager copies T and S to the host to size the workspace
-// (gpu_workspace_manager.h:87-96); unlike it, labels use row stride max(S) and the alignment row
-// stride max(T) exactly as the reference does (gpu_rnnt_kernel.h:133, gpu_workspace_manager.h:200).
+// Pointer conventions follow the reference: acts, labels, T, S and alignments are DEVICE pointers. Like the
+// reference, the manager copies T and S to the host to size the workspace (gpu_workspace_manager.h:87-96); labels
+// use row stride max(S) and the alignment row stride max(T), as the reference does (gpu_rnnt_kernel.h:133,
+// gpu_workspace_manager.h:200).
 //
-// Differences: the workspace layout is private (no public data members), and
-// restrict_to_alignment() records the alignment and builds the band on the device at compute time
-// instead of a host loop with blocking copies (gpu_workspace_manager.h:191-219).
+// Differences:
+//  * the workspace layout is private: the reference's public data members (workspace_, denom, alphas, betas,
+//    min_allowed_s, ...) are not exposed -- their contents are, through the getters below;
+//  * restrict_to_alignment() records the alignment, and the band is built on the device at compute time instead of
+//    a host loop with blocking copies (:191-219);
+//  * the getters read the state of the last cost() / cost_and_grad() on this workspace (betas / ll_backward only
+//    after cost_and_grad, as in the reference, whose cost() skips the beta pass). Cells outside the lattice band
+//    read -inf (the reference leaves them unwritten), and denom_host() covers every row as the reference's reduce
+//    does. Host copies are ordered on the computer's stream and synchronous, like the reference's cudaMemcpy.
 #ifndef MONOTONIC_RNNT_GPU_WORKSPACE_MANAGER_H
 #define MONOTONIC_RNNT_GPU_WORKSPACE_MANAGER_H
 
@@ -52,12 +59,24 @@ class GpuRNNTWorkspaceManager<float> : public RNNTWorkspaceManager {
     // blank_idx marks blank frames in it (reference :191-219). Takes effect on the next computation.
     void restrict_to_alignment(const int *const alignments, int max_shift, int blank_idx);
 
-    // Host-side getters (reference :87-190 subset)
+    // Host-side getters (reference :87-190)
     [[nodiscard]] int B_host() const;
     [[nodiscard]] int V_host() const;
     [[nodiscard]] std::vector<int> T_host() const;
     [[nodiscard]] std::vector<int> S_host() const;
-    [[nodiscard]] int num_denoms() const;
+    [[nodiscard]] int num_denoms() const;                 // sum_b T_b (S_b+1)
+    [[nodiscard]] int num_fwd_bwd_var_positions() const;  // the same count (dense alpha / beta storage)
+    [[nodiscard]] std::vector<int> var_start_offsets_host() const;  // [B] first row of each utterance
+    [[nodiscard]] std::vector<float> acts_host() const;   // [num_denoms() * V]
+    [[nodiscard]] std::vector<float> denom_host() const;  // [num_denoms()] -max - log sum exp of every row
+    [[nodiscard]] std::vector<float> alphas_host() const; // [num_denoms()] alpha(t, s) at var_start_offsets[b] + t(S_b+1) + s
+    [[nodiscard]] std::vector<float> betas_host() const;  // [num_denoms()] beta(t, s), same order
+    [[nodiscard]] int S_max_host() const;
+    [[nodiscard]] int T_max_host() const;
+    [[nodiscard]] std::vector<int> min_allowed_s_host() const;  // [B * T_max] alignment band (0 unrestricted)
+    [[nodiscard]] std::vector<int> max_allowed_s_host() const;  // [B * T_max] (S_b unrestricted)
+    [[nodiscard]] std::vector<float> ll_forward_host() const;   // [B] alpha(T_b-1, S_b)
+    [[nodiscard]] std::vector<float> ll_backward_host() const;  // [B] beta(0, 0)
 
     mrnnt_gpu_ws_state *state() const { return st_; }
 

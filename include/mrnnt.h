@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MRNNT_VERSION 6
+#define MRNNT_VERSION 7
 
 /* acts / grads element types */
 #define MRNNT_F32 0
@@ -65,7 +65,23 @@ typedef struct mrnnt_problem {
     /* --- version 6 --- */
     int grad_scale_broadcast; /* 1: grad_scale[0] scales every utterance (a stride-0 upstream gradient, e.g. the
                                 backward of costs.sum(): no copy into a [B] vector); 0: grad_scale[b] */
+    /* --- version 7 --- */
+    int lengths_on_device;   /* 1: the lengths exist only on the device (T_dev / S_dev; T_host / S_host may be NULL),
+                                as the reference's GPU binding requires (monotonic_rnnt.cu:85-88). The launch is then
+                                planned from bounds the host knows without reading them back -- num_rows (required:
+                                the packed rows, or B*pad_T*pad_S1 padded) and label_stride (>= every S_b) -- and the
+                                lattice offsets are built and the lengths validated on the device (T_b > 0, S_b >= 0,
+                                T_b >= S_b, S_b <= label_stride, packed rows == num_rows, padded / alignment strides).
+                                No host synchronisation; capturable in a HIP graph. lattice must be NULL. A length set
+                                that fails validation makes every cost and gradient of the call NaN (nothing outside
+                                the caller's buffers is touched) and raises *status_host. */
+    int *status_host;        /* optional, with lengths_on_device: a host word from mrnnt_status_word(); the device
+                                stores RNNT_STATUS_INVALID_VALUE into it when validation fails (never clears it) */
 } mrnnt_problem;
+
+/* A process-wide host-mapped int (initially 0) the device can store into without a copy: pass it as
+ * mrnnt_problem.status_host and poll it from the host at leisure (reset it to 0 yourself). */
+int *mrnnt_status_word(void);
 
 /* Validate lengths (reference semantics: B > 0, V > 0, T_b > 0, S_b >= 0, T_b >= S_b) and return the
  * device workspace bytes needed by mrnnt_forward / mrnnt_backward for this problem. Host-only. */
@@ -108,6 +124,21 @@ RNNTStatus mrnnt_read_loglik(const mrnnt_problem *p, const void *workspace, doub
  * t (S_b+1) + s. Device buffers of N elements; any may be NULL. Asynchronous on `stream`. */
 RNNTStatus mrnnt_read_state(const mrnnt_problem *p, const void *workspace, float *den_dev, double *alpha_dev,
                             double *beta_dev, hipStream_t stream);
+
+/* Log-softmax denominator of EVERY lattice row, den[r] = -max_v z - log sum_v exp(z - max) in the packed row
+ * order of mrnnt_read_state (the reference's denom_host(), gpu_workspace_manager.h:137-141, whose reduce covers
+ * all rows): the rows the last mrnnt_forward reduced are copied from the workspace, the others (outside the band or
+ * the alignment window, which the forward never reads) are reduced from acts here. den_dev: device fp32 [N].
+ * Asynchronous on `stream`. */
+RNNTStatus mrnnt_read_denoms(const mrnnt_problem *p, const void *workspace, float *den_dev, hipStream_t stream);
+
+/* The alignment band of the problem in the reference's [B, ld] layout (gpu_workspace_manager.h:167-177,191-219):
+ * min_dev[b*ld + t] / max_dev[b*ld + t] = the lowest / highest label position alpha(t, .) may take, for t < T_b;
+ * 0 / S_b for t >= T_b and for every t without an alignment (the reference's initial values, :317-328). Builds the
+ * band in `workspace` from p->alignment (device kernels, as mrnnt_forward does), so it needs no preceding
+ * forward. ld >= max T_b; either output may be NULL. Asynchronous on `stream`. */
+RNNTStatus mrnnt_read_band(const mrnnt_problem *p, void *workspace, int *min_dev, int *max_dev, int64_t ld,
+                           hipStream_t stream);
 
 /* Message describing the last non-success status returned on this thread. */
 const char *mrnnt_last_error(void);

@@ -51,26 +51,66 @@ RNNTStatus fail_hip(hipError_t e, const char *where) {
 constexpr size_t kAlign = 256;
 size_t align_up(size_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
 
+// Launch plan of one problem. With host lengths every size is exact. With device-resident lengths
+// (lengths_on_device) the host plans from bounds it knows without a read-back: N = the rows of acts (packed: exact,
+// checked on the device; padded: B*pad_T*pad_S1), cols <= N (packed; every column holds >= 1 row) or B*pad_T
+// (padded), S_max <= label_stride; the setup kernel publishes the real values (DynWords) for the kernels.
 struct Plan {
     int B = 0, V = 0, S_max = 0, T_max = 0;
     int64_t N = 0, cols = 0;
     int elem = ELEM_F32;
     int64_t pad_T = 0, pad_S1 = 0;
     bool align = false;
+    bool dyn = false;
     size_t off_row, off_col, off_colb, off_mtmp, off_min, off_max, off_den, off_lpb, off_lpe, off_alpha, off_beta, off_ll,
-        off_llb, total;
+        off_llb, off_dyn, total;
 };
+
+RNNTStatus plan_device_lengths(const mrnnt_problem *p, Plan &q) {
+    if (!p->T_dev || !p->S_dev) return fail(RNNT_STATUS_INVALID_VALUE, "device lengths are required");
+    if (p->lattice)
+        return fail(RNNT_STATUS_INVALID_VALUE, "lattice must be NULL with lengths_on_device (built on the device)");
+    if (p->num_rows < 0) return fail(RNNT_STATUS_INVALID_VALUE, "num_rows is required with lengths_on_device");
+    if (p->label_stride < 0) return fail(RNNT_STATUS_INVALID_VALUE, "negative label row stride");
+    if (p->pad_S1 != 0) {
+        if (p->pad_S1 < 1 || p->pad_T < 1) return fail(RNNT_STATUS_INVALID_VALUE, "padded layout needs pad_T, pad_S1 >= 1");
+        q.N = (int64_t)p->B * p->pad_T * p->pad_S1;
+        q.cols = (int64_t)p->B * p->pad_T;
+        q.T_max = (int)std::min<int64_t>(p->pad_T, 1 << 30);
+        q.S_max = (int)std::min<int64_t>(p->label_stride, p->pad_S1 - 1);
+    } else {
+        q.N = p->num_rows;
+        q.cols = q.N;
+        q.T_max = (int)std::min<int64_t>(q.N, 1 << 30);
+        q.S_max = (int)std::min<int64_t>(p->label_stride, 1 << 30);
+    }
+    if (q.S_max + 1 > kMaxLabelsPlusOne)
+        return fail(RNNT_STATUS_INVALID_VALUE, "with device lengths the label row stride (" +
+                                                   std::to_string(p->label_stride) + ") bounds S_b and must be <= " +
+                                                   std::to_string(kMaxLabelsPlusOne - 1) +
+                                                   ": pass labels no wider than the longest label sequence");
+    if (p->num_rows != q.N)
+        return fail(RNNT_STATUS_INVALID_VALUE, "acts has " + std::to_string(p->num_rows) + " rows but the padded layout needs " +
+                                                   std::to_string(q.N));
+    return RNNT_STATUS_SUCCESS;
+}
 
 RNNTStatus make_plan(const mrnnt_problem *p, Plan *pl) {
     if (!p) return fail(RNNT_STATUS_INVALID_VALUE, "null problem");
     if (p->B <= 0) return fail(RNNT_STATUS_INVALID_VALUE, "B must be > 0");
     if (p->V <= 0) return fail(RNNT_STATUS_INVALID_VALUE, "V must be > 0");
-    if (!p->T_host || !p->S_host) return fail(RNNT_STATUS_INVALID_VALUE, "host lengths are required");
+    const bool dyn = p->lengths_on_device != 0;
+    if (!dyn && (!p->T_host || !p->S_host)) return fail(RNNT_STATUS_INVALID_VALUE, "host lengths are required");
     if (p->blank < 0 || p->blank >= p->V) return fail(RNNT_STATUS_INVALID_VALUE, "blank label out of range [0, V)");
     Plan q;
     q.B = p->B;
     q.V = p->V;
-    for (int b = 0; b < p->B; ++b) {
+    q.dyn = dyn;
+    if (dyn) {
+        const RNNTStatus st = plan_device_lengths(p, q);
+        if (st != RNNT_STATUS_SUCCESS) return st;
+    }
+    for (int b = 0; !dyn && b < p->B; ++b) {
         const int T = p->T_host[b], S = p->S_host[b];
         // reference validation: cpu_workspace_manager.h:103-107 / gpu_workspace_manager.h:235-239
         if (T <= 0 || S < 0 || T < S)
@@ -86,19 +126,24 @@ RNNTStatus make_plan(const mrnnt_problem *p, Plan *pl) {
         return fail(RNNT_STATUS_INVALID_VALUE, "max label length " + std::to_string(q.S_max) + " exceeds " +
                                                    std::to_string(kMaxLabelsPlusOne - 1));
     // the kernels read labels[b * label_stride + s] for s < S_b and alignment[b * align_stride + t] for t < T_b
+    // (with device lengths the setup kernel checks S_b <= label_stride and T_b <= align_stride)
     if (q.S_max > 0 && p->label_stride < q.S_max)
         return fail(RNNT_STATUS_INVALID_VALUE, "label row stride " + std::to_string(p->label_stride) +
                                                    " < max label length " + std::to_string(q.S_max));
-    if (p->alignment && p->align_stride < q.T_max)
+    if (!dyn && p->alignment && p->align_stride < q.T_max)
         return fail(RNNT_STATUS_INVALID_VALUE, "alignment row stride " + std::to_string(p->align_stride) +
                                                    " < max input length " + std::to_string(q.T_max));
+    if (dyn && p->alignment && p->align_stride < 1)
+        return fail(RNNT_STATUS_INVALID_VALUE, "alignment row stride must be >= 1");
     if (p->acts_dtype != ELEM_F32 && p->acts_dtype != ELEM_BF16 && p->acts_dtype != ELEM_F16)
         return fail(RNNT_STATUS_INVALID_VALUE, "unknown acts_dtype " + std::to_string(p->acts_dtype));
     q.elem = p->acts_dtype;
     q.pad_T = p->pad_T;
     q.pad_S1 = p->pad_S1;
     int64_t acts_rows = q.N;
-    if (q.pad_S1 != 0) {
+    if (dyn) {
+        // sizes are bounds (plan_device_lengths); nothing more to check on the host
+    } else if (q.pad_S1 != 0) {
         if (q.pad_S1 < (int64_t)q.S_max + 1 || q.pad_T < q.T_max)
             return fail(RNNT_STATUS_INVALID_VALUE, "padded layout [B, " + std::to_string(q.pad_T) + ", " +
                                                        std::to_string(q.pad_S1) + ", V] too small for max T " +
@@ -119,9 +164,6 @@ RNNTStatus make_plan(const mrnnt_problem *p, Plan *pl) {
     q.off_row = take(sizeof(int64_t) * (q.B + 1));
     q.off_col = take(sizeof(int64_t) * (q.B + 1));
     q.off_colb = take(sizeof(int) * q.cols);
-    q.off_mtmp = q.align ? take(sizeof(int) * (q.cols + q.B)) : 0;
-    q.off_min = q.align ? take(sizeof(int) * q.cols) : 0;
-    q.off_max = q.align ? take(sizeof(int) * q.cols) : 0;
     q.off_den = take(sizeof(float) * q.N);
     q.off_lpb = take(sizeof(double) * (q.N + 2 * kLpPad));
     q.off_lpe = take(sizeof(double) * (q.N + 2 * kLpPad));
@@ -129,8 +171,37 @@ RNNTStatus make_plan(const mrnnt_problem *p, Plan *pl) {
     q.off_beta = take(sizeof(double) * q.N);
     q.off_ll = take(sizeof(double) * q.B);
     q.off_llb = take(sizeof(double) * q.B);
+    // the alignment band after the per-row state, so the state's offsets do not depend on the alignment flag (the
+    // C++ manager's band getter rebuilds the band in a workspace that holds the state of an earlier computation)
+    q.off_mtmp = q.align ? take(sizeof(int) * (q.cols + q.B)) : 0;
+    q.off_min = q.align ? take(sizeof(int) * q.cols) : 0;
+    q.off_max = q.align ? take(sizeof(int) * q.cols) : 0;
+    q.off_dyn = q.dyn ? take(sizeof(DynWords)) : 0;
     q.total = o;
     *pl = q;
+    return RNNT_STATUS_SUCCESS;
+}
+
+// mrnnt_status_word(): one host-mapped word per process, and its device address
+std::mutex g_status_mu;
+int *g_status_host = nullptr;
+int *g_status_dev = nullptr;
+
+// Device address of a caller's status word (host-mapped memory), nullptr for none.
+RNNTStatus status_device_ptr(const mrnnt_problem *p, int **dev) {
+    *dev = nullptr;
+    if (!p->status_host) return RNNT_STATUS_SUCCESS;
+    {
+        std::lock_guard<std::mutex> lk(g_status_mu);
+        if (p->status_host == g_status_host) {
+            *dev = g_status_dev;
+            return RNNT_STATUS_SUCCESS;
+        }
+    }
+    void *d = nullptr;
+    if (hipHostGetDevicePointer(&d, p->status_host, 0) != hipSuccess || !d)
+        return fail(RNNT_STATUS_INVALID_VALUE, "status_host is not host-mapped memory (use mrnnt_status_word())");
+    *dev = static_cast<int *>(d);
     return RNNT_STATUS_SUCCESS;
 }
 
@@ -182,8 +253,22 @@ DevProblem make_dev(const mrnnt_problem *p, const Plan &pl, const void *ws) {
     d.beta = reinterpret_cast<double *>(w + pl.off_beta);
     d.ll = reinterpret_cast<double *>(w + pl.off_ll);
     d.llb = reinterpret_cast<double *>(w + pl.off_llb);
+    d.dyn = pl.dyn ? reinterpret_cast<DynWords *>(w + pl.off_dyn) : nullptr;
+    d.steal = 0;
     return d;
 }
+
+// Column order of a streaming pass (DevProblem::col_mul): XCD-chunked (< 0), scattered (> 0: with device lengths a
+// marker the kernels replace by the device's multiplier, resolve_dyn) or in order (0). bit: 1 log-softmax, 2 gradient.
+int64_t column_order(const Plan &pl, int bit) {
+    if (tuning().col_xcd & bit) return -1;
+    if (!(tuning().col_scatter & bit)) return 0;
+    return pl.dyn ? 1 : scatter_mul(pl.cols);
+}
+
+// Workgroups of 4 waves per CU of the log-softmax's persistent, work-stealing grid (device-resident lengths: the
+// host does not know the column count to launch one workgroup per column)
+constexpr int kStealGridPerCU = 16;
 
 RNNTStatus check_pointers(const mrnnt_problem *p) {
     if (!p->acts) return fail(RNNT_STATUS_INVALID_VALUE, "acts is null");
@@ -323,7 +408,30 @@ RNNTStatus mrnnt_forward(const mrnnt_problem *p, void *ws, size_t ws_bytes, floa
     DevProblem d = make_dev(p, pl, ws);
     char *w = static_cast<char *>(ws);
     hipError_t e = hipSuccess;
-    if (!p->lattice) {  // lattice offsets on the device (the log-softmax kernel zeroes the lp pads itself)
+    if (pl.dyn) {  // device-resident lengths: offsets, column map and validation in one launch, no read-back
+        DynSetupArgs a;
+        std::memset(&a, 0, sizeof(a));
+        if ((st = status_device_ptr(p, &a.status_host)) != RNNT_STATUS_SUCCESS) return st;
+        a.T = p->T_dev;
+        a.S = p->S_dev;
+        a.B = pl.B;
+        a.packed = pl.pad_S1 == 0;
+        a.rows = pl.N;
+        a.cols_cap = pl.cols;
+        a.S_cap = pl.S_max;
+        a.T_cap = pl.pad_S1 ? pl.pad_T : 0;
+        if (p->alignment) a.T_cap = a.T_cap ? std::min<int64_t>(a.T_cap, p->align_stride) : p->align_stride;
+        a.S1_cap = pl.pad_S1;
+        a.scatter = (tuning().col_scatter & 3) != 0 && !(tuning().col_xcd & 3);
+        a.row_off = reinterpret_cast<int64_t *>(w + pl.off_row);
+        a.col_off = reinterpret_cast<int64_t *>(w + pl.off_col);
+        a.col_b = reinterpret_cast<int *>(w + pl.off_colb);
+        a.lpb = d.lpb;
+        a.lpe = d.lpe;
+        a.dyn = d.dyn;
+        e = timed(K_SETUP, stream, [&] { return launch_setup_dyn(a, stream); });
+        if (e != hipSuccess) return fail_hip(e, "device-lengths setup kernel");
+    } else if (!p->lattice) {  // lattice offsets on the device (the log-softmax kernel zeroes the lp pads itself)
         e = timed(K_SETUP, stream, [&] {
             return launch_setup(p->T_dev, p->S_dev, pl.B, reinterpret_cast<int64_t *>(w + pl.off_row),
                                 reinterpret_cast<int64_t *>(w + pl.off_col),
@@ -339,8 +447,12 @@ RNNTStatus mrnnt_forward(const mrnnt_problem *p, void *ws, size_t ws_bytes, floa
         });
         if (e != hipSuccess) return fail_hip(e, "alignment band kernels");
     }
-    const int grid = streaming_grid(pl.cols, tuning().softmax_grid_per_cu);
-    d.col_mul = (tuning().col_xcd & 1) ? -1 : (tuning().col_scatter & 1) ? scatter_mul(pl.cols) : 0;
+    int grid = streaming_grid(pl.cols, tuning().softmax_grid_per_cu);
+    if (pl.dyn && tuning().softmax_grid_per_cu <= 0) {  // one workgroup per column needs the column count
+        grid = streaming_grid(pl.cols, kStealGridPerCU);
+        d.steal = grid < pl.cols;
+    }
+    d.col_mul = column_order(pl, 1);
     e = timed(K_SOFTMAX, stream, [&] { return launch_softmax(d, pl.elem, grid, stream); });
     if (e != hipSuccess) return fail_hip(e, "log-softmax kernel");
     e = timed(K_DP, stream, [&] { return launch_dp(d, pl.S_max, with_beta ? 1 : 0, costs_dev, stream); });
@@ -357,7 +469,7 @@ RNNTStatus mrnnt_backward(const mrnnt_problem *p, const void *ws, const float *g
     if (!ws) return fail(RNNT_STATUS_INVALID_VALUE, "workspace is null");
     if (!grads) return fail(RNNT_STATUS_INVALID_VALUE, "grads is null");
     DevProblem d = make_dev(p, pl, ws);
-    d.col_mul = (tuning().col_xcd & 2) ? -1 : (tuning().col_scatter & 2) ? scatter_mul(pl.cols) : 0;
+    d.col_mul = column_order(pl, 2);
     // grad_variant 3 sweeps rows (packed layout only), the others walk lattice columns
     const int grid = (tuning().grad_variant == 3 && pl.pad_S1 == 0)
                          ? streaming_grid(pl.N, std::max(1, tuning().grad_grid_per_cu))
@@ -410,6 +522,80 @@ RNNTStatus mrnnt_read_state(const mrnnt_problem *p, const void *ws, float *den_d
     if ((alpha_dev || beta_dev) && launch_mask_state(d, alpha_dev, beta_dev, stream) != hipSuccess)
         return fail(RNNT_STATUS_EXECUTION_FAILED, "mask state");
     return RNNT_STATUS_SUCCESS;
+}
+
+RNNTStatus mrnnt_read_denoms(const mrnnt_problem *p, const void *ws, float *den_dev, hipStream_t stream) {
+    Plan pl;
+    RNNTStatus st = make_plan(p, &pl);
+    if (st != RNNT_STATUS_SUCCESS) return st;
+    if ((st = check_pointers(p)) != RNNT_STATUS_SUCCESS) return st;
+    if (!ws || !den_dev) return fail(RNNT_STATUS_INVALID_VALUE, "workspace / den is null");
+    const hipError_t e = launch_den_all(make_dev(p, pl, ws), pl.elem, den_dev, stream);
+    if (e != hipSuccess) return fail_hip(e, "denominator read-out kernel");
+    return RNNT_STATUS_SUCCESS;
+}
+
+RNNTStatus mrnnt_read_band(const mrnnt_problem *p, void *ws, int *min_dev, int *max_dev, int64_t ld,
+                           hipStream_t stream) {
+    Plan pl;
+    RNNTStatus st = make_plan(p, &pl);
+    if (st != RNNT_STATUS_SUCCESS) return st;
+    if (!ws) return fail(RNNT_STATUS_INVALID_VALUE, "workspace is null");
+    if (!p->T_dev || !p->S_dev) return fail(RNNT_STATUS_INVALID_VALUE, "device lengths are required");
+    if (ld < 1 || (!pl.dyn && ld < pl.T_max))
+        return fail(RNNT_STATUS_INVALID_VALUE, "band row stride " + std::to_string(ld) + " < max input length");
+    DevProblem d = make_dev(p, pl, ws);
+    char *w = static_cast<char *>(ws);
+    hipError_t e = hipSuccess;
+    if (pl.dyn) {  // offsets + validation exactly as mrnnt_forward builds them
+        DynSetupArgs a;
+        std::memset(&a, 0, sizeof(a));
+        a.T = p->T_dev;
+        a.S = p->S_dev;
+        a.B = pl.B;
+        a.packed = pl.pad_S1 == 0;
+        a.rows = pl.N;
+        a.cols_cap = pl.cols;
+        a.S_cap = pl.S_max;
+        a.T_cap = pl.pad_S1 ? pl.pad_T : 0;
+        if (p->alignment) a.T_cap = a.T_cap ? std::min<int64_t>(a.T_cap, p->align_stride) : p->align_stride;
+        a.S1_cap = pl.pad_S1;
+        a.row_off = reinterpret_cast<int64_t *>(w + pl.off_row);
+        a.col_off = reinterpret_cast<int64_t *>(w + pl.off_col);
+        a.col_b = reinterpret_cast<int *>(w + pl.off_colb);
+        a.dyn = d.dyn;
+        e = launch_setup_dyn(a, stream);
+    } else if (!p->lattice) {
+        e = launch_setup(p->T_dev, p->S_dev, pl.B, reinterpret_cast<int64_t *>(w + pl.off_row),
+                         reinterpret_cast<int64_t *>(w + pl.off_col), reinterpret_cast<int *>(w + pl.off_colb), nullptr,
+                         nullptr, 0, stream);
+    }
+    if (e != hipSuccess) return fail_hip(e, "setup kernel");
+    if (pl.align) {
+        e = launch_align(d, p->alignment, p->align_stride, p->align_blank, p->max_shift,
+                         reinterpret_cast<int *>(w + pl.off_mtmp), reinterpret_cast<int *>(w + pl.off_min),
+                         reinterpret_cast<int *>(w + pl.off_max), stream);
+        if (e != hipSuccess) return fail_hip(e, "alignment band kernels");
+    }
+    if ((e = launch_band_read(d, min_dev, max_dev, ld, stream)) != hipSuccess) return fail_hip(e, "band read-out kernel");
+    return RNNT_STATUS_SUCCESS;
+}
+
+int *mrnnt_status_word(void) {
+    std::lock_guard<std::mutex> lk(g_status_mu);
+    if (!g_status_host) {
+        void *h = nullptr, *d = nullptr;
+        if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent) != hipSuccess)
+            return nullptr;
+        if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+            (void)hipHostFree(h);
+            return nullptr;
+        }
+        std::memset(h, 0, 64);
+        g_status_host = static_cast<int *>(h);
+        g_status_dev = static_cast<int *>(d);
+    }
+    return g_status_host;
 }
 
 RNNTStatus mrnnt_grad_live_rows(const mrnnt_problem *p, const void *ws, unsigned long long *count_dev,
@@ -741,18 +927,23 @@ struct mrnnt_gpu_ws_state {
     const int *alignment = nullptr;
     int max_shift = 0;
     int align_blank = 0;
+    // the last computation on the workspace (what the inspection getters read back)
+    bool computed = false;
+    bool with_beta = false;
+    int blank = 0;
+    hipStream_t stream = nullptr;
 };
 
 namespace {
 
-// Host copies of T/S (the reference does the same blocking D2H copies, gpu_workspace_manager.h:87-96).
-bool host_lengths(const mrnnt_gpu_ws_state *s, std::vector<int> &T, std::vector<int> &S) {
+// Host copies of T/S (the reference makes the same D2H copies, gpu_workspace_manager.h:87-96), ordered on `stream`.
+bool host_lengths(const mrnnt_gpu_ws_state *s, std::vector<int> &T, std::vector<int> &S, hipStream_t stream = nullptr) {
     T.assign(s->B, 0);
     S.assign(s->B, 0);
     if (s->B <= 0) return true;
-    if (hipMemcpy(T.data(), s->T_dev, sizeof(int) * s->B, hipMemcpyDeviceToHost) != hipSuccess) return false;
-    if (hipMemcpy(S.data(), s->S_dev, sizeof(int) * s->B, hipMemcpyDeviceToHost) != hipSuccess) return false;
-    return true;
+    if (hipMemcpyAsync(T.data(), s->T_dev, sizeof(int) * s->B, hipMemcpyDeviceToHost, stream) != hipSuccess) return false;
+    if (hipMemcpyAsync(S.data(), s->S_dev, sizeof(int) * s->B, hipMemcpyDeviceToHost, stream) != hipSuccess) return false;
+    return hipStreamSynchronize(stream) == hipSuccess;
 }
 
 mrnnt_problem problem_of(const mrnnt_gpu_ws_state *s, const std::vector<int> &T, const std::vector<int> &S,
@@ -798,16 +989,19 @@ RNNTStatus manager_compute(GpuRNNTWorkspaceManager<float> &wm, int blank, hipStr
     if (!costs) return fail(RNNT_STATUS_INVALID_VALUE, "costs is null");
     if (!s->workspace) return fail(RNNT_STATUS_INVALID_VALUE, "workspace not set (set_workspace/create_workspace)");
     std::vector<int> T, S;
-    if (!host_lengths(s, T, S)) return fail(RNNT_STATUS_MEMOPS_FAILED, "copying lengths to host");
+    if (!host_lengths(s, T, S, stream)) return fail(RNNT_STATUS_MEMOPS_FAILED, "copying lengths to host");
     size_t bytes = 0, coff = 0;
     RNNTStatus st = manager_size(s, T, S, &bytes, &coff);
     if (st != RNNT_STATUS_SUCCESS) return st;
     mrnnt_problem p = problem_of(s, T, S, blank);
     // this surface synchronises anyway (host costs): read the labels back and range-check them, as the flat
-    // entry points cannot without a sync (there an out-of-range device label gives a NaN cost)
+    // entry points cannot without a sync (there an out-of-range device label gives a non-finite cost). The copy
+    // is ordered on the caller's stream, after whatever produced the labels there.
     if (p.label_stride > 0) {
         std::vector<int> lab((size_t)s->B * p.label_stride);
-        if (hipMemcpy(lab.data(), s->labels, sizeof(int) * lab.size(), hipMemcpyDeviceToHost) != hipSuccess)
+        if (hipMemcpyAsync(lab.data(), s->labels, sizeof(int) * lab.size(), hipMemcpyDeviceToHost, stream) !=
+                hipSuccess ||
+            hipStreamSynchronize(stream) != hipSuccess)
             return fail(RNNT_STATUS_MEMOPS_FAILED, "copying labels to host");
         for (int b = 0; b < s->B; ++b)
             for (int i = 0; i < S[b]; ++i) {
@@ -820,11 +1014,42 @@ RNNTStatus manager_compute(GpuRNNTWorkspaceManager<float> &wm, int blank, hipStr
     float *costs_dev = reinterpret_cast<float *>(static_cast<char *>(s->workspace) + coff);
     st = mrnnt_cost_and_grad(&p, s->workspace, coff, costs_dev, grads, nullptr, stream);
     if (st != RNNT_STATUS_SUCCESS) return st;
+    s->computed = true;
+    s->with_beta = grads != nullptr;
+    s->blank = blank;
+    s->stream = stream;
     hipError_t e = hipMemcpyAsync(costs, costs_dev, sizeof(float) * s->B, hipMemcpyDeviceToHost, stream);
     if (e != hipSuccess) return fail(RNNT_STATUS_MEMOPS_FAILED, std::string("costs D2H: ") + hipGetErrorString(e));
     e = hipStreamSynchronize(stream);
     if (e != hipSuccess) return fail_hip(e, "stream synchronize");
     return RNNT_STATUS_SUCCESS;
+}
+
+// A device scratch buffer for the inspection getters (they are synchronous, as the reference's are).
+struct DevBuf {
+    void *p = nullptr;
+    explicit DevBuf(size_t bytes) {
+        if (hipMalloc(&p, std::max<size_t>(bytes, 16)) != hipSuccess) p = nullptr;
+    }
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+};
+
+// Reads back n elements of type Out (converted from In) through `read`, which fills a device buffer of n In on
+// `stream`; empty on failure or when there is no workspace.
+template <class In, class Out, class F>
+std::vector<Out> read_back(const mrnnt_gpu_ws_state *s, size_t n, hipStream_t stream, F &&read) {
+    if (!s->workspace) return {};
+    DevBuf buf(sizeof(In) * n);
+    if (!buf.p || read(static_cast<In *>(buf.p)) != RNNT_STATUS_SUCCESS) return {};
+    std::vector<In> h(n);
+    if (n && (hipMemcpyAsync(h.data(), buf.p, sizeof(In) * n, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+              hipStreamSynchronize(stream) != hipSuccess))
+        return {};
+    return std::vector<Out>(h.begin(), h.end());
 }
 
 }  // namespace
@@ -858,6 +1083,7 @@ void GpuRNNTWorkspaceManager<float>::set_workspace(void *workspace) {
     if (st_->owned && st_->workspace && st_->workspace != workspace) (void)hipFree(st_->workspace);
     st_->workspace = workspace;
     st_->owned = false;
+    st_->computed = false;
 }
 
 RNNTStatus GpuRNNTWorkspaceManager<float>::create_workspace() {
@@ -875,6 +1101,7 @@ void GpuRNNTWorkspaceManager<float>::free_workspace() {
     if (st_->workspace) (void)hipFree(st_->workspace);
     st_->workspace = nullptr;
     st_->owned = false;
+    st_->computed = false;
 }
 
 void GpuRNNTWorkspaceManager<float>::restrict_to_alignment(const int *const alignments, int max_shift, int blank_idx) {
@@ -888,22 +1115,122 @@ int GpuRNNTWorkspaceManager<float>::V_host() const { return st_->V; }
 
 std::vector<int> GpuRNNTWorkspaceManager<float>::T_host() const {
     std::vector<int> T, S;
-    host_lengths(st_, T, S);
+    host_lengths(st_, T, S, st_->stream);
     return T;
 }
 
 std::vector<int> GpuRNNTWorkspaceManager<float>::S_host() const {
     std::vector<int> T, S;
-    host_lengths(st_, T, S);
+    host_lengths(st_, T, S, st_->stream);
     return S;
 }
 
 int GpuRNNTWorkspaceManager<float>::num_denoms() const {
     std::vector<int> T, S;
-    host_lengths(st_, T, S);
+    host_lengths(st_, T, S, st_->stream);
     int64_t n = 0;
     for (size_t b = 0; b < T.size(); ++b) n += (int64_t)T[b] * (S[b] + 1);
     return (int)n;
+}
+
+int GpuRNNTWorkspaceManager<float>::num_fwd_bwd_var_positions() const { return num_denoms(); }
+
+std::vector<int> GpuRNNTWorkspaceManager<float>::var_start_offsets_host() const {
+    std::vector<int> T, S;
+    host_lengths(st_, T, S, st_->stream);
+    std::vector<int> off(T.size(), 0);
+    int64_t r = 0;
+    for (size_t b = 0; b < T.size(); ++b) {
+        off[b] = (int)r;
+        r += (int64_t)T[b] * (S[b] + 1);
+    }
+    return off;
+}
+
+int GpuRNNTWorkspaceManager<float>::S_max_host() const {
+    const std::vector<int> S = S_host();
+    return S.empty() ? 0 : *std::max_element(S.begin(), S.end());
+}
+
+int GpuRNNTWorkspaceManager<float>::T_max_host() const {
+    const std::vector<int> T = T_host();
+    return T.empty() ? 0 : *std::max_element(T.begin(), T.end());
+}
+
+std::vector<float> GpuRNNTWorkspaceManager<float>::acts_host() const {
+    const size_t n = (size_t)num_denoms() * (size_t)std::max(0, st_->V);
+    std::vector<float> h(n);
+    if (n && (hipMemcpyAsync(h.data(), st_->acts, sizeof(float) * n, hipMemcpyDeviceToHost, st_->stream) != hipSuccess ||
+              hipStreamSynchronize(st_->stream) != hipSuccess))
+        return {};
+    return h;
+}
+
+// The getters below read the state of the last cost / cost_and_grad on this workspace through the flat
+// inspection entry points (mrnnt_read_denoms / _state / _loglik / _band), in the reference's dense T*(S+1)
+// per-utterance order (var_start_offsets[b] + t*(S_b+1) + s).
+std::vector<float> GpuRNNTWorkspaceManager<float>::denom_host() const {
+    std::vector<int> T, S;
+    if (!host_lengths(st_, T, S, st_->stream)) return {};
+    const mrnnt_problem p = problem_of(st_, T, S, st_->blank);
+    return read_back<float, float>(st_, (size_t)num_denoms(), st_->stream,
+                                   [&](float *d) { return mrnnt_read_denoms(&p, st_->workspace, d, st_->stream); });
+}
+
+std::vector<float> GpuRNNTWorkspaceManager<float>::alphas_host() const {
+    std::vector<int> T, S;
+    if (!host_lengths(st_, T, S, st_->stream)) return {};
+    const mrnnt_problem p = problem_of(st_, T, S, st_->blank);
+    return read_back<double, float>(st_, (size_t)num_denoms(), st_->stream, [&](double *d) {
+        return mrnnt_read_state(&p, st_->workspace, nullptr, d, nullptr, st_->stream);
+    });
+}
+
+std::vector<float> GpuRNNTWorkspaceManager<float>::betas_host() const {
+    std::vector<int> T, S;
+    if (!host_lengths(st_, T, S, st_->stream)) return {};
+    const mrnnt_problem p = problem_of(st_, T, S, st_->blank);
+    return read_back<double, float>(st_, (size_t)num_denoms(), st_->stream, [&](double *d) {
+        return mrnnt_read_state(&p, st_->workspace, nullptr, nullptr, d, st_->stream);
+    });
+}
+
+std::vector<float> GpuRNNTWorkspaceManager<float>::ll_forward_host() const {
+    std::vector<int> T, S;
+    if (!host_lengths(st_, T, S, st_->stream)) return {};
+    const mrnnt_problem p = problem_of(st_, T, S, st_->blank);
+    return read_back<double, float>(st_, (size_t)st_->B, st_->stream, [&](double *d) {
+        return mrnnt_read_loglik(&p, st_->workspace, d, nullptr, st_->stream);
+    });
+}
+
+std::vector<float> GpuRNNTWorkspaceManager<float>::ll_backward_host() const {
+    std::vector<int> T, S;
+    if (!host_lengths(st_, T, S, st_->stream)) return {};
+    const mrnnt_problem p = problem_of(st_, T, S, st_->blank);
+    return read_back<double, float>(st_, (size_t)st_->B, st_->stream, [&](double *d) {
+        return mrnnt_read_loglik(&p, st_->workspace, nullptr, d, st_->stream);
+    });
+}
+
+std::vector<int> GpuRNNTWorkspaceManager<float>::min_allowed_s_host() const {
+    std::vector<int> T, S;
+    if (!host_lengths(st_, T, S, st_->stream)) return {};
+    const mrnnt_problem p = problem_of(st_, T, S, st_->blank);
+    const int64_t ld = std::max<int64_t>(1, p.align_stride);
+    return read_back<int, int>(st_, (size_t)st_->B * ld, st_->stream, [&](int *d) {
+        return mrnnt_read_band(&p, st_->workspace, d, nullptr, ld, st_->stream);
+    });
+}
+
+std::vector<int> GpuRNNTWorkspaceManager<float>::max_allowed_s_host() const {
+    std::vector<int> T, S;
+    if (!host_lengths(st_, T, S, st_->stream)) return {};
+    const mrnnt_problem p = problem_of(st_, T, S, st_->blank);
+    const int64_t ld = std::max<int64_t>(1, p.align_stride);
+    return read_back<int, int>(st_, (size_t)st_->B * ld, st_->stream, [&](int *d) {
+        return mrnnt_read_band(&p, st_->workspace, nullptr, d, ld, st_->stream);
+    });
 }
 
 GpuRNNTComputer<float>::GpuRNNTComputer(GpuRNNTWorkspaceManager<float> &workspace_manager, int blank,

@@ -247,18 +247,21 @@ int threads_of(int num_threads) { return num_threads > 0 ? num_threads : omp_get
 
 // Alignment band (restrict_to_alignment, cpu_workspace_manager.h:207-224): with m(t) = aligned labels among
 // the first t frames, alpha(t, .) lives in [m(t+1-k), m(t+1+k)] (indices clamped to [0, T]).
+void band_utt(const int *al, int T, int k, int align_blank, int *min_s, int *max_s) {
+    std::vector<int> m(T + 1, 0);
+    for (int t = 0; t < T; ++t) m[t + 1] = m[t] + (al[t] != align_blank ? 1 : 0);
+    for (int t = 0; t < T; ++t) {
+        min_s[t] = m[std::min(std::max(0, t + 1 - k), T)];
+        max_s[t] = m[std::max(0, std::min(T, t + 1 + k))];
+    }
+}
+
 void build_band(const mrnnt_problem *p, const CpuPlan &pl, const Views &w, int nt) {
 #pragma omp parallel for schedule(dynamic, 1) num_threads(nt)
     for (int b = 0; b < pl.B; ++b) {
-        const int T = p->T_host[b], k = p->max_shift;
-        const int *al = p->alignment + (int64_t)b * p->align_stride;
-        std::vector<int> m(T + 1, 0);
-        for (int t = 0; t < T; ++t) m[t + 1] = m[t] + (al[t] != p->align_blank ? 1 : 0);
         const int64_t c0 = pl.col_off[b];
-        for (int t = 0; t < T; ++t) {
-            w.min_s[c0 + t] = m[std::min(std::max(0, t + 1 - k), T)];
-            w.max_s[c0 + t] = m[std::max(0, std::min(T, t + 1 + k))];
-        }
+        band_utt(p->alignment + (int64_t)b * p->align_stride, p->T_host[b], p->max_shift, p->align_blank,
+                 w.min_s + c0, w.max_s + c0);
     }
 }
 
@@ -413,7 +416,7 @@ void grad_column(const mrnnt_problem *p, const CpuPlan &pl, const Views &w, cons
         const int64_t r = r0 + s;
         const float c = (float)((double)w.den[r] + base + b0);
         const float *z = acts + (a0 + s) * V;
-        const int l = (s < S && lab[s] != blank) ? lab[s] : -1;
+        const int l = (s < S && (unsigned)lab[s] < (unsigned)V && lab[s] != blank) ? lab[s] : -1;
         const float zb = z[blank], zl = l >= 0 ? z[l] : 0.0f;  // read first: grads may alias acts
         grad_row(z, g, V, c, sc);
         const float cb = (float)std::exp(w.lpb[r] + base + b1);
@@ -520,12 +523,20 @@ struct mrnnt_cpu_ws_state {
     const int *labels;
     int B, V;
     std::vector<int> T, S;
+    std::vector<int64_t> row_off, col_off;  // lattice row / column offsets (row_off[b] + t (S_b+1) + s)
+    int S_max = 0, T_max = 0;
     void *workspace = nullptr;
     bool owned = false;
     std::vector<int> alignment;  // copied by restrict_to_alignment, row stride max(T)
     bool restricted = false;
     int max_shift = 0;
     int align_blank = 0;
+    std::vector<int> min_s, max_s;  // band per lattice column: the reference's min/max_allowed_s_ (:51-56, :207-224)
+    // views of the workspace's per-row state (set_workspace), and the band of the last computation
+    float *den = nullptr;
+    double *alpha = nullptr, *beta = nullptr;
+    bool computed_restricted = false;
+    std::vector<int> cmin_s, cmax_s;
 };
 
 namespace {
@@ -541,9 +552,9 @@ mrnnt_problem cpu_problem_of(const mrnnt_cpu_ws_state *s, int blank) {
     p.acts = s->acts;
     p.labels = s->labels;
     // the reference's strides: labels max(S) (cpu_workspace_manager.h:121), alignment max(T) (:208)
-    p.label_stride = s->S.empty() ? 0 : *std::max_element(s->S.begin(), s->S.end());
+    p.label_stride = s->S_max;
     p.alignment = s->restricted ? s->alignment.data() : nullptr;
-    p.align_stride = s->T.empty() ? 0 : *std::max_element(s->T.begin(), s->T.end());
+    p.align_stride = s->T_max;
     p.align_blank = s->align_blank;
     p.max_shift = s->max_shift;
     p.num_rows = -1;
@@ -558,9 +569,16 @@ RNNTStatus cpu_compute(mrnnt_cpu_ws_state *s, int blank, int num_threads, float 
     RNNTStatus st = mrnnt_cpu_workspace_size(&p, &bytes);
     if (st != RNNT_STATUS_SUCCESS) return st;
     st = mrnnt_cpu_forward(&p, s->workspace, bytes, costs, grads != nullptr, num_threads);
-    if (st != RNNT_STATUS_SUCCESS || !grads) return st;
+    if (st != RNNT_STATUS_SUCCESS) return st;
+    s->computed_restricted = s->restricted;
+    s->cmin_s = s->min_s;
+    s->cmax_s = s->max_s;
+    if (!grads) return st;
     return mrnnt_cpu_backward(&p, s->workspace, nullptr, grads, num_threads);
 }
+
+constexpr float kNegInfF = -std::numeric_limits<float>::infinity();
+constexpr float kNaNF = std::numeric_limits<float>::quiet_NaN();
 
 }  // namespace
 
@@ -574,6 +592,18 @@ CpuRNNTWorkspaceManager<float>::CpuRNNTWorkspaceManager(const float *const acts,
     if (B > 0 && T && S) {
         st_->T.assign(T, T + B);
         st_->S.assign(S, S + B);
+        st_->S_max = *std::max_element(S, S + B);
+        st_->T_max = *std::max_element(T, T + B);
+        st_->row_off.assign(B + 1, 0);
+        st_->col_off.assign(B + 1, 0);
+        for (int b = 0; b < B; ++b) {  // (invalid lengths are rejected by get_workspace_size; keep offsets sane)
+            st_->row_off[b + 1] = st_->row_off[b] + (int64_t)std::max(0, T[b]) * (std::max(0, S[b]) + 1);
+            st_->col_off[b + 1] = st_->col_off[b] + std::max(0, T[b]);
+        }
+        st_->min_s.assign(st_->col_off[B], 0);
+        st_->max_s.resize(st_->col_off[B]);
+        for (int b = 0; b < B; ++b)
+            std::fill(st_->max_s.begin() + st_->col_off[b], st_->max_s.begin() + st_->col_off[b + 1], S[b]);
     }
 }
 
@@ -595,6 +625,16 @@ void CpuRNNTWorkspaceManager<float>::set_workspace(void *workspace) {
     if (st_->owned && st_->workspace && st_->workspace != workspace) std::free(st_->workspace);
     st_->workspace = workspace;
     st_->owned = false;
+    st_->den = nullptr;
+    st_->alpha = st_->beta = nullptr;
+    CpuPlan pl;  // the per-row state's offsets do not depend on the alignment (the band comes last)
+    const mrnnt_problem p = cpu_problem_of(st_, 0);
+    if (workspace && st_->B > 0 && make_cpu_plan(&p, &pl) == RNNT_STATUS_SUCCESS) {
+        const Views w = views(pl, workspace);
+        st_->den = w.den;
+        st_->alpha = w.alpha;
+        st_->beta = w.beta;
+    }
 }
 
 RNNTStatus CpuRNNTWorkspaceManager<float>::create_workspace() {
@@ -612,20 +652,104 @@ void CpuRNNTWorkspaceManager<float>::free_workspace() {
     if (st_->owned) std::free(st_->workspace);
     st_->workspace = nullptr;
     st_->owned = false;
+    st_->den = nullptr;
+    st_->alpha = st_->beta = nullptr;
 }
 
 void CpuRNNTWorkspaceManager<float>::restrict_to_alignment(const int *const alignments, int max_shift, int blank_idx) {
-    const int T_max = st_->T.empty() ? 0 : *std::max_element(st_->T.begin(), st_->T.end());
-    st_->alignment.assign(alignments, alignments + (size_t)st_->B * T_max);
+    st_->alignment.assign(alignments, alignments + (size_t)st_->B * st_->T_max);
     st_->restricted = true;
     st_->max_shift = max_shift;
     st_->align_blank = blank_idx;
+    for (int b = 0; b < st_->B && !st_->col_off.empty(); ++b)
+        band_utt(st_->alignment.data() + (size_t)b * st_->T_max, st_->T[b], max_shift, blank_idx,
+                 st_->min_s.data() + st_->col_off[b], st_->max_s.data() + st_->col_off[b]);
 }
 
 int CpuRNNTWorkspaceManager<float>::B() const { return st_->B; }
 int CpuRNNTWorkspaceManager<float>::V() const { return st_->V; }
 int CpuRNNTWorkspaceManager<float>::T(int b) const { return st_->T[b]; }
 int CpuRNNTWorkspaceManager<float>::S(int b) const { return st_->S[b]; }
+
+int CpuRNNTWorkspaceManager<float>::alpha_s_min(int b, int t) const {
+    return std::max(st_->min_s[st_->col_off[b] + t], t - (st_->T[b] - 1 - st_->S[b]));
+}
+int CpuRNNTWorkspaceManager<float>::alpha_s_max(int b, int t) const {
+    return std::min(st_->max_s[st_->col_off[b] + t], t + 1);
+}
+int CpuRNNTWorkspaceManager<float>::beta_s_min(int b, int t) const {
+    return t == 0 ? 0 : std::max(st_->min_s[st_->col_off[b] + t - 1], t - (st_->T[b] - st_->S[b]));
+}
+int CpuRNNTWorkspaceManager<float>::beta_s_max(int b, int t) const {
+    return t == 0 ? 0 : std::min(st_->max_s[st_->col_off[b] + t - 1], t);
+}
+
+int CpuRNNTWorkspaceManager<float>::label(int b, int s) const {
+    return st_->labels[(int64_t)b * st_->S_max + s];
+}
+
+long long CpuRNNTWorkspaceManager<float>::act_index(int b, int t, int s, int v) const {
+    return (st_->row_off[b] + (int64_t)t * (st_->S[b] + 1) + s) * (int64_t)st_->V + v;
+}
+
+float CpuRNNTWorkspaceManager<float>::act(int b, int t, int s, int v) const { return st_->acts[act_index(b, t, s, v)]; }
+
+void CpuRNNTWorkspaceManager<float>::set_denom(int b, int t, int s, float value) { get_denom(b, t, s) = value; }
+
+float &CpuRNNTWorkspaceManager<float>::get_denom(int b, int t, int s) {
+    static thread_local float none;
+    if (!st_->den) return none = kNaNF;
+    const int T = st_->T[b], S = st_->S[b];
+    const int64_t c = st_->col_off[b] + t, r = st_->row_off[b] + (int64_t)t * (S + 1) + s;
+    // rows the last computation reduced: the band (and alignment window), as in softmax_pass / row_window
+    int lo = std::max(0, t - (T - S)), hi = std::min(t, S);
+    if (st_->computed_restricted && !st_->cmin_s.empty()) {
+        int wlo = st_->cmin_s[c] - 1, whi = st_->cmax_s[c];
+        wlo = std::min(wlo, t > 0 ? st_->cmin_s[c - 1] : 0);
+        whi = std::max(whi, t > 0 ? st_->cmax_s[c - 1] : 0);
+        lo = std::max(lo, wlo);
+        hi = std::min(hi, whi);
+    }
+    if (s < lo || s > hi) {  // never read by the computation: reduce it now (the reference's pass covers every row)
+        float m;
+        double sum;
+        row_max_sum(st_->acts + r * st_->V, st_->V, m, sum);
+        st_->den[r] = (float)(-(double)m - std::log(sum));
+    }
+    return st_->den[r];
+}
+
+void CpuRNNTWorkspaceManager<float>::set_alpha(int b, int t, int s, float value) {
+    if (st_->alpha) st_->alpha[st_->row_off[b] + (int64_t)t * (st_->S[b] + 1) + s] = value;
+}
+
+float CpuRNNTWorkspaceManager<float>::get_alpha(int b, int t, int s) const {
+    // reference cpu_workspace_manager.h:161-181: virtual starts, alignment band, lattice band
+    const int T = st_->T[b], S = st_->S[b];
+    if (s == -1) return kNegInfF;
+    if (t == -1) return s == 0 ? 0.0f : kNegInfF;
+    const int64_t c = st_->col_off[b] + t;
+    if (s < st_->min_s[c] || s > st_->max_s[c]) return kNegInfF;
+    if (s > t + 1 || S - s > T - 1 - t) return kNegInfF;
+    if (!st_->alpha) return kNaNF;
+    return (float)st_->alpha[st_->row_off[b] + (int64_t)t * (S + 1) + s];
+}
+
+void CpuRNNTWorkspaceManager<float>::set_beta(int b, int t, int s, float value) {
+    if (st_->beta) st_->beta[st_->row_off[b] + (int64_t)t * (st_->S[b] + 1) + s] = value;
+}
+
+float CpuRNNTWorkspaceManager<float>::get_beta(int b, int t, int s) {
+    // reference cpu_workspace_manager.h:185-205
+    const int T = st_->T[b], S = st_->S[b];
+    if (s == S + 1) return kNegInfF;
+    if (t == T) return s == S ? 0.0f : kNegInfF;
+    const int64_t c = st_->col_off[b] + t;
+    if (t > 0 && (s < st_->min_s[c - 1] || s > st_->max_s[c - 1])) return kNegInfF;
+    if (s > t || S - s - 1 > T - 1 - t) return kNegInfF;
+    if (!st_->beta) return kNaNF;
+    return (float)st_->beta[st_->row_off[b] + (int64_t)t * (S + 1) + s];
+}
 
 CpuRNNTComputer<float>::CpuRNNTComputer(CpuRNNTWorkspaceManager<float> &workspace_manager, int blank, int num_threads)
     : workspace_manager_(workspace_manager), blank_(blank), num_threads_(num_threads) {}

@@ -109,6 +109,54 @@ __device__ __forceinline__ int64_t visit_col(const DevProblem &p, int64_t ci) {
     return x * q + (x < r ? x : r) + (ci >> 3);
 }
 
+// Device-resident lengths: the real column / row counts and the column-order multiplier published by the call's
+// setup kernel replace the host bounds in the kernel's copy of the problem. Returns false when the lengths failed
+// validation (then num_cols = 0: column walks do nothing). Without device lengths: a no-op returning true.
+__device__ __forceinline__ bool resolve_dyn(DevProblem &p) {
+    if (!p.dyn) return true;
+    const int st = __builtin_amdgcn_readfirstlane(p.dyn->status);
+    if (st) {
+        p.num_cols = 0;
+        return false;
+    }
+    p.num_cols = p.dyn->num_cols;
+    p.num_rows = p.dyn->num_rows;
+    if (p.col_mul > 0) p.col_mul = p.dyn->col_mul;  // scattered order requested: the device's coprime multiplier
+    return true;
+}
+
+__device__ __forceinline__ int64_t uniform64(int64_t v) {
+    const int lo = __builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const int hi = __builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)v >> 32));
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+// Column walk of a workgroup of a streaming kernel: visits ci = blockIdx.x, blockIdx.x + gridDim.x, ... < num_cols,
+// calling body(ci) (the whole workgroup, uniform ci). With p.steal (device-resident lengths, whose column count the
+// host does not know: the grid is sized to the CUs, not to the columns) the first gridDim.x columns go to the
+// workgroups in order and every later one to the workgroup that finishes first -- a shared counter the setup kernel
+// zeroed, the next index requested at the start of a column and handed over through LDS at its end (one barrier per
+// column), so a persistent grid balances like the hardware-scheduled one-workgroup-per-column launch.
+template <class F>
+__device__ __forceinline__ void walk_columns(const DevProblem &p, F &&body) {
+    if (!p.steal) {
+        for (int64_t ci = blockIdx.x; ci < p.num_cols; ci += gridDim.x) body(ci);
+        return;
+    }
+    __shared__ int64_t next_col[2];
+    int par = 0;
+    int64_t ci = blockIdx.x;
+    while (ci < p.num_cols) {
+        unsigned long long mine = 0;
+        if (threadIdx.x == 0) mine = atomicAdd(&p.dyn->steal, 1ull);
+        body(ci);
+        if (threadIdx.x == 0) next_col[par] = (int64_t)gridDim.x + (int64_t)mine;
+        __syncthreads();
+        ci = uniform64(next_col[par]);
+        par ^= 1;
+    }
+}
+
 // First acts/grads row of lattice column (b, t): packed layout (reference contract) = the internal
 // row rowc; padded [B, pad_T, pad_S1, V] layout = (b * pad_T + t) * pad_S1.
 __device__ __forceinline__ int64_t acts_col_base(const DevProblem &p, int b, int t, int64_t rowc) {
@@ -276,6 +324,18 @@ __device__ __forceinline__ RowCoef row_coef(const DevProblem &p, int t, int T, i
     const int lab = (s < S) ? lab_b[s] : -1;
     rc.lab = (lab == p.blank || (unsigned)lab >= (unsigned)p.V) ? -1 : lab;  // out of range: never matched / written
     return rc;
+}
+
+// Device-resident lengths that failed validation: every gradient element is NaN (the costs are NaN too), written
+// over the caller's whole grads buffer (rows as the host sized it) by the workgroups of the gradient launch.
+template <class IO>
+__device__ __forceinline__ void fill_failed_grads(const DevProblem &p, void *grads) {
+    typename IO::S *g = static_cast<typename IO::S *>(grads);
+    const int64_t rows = p.pad_S1 ? (int64_t)p.B * p.pad_T * p.pad_S1 : p.num_rows;
+    const int64_t n = rows * (int64_t)p.V;
+    const typename IO::S nan = IO::from_f(__builtin_nanf(""));
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        g[i] = nan;
 }
 
 template <bool NT, class V>

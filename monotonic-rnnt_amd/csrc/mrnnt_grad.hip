@@ -37,6 +37,10 @@ __device__ __forceinline__ typename IO::V grad_vec(const typename IO::V &xv, con
 template <class IO, int U, int R, bool NTL, bool NTS>
 __global__ __launch_bounds__(256) void grad_kernel(DevProblem p, const float *__restrict__ scale,
                                                        void *__restrict__ grads) {
+    if (!resolve_dyn(p)) {  // device-resident lengths failed validation: NaN gradients
+        fill_failed_grads<IO>(p, grads);
+        return;
+    }
     typedef typename IO::V Vec;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -108,6 +112,10 @@ __global__ __launch_bounds__(256) void grad_kernel(DevProblem p, const float *__
 template <class IO, int U, int R, bool NTL, bool NTS>
 __global__ __launch_bounds__(256) void grad_staged_kernel(DevProblem p, const float *__restrict__ scale,
                                                           void *__restrict__ grads) {
+    if (!resolve_dyn(p)) {  // device-resident lengths failed validation: NaN gradients
+        fill_failed_grads<IO>(p, grads);
+        return;
+    }
     typedef typename IO::V Vec;
     constexpr int SEG = 256;
     constexpr int DEAD = -2;  // label slot of a row whose gradient is exactly zero (out of band or dead)
@@ -195,6 +203,10 @@ __global__ __launch_bounds__(256) void grad_staged_kernel(DevProblem p, const fl
 template <class IO, int U, bool NTL, bool NTS>
 __global__ __launch_bounds__(256) void grad_rows_kernel(DevProblem p, const float *__restrict__ scale,
                                                             void *__restrict__ grads) {
+    if (!resolve_dyn(p)) {  // device-resident lengths failed validation: NaN gradients
+        fill_failed_grads<IO>(p, grads);
+        return;
+    }
     typedef typename IO::V Vec;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -244,6 +256,10 @@ __global__ __launch_bounds__(256) void grad_rows_kernel(DevProblem p, const floa
 template <class IO>
 __global__ __launch_bounds__(256) void grad_scalar_kernel(DevProblem p, const float *__restrict__ scale,
                                                           void *__restrict__ grads) {
+    if (!resolve_dyn(p)) {  // device-resident lengths failed validation: NaN gradients
+        fill_failed_grads<IO>(p, grads);
+        return;
+    }
     typedef typename IO::S Sc;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -289,6 +305,7 @@ __global__ __launch_bounds__(256) void grad_scalar_kernel(DevProblem p, const fl
 // Number of in-band rows whose acts the gradient kernels read (live rows; all in-band rows with
 // occ_skip = 0). Not on the hot path: bench/inspection only (mrnnt_grad_live_rows).
 __global__ __launch_bounds__(256) void count_live_kernel(DevProblem p, unsigned long long *__restrict__ count) {
+    resolve_dyn(p);
     __shared__ unsigned long long part[4];
     unsigned long long n = 0;
     Cursor cur;
@@ -326,6 +343,7 @@ hipError_t launch_count_live(const DevProblem &p, unsigned long long *count, hip
 // One wave per padded row, grid-stride; lattice rows are skipped (written by the gradient kernel).
 template <class IO>
 __global__ __launch_bounds__(256) void pad_zero_kernel(DevProblem p, void *__restrict__ grads, int vec) {
+    if (!resolve_dyn(p)) return;  // the gradient kernel filled the whole buffer with NaN
     typedef typename IO::S Sc;
     typedef typename IO::V Vec;
     const int lane = threadIdx.x & 63;

@@ -12,6 +12,18 @@ namespace mrnnt {
 // Element type of acts and grads (the math is fp32/fp64 inside the kernels).
 enum ElemType { ELEM_F32 = 0, ELEM_BF16 = 1, ELEM_F16 = 2 };
 
+// Device-resident lengths (mrnnt_problem.lengths_on_device): the setup kernel of the call validates the lengths
+// and publishes what the host could not plan, for the later kernels of the same call (one 64-byte line).
+struct DynWords {
+    int status;                // 0, or RNNT_STATUS_INVALID_VALUE: the lengths failed validation (nothing runs)
+    int pad_;
+    int64_t num_cols;          // sum_b T_b
+    int64_t num_rows;          // sum_b T_b (S_b + 1)
+    int64_t col_mul;           // scattered column order: a multiplier coprime with num_cols (0: in order)
+    unsigned long long steal;  // work counter of the log-softmax's column walk (zeroed by the setup kernel)
+    int64_t spare_[3];
+};
+
 // Everything a kernel needs, passed by value as a kernel argument.
 // Internal per-row arrays use the packed lattice row r = row_off[b] + t*(S_b+1) + s (column (b, t) at
 // col_off[b] + t). acts/grads rows use the caller's layout: packed (the same r) or padded
@@ -42,6 +54,9 @@ struct DevProblem {
     double *beta;               // [N]  beta(t, s)
     double *ll;                 // [B]  alpha(T-1, S)
     double *llb;                // [B]  beta(0, 0)
+    DynWords *dyn;              // device-resident lengths: num_cols / num_rows / col_mul above are host bounds and
+                                // the kernels take the real values from here (resolve_dyn); nullptr otherwise
+    int steal;                  // log-softmax: columns past the grid handed out by dyn->steal (work stealing)
 };
 
 // Fused joint network (mrnnt_joint.hip): logits z(b,t,s,:) = W * tanh(enc[b,t,:] + pred[b,s,:]) + bias are
@@ -127,6 +142,31 @@ enum KernelId { K_BAND = 0, K_SOFTMAX = 1, K_DP = 2, K_GRAD = 3, K_SETUP = 4, K_
 // lpb / lpe (may be null): zero their 64 pad entries either side of [0, n)
 hipError_t launch_setup(const int *T, const int *S, int B, int64_t *row_off, int64_t *col_off, int *col_b,
                         double *lpb, double *lpe, int64_t n, hipStream_t stream);
+// Device-resident lengths: lattice offsets, column map, validation and the DynWords in one launch (B workgroups).
+struct DynSetupArgs {
+    const int *T;
+    const int *S;
+    int B;
+    int packed;         // 1: sum_b T_b (S_b+1) must equal rows; 0 (padded layout): rows is an upper bound
+    int64_t rows;
+    int64_t cols_cap;   // capacity of col_b (and of the alignment band arrays)
+    int64_t S_cap;      // S_b <= S_cap (the label row stride)
+    int64_t T_cap;      // T_b <= T_cap (alignment row stride / pad_T), 0 = unbounded
+    int64_t S1_cap;     // S_b + 1 <= S1_cap (pad_S1), 0 = unbounded
+    int scatter;        // publish a scattered column-order multiplier
+    int64_t *row_off;
+    int64_t *col_off;
+    int *col_b;
+    double *lpb;        // lp arrays: their 64 entries either side of [0, rows) are zeroed
+    double *lpe;
+    DynWords *dyn;
+    int *status_host;   // device address of the caller's host-mapped status word, or nullptr
+};
+hipError_t launch_setup_dyn(const DynSetupArgs &a, hipStream_t stream);
+// mrnnt_read_denoms: den of every row (copied where the forward reduced it, reduced from acts elsewhere)
+hipError_t launch_den_all(const DevProblem &p, int elem, float *den_out, hipStream_t stream);
+// mrnnt_read_band: min / max allowed s in the [B, ld] layout
+hipError_t launch_band_read(const DevProblem &p, int *min_out, int *max_out, int64_t ld, hipStream_t stream);
 hipError_t launch_align(const DevProblem &p, const int *alignment, int64_t align_stride, int align_blank,
                         int max_shift, int *mtmp, int *min_s, int *max_s, hipStream_t stream);
 hipError_t launch_softmax(const DevProblem &p, int elem, int grid, hipStream_t stream);

@@ -199,11 +199,27 @@ __device__ __forceinline__ void beta_pass(const DevProblem &p, int b, double (*x
     if (threadIdx.x == 0) p.llb[b] = bn[0];
 }
 
+// Device-resident lengths that failed validation (mrnnt_setup.hip, setup_dyn_kernel): the workgroup's lengths may be
+// anything, so it touches no lattice array -- its cost and log-likelihoods are NaN.
+__device__ __forceinline__ bool dyn_failed(const DevProblem &p, int b, bool bwd, float *costs) {
+    if (!p.dyn || !__builtin_amdgcn_readfirstlane(p.dyn->status)) return false;
+    if (threadIdx.x == 0) {
+        if (bwd) {
+            p.llb[b] = __builtin_nan("");
+        } else {
+            p.ll[b] = __builtin_nan("");
+            if (costs) costs[b] = __builtin_nanf("");
+        }
+    }
+    return true;
+}
+
 template <int K, int D, int NW, bool BAND>
 __global__ __launch_bounds__(64 * NW) void recursion_kernel(DevProblem p, int with_beta, float *__restrict__ costs) {
     __shared__ double xb[2][8];
     const int b = with_beta ? (int)(blockIdx.x >> 1) : (int)blockIdx.x;
     const bool bwd = with_beta && (blockIdx.x & 1);
+    if (dyn_failed(p, b, bwd, costs)) return;
     if (bwd)
         beta_pass<K, D, NW, BAND>(p, b, xb);
     else
@@ -449,6 +465,7 @@ __global__ __launch_bounds__(64 * NW) void recursion_halo_kernel(DevProblem p, i
     __shared__ double xh[2][8][HL > 0 ? HL : 1];
     const int b = with_beta ? (int)(blockIdx.x >> 1) : (int)blockIdx.x;
     const bool bwd = with_beta && (blockIdx.x & 1);
+    if (dyn_failed(p, b, bwd, costs)) return;
     if (bwd)
         beta_pass_halo<D, NW, HL, BAND, LEAN>(p, b, xh);
     else

@@ -1,5 +1,7 @@
 // mrnnt_setup.hip -- per-call metadata on the device (no host copies): lattice row/column offsets from the
 // length arrays, the alignment band, and the launch knobs.
+#include <algorithm>
+
 #include "mrnnt_device.h"
 
 namespace mrnnt {
@@ -60,6 +62,7 @@ __global__ __launch_bounds__(64) void setup_kernel(const int *__restrict__ T, co
 // utterance, then one thread per frame.
 __global__ __launch_bounds__(64) void align_prefix_kernel(DevProblem p, const int *__restrict__ alignment,
                                                           int64_t astride, int ablank, int *__restrict__ m) {
+    if (!resolve_dyn(p)) return;  // device-resident lengths failed validation: offsets are not trustworthy
     const int b = blockIdx.x;
     const int lane = threadIdx.x;
     const int T = p.T[b];
@@ -79,6 +82,7 @@ __global__ __launch_bounds__(64) void align_prefix_kernel(DevProblem p, const in
 
 __global__ __launch_bounds__(256) void align_band_kernel(DevProblem p, int k, const int *__restrict__ m,
                                                          int *__restrict__ min_s, int *__restrict__ max_s) {
+    if (!resolve_dyn(p)) return;
     for (int b = blockIdx.y; b < p.B; b += gridDim.y) {  // grid y is capped at 65535 utterances per pass
         const int T = p.T[b];
         const int64_t mb = p.col_off[b] + b;
@@ -123,6 +127,7 @@ hipError_t launch_align(const DevProblem &p, const int *alignment, int64_t align
 // row reads.
 __global__ __launch_bounds__(64) void mask_state_kernel(DevProblem p, double *__restrict__ alpha,
                                                         double *__restrict__ beta) {
+    resolve_dyn(p);
     for (int64_t c = blockIdx.x; c < p.num_cols; c += gridDim.x) {
         const int b = p.col_b[c];
         const int T = p.T[b], S = p.S[b];
@@ -139,6 +144,175 @@ __global__ __launch_bounds__(64) void mask_state_kernel(DevProblem p, double *__
 hipError_t launch_mask_state(const DevProblem &p, double *alpha, double *beta, hipStream_t stream) {
     const int grid = (int)(p.num_cols < (1 << 16) ? p.num_cols : (1 << 16));
     mask_state_kernel<<<grid > 0 ? grid : 1, 64, 0, stream>>>(p, alpha, beta);
+    return hipGetLastError();
+}
+
+// ---- device-resident lengths (mrnnt_problem.lengths_on_device) -------------------------------------------------
+// One workgroup per utterance: the prefix of the valid lengths before it gives its lattice row / column offsets, it
+// writes its own column map entries, and the last workgroup, which reads every length, validates the batch and
+// publishes the DynWords (status, real column / row counts, scattered-order multiplier, zeroed work counter) for the
+// later kernels of the call. Invalid lengths count as empty utterances, so no offset leaves the capacities the host
+// sized; the call then fails closed (DynWords.status: the later kernels write NaN costs and gradients only).
+// O(B^2 / 256) length reads in all -- one launch instead of a scan kernel + a map kernel.
+__device__ __forceinline__ bool dyn_len_ok(const DynSetupArgs &a, int T, int S) {
+    return T > 0 && S >= 0 && T >= S && S <= a.S_cap && (a.T_cap == 0 || T <= a.T_cap) &&
+           (a.S1_cap == 0 || (int64_t)S + 1 <= a.S1_cap);
+}
+
+__device__ __forceinline__ int64_t block_sum64(int64_t v, int64_t *red) {  // 256 threads, every thread gets the sum
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    __syncthreads();  // red is reused by consecutive sums
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    return red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ __launch_bounds__(256) void setup_dyn_kernel(DynSetupArgs a) {
+    __shared__ int64_t red[4];
+    const int b = blockIdx.x;
+    const bool last = b == a.B - 1;
+    int64_t r = 0, c = 0, bad = 0;
+    const int n = last ? a.B : b;
+    for (int i = threadIdx.x; i < n; i += 256) {
+        const int T = a.T[i], S = a.S[i];
+        const bool ok = dyn_len_ok(a, T, S);
+        bad += ok ? 0 : 1;
+        if (ok && i < b) {
+            r += (int64_t)T * (S + 1);
+            c += T;
+        }
+    }
+    r = block_sum64(r, red);
+    c = block_sum64(c, red);
+    if (last) bad = block_sum64(bad, red);
+    const int T = a.T[b], S = a.S[b];
+    const bool ok = dyn_len_ok(a, T, S);
+    const int64_t rb = ok ? (int64_t)T * (S + 1) : 0, cb = ok ? T : 0;
+    if (threadIdx.x == 0) {
+        if (b == 0) {
+            a.row_off[0] = 0;
+            a.col_off[0] = 0;
+        }
+        a.row_off[b + 1] = r + rb;
+        a.col_off[b + 1] = c + cb;
+    }
+    if (ok && c + cb <= a.cols_cap)
+        for (int t = threadIdx.x; t < T; t += 256) a.col_b[c + t] = b;
+    if (!last) return;
+    const int64_t R = r + rb, C = c + cb;
+    const bool fail = bad != 0 || (a.packed ? R != a.rows : R > a.rows) || C > a.cols_cap;
+    // scattered column order (the gradient's visit_col): the first multiplier >= 0.618 C coprime with C, 64
+    // candidates per pass with lane-parallel Euclid (any coprime multiplier makes i -> i * m mod C a permutation)
+    int64_t mul = 0;
+    if (!fail && a.scatter && C >= 3 && C < (1ll << 31) && threadIdx.x < 64) {
+        for (uint32_t base = max(2u, (uint32_t)(0.6180339887 * (double)C));; base += 64) {
+            uint32_t x = base + threadIdx.x, y = (uint32_t)C;
+            while (y) {
+                const uint32_t rem = x % y;
+                x = y;
+                y = rem;
+            }
+            const unsigned long long hit = __ballot(x == 1);
+            if (hit) {
+                mul = (int64_t)base + __ffsll((long long)hit) - 1;
+                break;
+            }
+        }
+    }
+    if (threadIdx.x == 0) {
+        DynWords *d = a.dyn;
+        d->status = fail ? (int)RNNT_STATUS_INVALID_VALUE : 0;
+        d->num_cols = fail ? 0 : C;
+        d->num_rows = fail ? 0 : R;
+        d->col_mul = mul;
+        d->steal = 0;
+        if (fail && a.status_host)  // a plain system-scope store into the caller's host-mapped word
+            __hip_atomic_store(a.status_host, (int)RNNT_STATUS_INVALID_VALUE, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (threadIdx.x < 64 && a.lpb) {  // the recursion's reads just outside [0, N) (see setup_kernel)
+        const int i = threadIdx.x;
+        const int64_t end = fail ? 0 : R;
+        a.lpb[i - 64] = 0.0;
+        a.lpe[i - 64] = 0.0;
+        a.lpb[end + i] = 0.0;
+        a.lpe[end + i] = 0.0;
+    }
+}
+
+hipError_t launch_setup_dyn(const DynSetupArgs &a, hipStream_t stream) {
+    setup_dyn_kernel<<<a.B, 256, 0, stream>>>(a);
+    return hipGetLastError();
+}
+
+// ---- inspection (not on the hot path) ---------------------------------------------------------------------------
+// mrnnt_read_denoms: den of every lattice row. Rows the forward reduced (in band, inside the alignment window) are
+// copied; the others are reduced here from acts, one wave per row (the reference's reduce covers every row,
+// reduce.h:79-139, and its getter returns them all).
+template <class IO>
+__global__ __launch_bounds__(256) void den_all_kernel(DevProblem p, float *__restrict__ out) {
+    resolve_dyn(p);
+    typedef typename IO::S Sc;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const Sc *__restrict__ acts = reinterpret_cast<const Sc *>(p.acts);
+    for (int64_t c = blockIdx.x; c < p.num_cols; c += gridDim.x) {
+        const int b = p.col_b[c];
+        const int T = p.T[b], S = p.S[b];
+        const int t = (int)(c - p.col_off[b]);
+        const int64_t rowc = p.row_off[b] + (int64_t)t * (S + 1);
+        const int64_t arow = acts_col_base(p, b, t, rowc);
+        int lo = max(0, t - (T - S)), hi = min(t, S);
+        align_window(p, c, t, lo, hi);
+        for (int s = wave; s <= S; s += 4) {
+            if (s >= lo && s <= hi) {
+                if (lane == 0) out[rowc + s] = p.den[rowc + s];
+                continue;
+            }
+            const Sc *__restrict__ z = acts + (arow + s) * (int64_t)p.V;
+            float m = NEG_INF_F, sum = 0.0f;
+            for (int v = lane; v < p.V; v += 64) {
+                const float x = IO::to_f(z[v]);
+                const float mn = fmaxf(m, x);
+                const float mr = (mn == NEG_INF_F) ? 0.0f : mn;
+                sum = sum * fast_exp2((m - mr) * kLog2e) + fast_exp2((x - mr) * kLog2e);
+                m = mn;
+            }
+            wave_reduce_max_sum(m, sum);
+            if (lane == 0) out[rowc + s] = (float)(-(double)m - log_row_sum(sum));
+        }
+    }
+}
+
+hipError_t launch_den_all(const DevProblem &p, int elem, float *den_out, hipStream_t stream) {
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(p.num_cols, 1 << 16));
+    switch (elem) {
+        case ELEM_F32: den_all_kernel<IoF32><<<grid, 256, 0, stream>>>(p, den_out); break;
+        case ELEM_BF16: den_all_kernel<IoBF16><<<grid, 256, 0, stream>>>(p, den_out); break;
+        case ELEM_F16: den_all_kernel<IoF16><<<grid, 256, 0, stream>>>(p, den_out); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// mrnnt_read_band: the band in the reference's [B, ld] layout; t >= T_b and unrestricted calls give (0, S_b)
+__global__ __launch_bounds__(256) void band_read_kernel(DevProblem p, int *__restrict__ min_out,
+                                                        int *__restrict__ max_out, int64_t ld) {
+    if (!resolve_dyn(p)) return;
+    for (int b = blockIdx.x; b < p.B; b += gridDim.x) {
+        const int T = p.T[b], S = p.S[b];
+        const int64_t c0 = p.col_off[b];
+        for (int64_t t = threadIdx.x; t < ld; t += blockDim.x) {
+            const bool in = p.min_s && t < T;
+            if (min_out) min_out[(int64_t)b * ld + t] = in ? p.min_s[c0 + t] : 0;
+            if (max_out) max_out[(int64_t)b * ld + t] = in ? p.max_s[c0 + t] : S;
+        }
+    }
+}
+
+hipError_t launch_band_read(const DevProblem &p, int *min_out, int *max_out, int64_t ld, hipStream_t stream) {
+    band_read_kernel<<<std::max(1, std::min(p.B, 65535)), 256, 0, stream>>>(p, min_out, max_out, ld);
     return hipGetLastError();
 }
 

@@ -42,6 +42,7 @@ __device__ __forceinline__ void zero_lp_pads(const DevProblem &p) {
 // 64*U*E elements), R = rows a wave reduces at once (U*R vector loads in flight per lane).
 template <class IO, int U, int R, bool NTL>
 __global__ __launch_bounds__(256) void softmax_kernel(DevProblem p) {
+    resolve_dyn(p);
     zero_lp_pads(p);
     constexpr int NW = 4;
     constexpr int E = IO::E;
@@ -54,7 +55,7 @@ __global__ __launch_bounds__(256) void softmax_kernel(DevProblem p) {
     const int bj = blank / E, bc = blank % E, blane = bj & 63;
     const Vec ninf = splat<IO>(NEG_INF_F);
 
-    for (int64_t c = blockIdx.x; c < p.num_cols; c += gridDim.x) {
+    walk_columns(p, [&](int64_t c) {
         const int b = p.col_b[c];
         const int T = p.T[b], S = p.S[b];
         const int t = (int)(c - p.col_off[b]);
@@ -124,7 +125,7 @@ __global__ __launch_bounds__(256) void softmax_kernel(DevProblem p) {
                 if (lane == 0) write_row(p, rowc + s + r, m[r], sum[r], zbv, zev);
             }
         }
-    }
+    });
 }
 
 // Element v of a lane's slice of the row (x[u][i], vector j = v / E in lane j % 64, u = j / 64 % U) into
@@ -149,6 +150,7 @@ __device__ __forceinline__ float lane_pick(const float (&x)[N], int k) {
 // before the wave sum (one exp and its bookkeeping per row fewer), and the R rows' DPP chains interleave.
 template <class IO, int U, int R, bool NTL, bool FULL, bool ONE = false>
 __global__ __launch_bounds__(256) void softmax_lean_kernel(DevProblem p) {
+    resolve_dyn(p);
     zero_lp_pads(p);
     constexpr int E = IO::E;
     constexpr int CH = 64 * U;  // vectors per chunk
@@ -160,7 +162,7 @@ __global__ __launch_bounds__(256) void softmax_lean_kernel(DevProblem p) {
     const int blank = p.blank;
     const Vec ninf = splat<IO>(NEG_INF_F);
 
-    for (int64_t ci = blockIdx.x; ci < p.num_cols; ci += gridDim.x) {
+    walk_columns(p, [&](int64_t ci) {
         const int64_t c = visit_col(p, ci);
         const int b = p.col_b[c];
         const int T = p.T[b], S = p.S[b];
@@ -235,7 +237,7 @@ __global__ __launch_bounds__(256) void softmax_lean_kernel(DevProblem p) {
                     p.lpe[row] = (double)eze + den;
                 }
             }
-            continue;
+            return;  // next column
         }
         for (int s = lo + wave * R; s <= hi; s += 4 * R) {
             const int nrow = __builtin_amdgcn_readfirstlane(min(R, hi - s + 1));
@@ -324,7 +326,7 @@ __global__ __launch_bounds__(256) void softmax_lean_kernel(DevProblem p) {
                 p.lpe[row] = (double)eze + den;
             }
         }
-    }
+    });
 }
 
 // 16-lane rows (the default for rows of <= 64 vectors: f32 V <= 256, bf16 / fp16 V <= 512; softmax_variant 13 /
@@ -341,6 +343,7 @@ __device__ __forceinline__ float dpp16(float v) {
 
 template <class IO, int NR, bool NTL>
 __global__ __launch_bounds__(256) void softmax_row16_kernel(DevProblem p) {
+    resolve_dyn(p);
     zero_lp_pads(p);
     constexpr int E = IO::E;
     typedef typename IO::V Vec;
@@ -354,7 +357,7 @@ __global__ __launch_bounds__(256) void softmax_row16_kernel(DevProblem p) {
     const int blank = p.blank;
     const Vec ninf = splat<IO>(NEG_INF_F);
 
-    for (int64_t ci = blockIdx.x; ci < p.num_cols; ci += gridDim.x) {
+    walk_columns(p, [&](int64_t ci) {
         const int64_t c = visit_col(p, ci);
         const int b = p.col_b[c];
         const int T = p.T[b], S = p.S[b];
@@ -426,12 +429,13 @@ __global__ __launch_bounds__(256) void softmax_row16_kernel(DevProblem p) {
                 }
             }
         }
-    }
+    });
 }
 
 // Scalar path (any V, any alignment, any element type): one row per wave, lanes stride over v.
 template <class IO>
 __global__ __launch_bounds__(256) void softmax_scalar_kernel(DevProblem p) {
+    resolve_dyn(p);
     zero_lp_pads(p);
     typedef typename IO::S Sc;
     const int lane = threadIdx.x & 63;
@@ -439,7 +443,7 @@ __global__ __launch_bounds__(256) void softmax_scalar_kernel(DevProblem p) {
     const int V = p.V;
     const int blank = p.blank;
     const Sc *__restrict__ acts = reinterpret_cast<const Sc *>(p.acts);
-    for (int64_t c = blockIdx.x; c < p.num_cols; c += gridDim.x) {
+    walk_columns(p, [&](int64_t c) {
         const int b = p.col_b[c];
         const int T = p.T[b], S = p.S[b];
         const int t = (int)(c - p.col_off[b]);
@@ -476,7 +480,7 @@ __global__ __launch_bounds__(256) void softmax_scalar_kernel(DevProblem p) {
             const float zev = lab >= 0 ? __shfl(ze, lab & 63) : ze;  // ze: 0, or NaN (bad label)
             if (lane == 0) write_row(p, rowc + s, m, sum, zbv, zev);
         }
-    }
+    });
 }
 
 template <class IO, bool NTL, int U>

@@ -68,6 +68,9 @@ class MrnntProblem(ctypes.Structure):
         ("lattice", ctypes.c_void_p),
         # version 6
         ("grad_scale_broadcast", ctypes.c_int),
+        # version 7
+        ("lengths_on_device", ctypes.c_int),
+        ("status_host", ctypes.c_void_p),
     ]
 
 
@@ -129,6 +132,9 @@ def _bind(path: str, dev: bool = False) -> ctypes.CDLL:
         "mrnnt_grad_live_rows": (i, [P, vp, vp, vp]),
         "mrnnt_read_state": (i, [P, vp, vp, vp, vp, vp]),
         "mrnnt_cpu_read_state": (i, [P, vp, vp, vp, vp]),
+        "mrnnt_read_denoms": (i, [P, vp, vp, vp]),
+        "mrnnt_read_band": (i, [P, vp, vp, vp, i64, vp]),
+        "mrnnt_status_word": (ctypes.POINTER(ctypes.c_int), []),
         "mrnnt_cpu_workspace_size": (i, [P, ctypes.POINTER(sz)]),
         "mrnnt_cpu_forward": (i, [P, vp, sz, vp, i, i]),
         "mrnnt_cpu_backward": (i, [P, vp, vp, vp, i]),
@@ -149,8 +155,8 @@ def _bind(path: str, dev: bool = False) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.mrnnt_version() < 6:
-        raise ImportError(f"{path} is a stale build (ABI version {lib.mrnnt_version()} < 6); "
+    if lib.mrnnt_version() < 7:
+        raise ImportError(f"{path} is a stale build (ABI version {lib.mrnnt_version()} < 7); "
                           "rebuild with `make -C monotonic-rnnt_amd`")
     return lib
 

@@ -26,6 +26,13 @@ Behavioural differences from the reference, all deliberate:
 
 Extensions beyond the reference: bf16/fp16 acts (costs stay fp32) and the padded
 [B, pad_T, pad_S1, V] acts layout, both read in place by the same kernels.
+
+Lengths on the GPU (the reference's required form, monotonic_rnnt.cu:85-88) are never read back: the launch is
+planned from acts.size(0) and labels.size(1) and the lattice is built and validated on the device (ABI v7
+lengths_on_device), so a step makes no host synchronisation and can be captured in a HIP graph. Lengths that fail
+that validation make the call's costs and gradients NaN and are reported by the next call (or check_lengths()),
+as a RuntimeError, the way an asynchronous device error surfaces; MRNNT_SYNC_LENGTH_CHECK=1 checks every call
+synchronously instead. Host (CPU) lengths plan the launch exactly, uploaded once per distinct shape.
 """
 from __future__ import annotations
 
@@ -74,6 +81,11 @@ class _Lengths:
         on another stream waits for that upload through an event. Returns (T_dev, S_dev, lattice_dev)."""
         hit = self.dev.get(dev)
         stream = torch.cuda.current_stream(dev)
+        if hit is None and torch.cuda.is_current_stream_capturing():
+            # the upload would only be captured, not run: an eager call with these lengths before the first replay
+            # would read unwritten offsets (ADVICE r2)
+            raise RuntimeError("monotonic_rnnt: these host lengths are first seen inside HIP-graph capture; run one "
+                               "warm-up call with them before capturing, or pass the lengths as GPU tensors")
         if hit is None:
             B = self.T.size
             p = _L.MrnntProblem()
@@ -127,6 +139,51 @@ def _lengths(input_lengths: torch.Tensor, label_lengths: torch.Tensor) -> _Lengt
     return hit
 
 
+import os as _os
+
+_SYNC_LENGTH_CHECK = _os.environ.get("MRNNT_SYNC_LENGTH_CHECK", "0") not in ("", "0")
+_STATUS = None
+_DYN_WS: "dict" = {}
+
+
+def _status_word():
+    """The library's host-mapped status word (mrnnt_status_word): the device stores into it when device-resident
+    lengths fail validation, with no copy on the stream."""
+    global _STATUS
+    if _STATUS is None:
+        ptr = _L.load().mrnnt_status_word()
+        if not ptr:
+            raise RuntimeError("monotonic_rnnt: could not allocate the host-mapped status word")
+        _STATUS = ptr
+    return _STATUS
+
+
+def check_lengths(sync: bool = True) -> None:
+    """Raise if an earlier call's GPU-resident lengths failed validation on the device (their costs and gradients
+    are NaN). sync=True waits for the current device's queued work first."""
+    if _STATUS is None:
+        return
+    if sync and torch.cuda.is_available():
+        torch.cuda.synchronize()
+    if _STATUS[0] != 0:
+        _STATUS[0] = 0
+        raise _L.MrnntError(_L.RNNT_STATUS_INVALID_VALUE, "monotonic_rnnt",
+                            "GPU-resident lengths of an earlier call failed validation on the device: need "
+                            "T_b > 0, 0 <= S_b <= T_b, S_b <= labels.size(1), sum_b T_b (S_b+1) == acts.size(0) "
+                            "(padded acts: T_b <= size(1), S_b < size(2)), T_b <= alignment.size(1); that call's "
+                            "costs and gradients are NaN")
+
+
+def _device_lengths(t: torch.Tensor, dev: torch.device, B: int, what: str) -> torch.Tensor:
+    t = t.detach()
+    if t.device != dev or t.dtype != torch.int32:
+        t = t.to(dev, torch.int32, non_blocking=True)
+    t = t.reshape(-1).contiguous()
+    if t.numel() != B:
+        raise RuntimeError(f"monotonic_rnnt: expected {B} {what}, got {t.numel()}")
+    return t
+
+
 class _Prepared:
     """Views of one call's inputs on the device they live on, plus the filled mrnnt_problem.
 
@@ -148,11 +205,19 @@ class _Prepared:
         self.acts = acts.contiguous()
         self.num_threads = int(num_threads)
         B = labels.size(0)
-        self.lengths = ln = _lengths(input_lengths, label_lengths)
-        self.T_host, self.S_host = ln.T, ln.S
-        if self.T_host.size != B or self.S_host.size != B:
-            raise RuntimeError(f"monotonic_rnnt: expected {B} input/label lengths, "
-                               f"got {self.T_host.size}/{self.S_host.size}")
+        # GPU acts with GPU lengths: planned without reading the lengths back (ABI v7 lengths_on_device)
+        self.dyn = self.on_gpu and (input_lengths.is_cuda or label_lengths.is_cuda)
+        if self.dyn:
+            self.lengths = ln = None
+            self.T_host = self.S_host = None
+            self.T_dev = _device_lengths(input_lengths, dev, B, "input lengths")
+            self.S_dev = _device_lengths(label_lengths, dev, B, "label lengths")
+        else:
+            self.lengths = ln = _lengths(input_lengths, label_lengths)
+            self.T_host, self.S_host = ln.T, ln.S
+            if self.T_host.size != B or self.S_host.size != B:
+                raise RuntimeError(f"monotonic_rnnt: expected {B} input/label lengths, "
+                                   f"got {self.T_host.size}/{self.S_host.size}")
         lab = labels.detach()
         if lab.device != dev or lab.dtype != torch.int32:
             lab = lab.to(dev, torch.int32)
@@ -160,10 +225,10 @@ class _Prepared:
             lab = lab.view(B, -1)
         self.labels = lab.contiguous() if lab.numel() else torch.zeros(B, 1, dtype=torch.int32, device=dev)
         self.lattice = None
-        if self.on_gpu:
+        if self.on_gpu and not self.dyn:
             self.T_dev, self.S_dev, self.lattice = ln.on(dev)
-            if not labels.is_cuda:
-                _check_labels(labels, self.S_host, acts.size(-1))
+        if self.on_gpu and not labels.is_cuda and not self.dyn:
+            _check_labels(labels, self.S_host, acts.size(-1))
         self.alignment = None
         if alignment is not None:
             al = alignment.detach().to(dev, torch.int32)
@@ -173,12 +238,18 @@ class _Prepared:
         p.V = self.acts.size(-1)
         p.blank = int(blank_label)
         p.max_shift = int(max_shift)
-        p.T_host = ln.T_ptr
-        p.S_host = ln.S_ptr
+        if self.dyn:
+            p.lengths_on_device = 1
+            # (first allocated outside graph capture; a capture that comes first fails closed without the report)
+            if _STATUS is not None or not torch.cuda.is_current_stream_capturing():
+                p.status_host = ctypes.cast(_status_word(), ctypes.c_void_p).value
+        else:
+            p.T_host = ln.T_ptr
+            p.S_host = ln.S_ptr
         if self.on_gpu:
             p.T_dev = self.T_dev.data_ptr()
             p.S_dev = self.S_dev.data_ptr()
-            p.lattice = self.lattice.data_ptr()
+            p.lattice = self.lattice.data_ptr() if self.lattice is not None else None
         p.acts = self.acts.data_ptr()
         p.labels = self.labels.data_ptr()
         p.label_stride = self.labels.size(1)
@@ -198,12 +269,20 @@ class _Prepared:
 
     def workspace(self) -> torch.Tensor:
         key = (self.on_gpu, self.alignment is not None, _L.load())
-        n = self.lengths.ws.get(key)  # a function of the lengths and the alignment flag only
+        if self.dyn:  # sized from bounds: the shapes of acts and labels
+            p = self.problem
+            key = key + (p.B, p.num_rows, p.label_stride, p.pad_T, p.pad_S1)
+            cache = _DYN_WS
+        else:
+            cache = self.lengths.ws  # a function of the lengths and the alignment flag only
+        n = cache.get(key)
         if n is None:
             c = ctypes.c_size_t(0)
             fn = _L.load().mrnnt_workspace_size if self.on_gpu else _L.load().mrnnt_cpu_workspace_size
             _L.check(fn(ctypes.byref(self.problem), ctypes.byref(c)), "workspace_size")
-            n = self.lengths.ws[key] = max(1, c.value)
+            n = cache[key] = max(1, c.value)
+            if self.dyn and len(_DYN_WS) > 256:
+                _DYN_WS.clear()
         return torch.empty(n, dtype=torch.uint8, device=self.device)
 
     def stream(self):
@@ -241,9 +320,14 @@ def _forward(prep: _Prepared, with_beta: bool):
         _L.check(lib.mrnnt_cpu_forward(ctypes.byref(prep.problem), _ptr(ws), ws.numel(), _ptr(costs),
                                        1 if with_beta else 0, prep.num_threads), "mrnnt_cpu_forward")
         return costs, ws
+    if prep.dyn:
+        check_lengths(sync=False)  # an earlier call's failed validation surfaces here (no wait)
     with _on_device(prep.device):  # kernels go to this device's current stream
         _L.check(lib.mrnnt_forward(ctypes.byref(prep.problem), _ptr(ws), ws.numel(), _ptr(costs),
                                    1 if with_beta else 0, prep.stream()), "mrnnt_forward")
+        if prep.dyn and _SYNC_LENGTH_CHECK and not torch.cuda.is_current_stream_capturing():
+            torch.cuda.current_stream(prep.device).synchronize()
+            check_lengths(sync=False)
     return costs, ws
 
 
@@ -392,4 +476,4 @@ class _Ext:
 
 monotonic_rnnt_cpp = _Ext()
 
-__all__ = ["MonotonicRNNTFunction", "monotonic_rnnt_loss", "MonotonicRNNTLoss", "monotonic_rnnt_cpp"]
+__all__ = ["MonotonicRNNTFunction", "monotonic_rnnt_loss", "MonotonicRNNTLoss", "monotonic_rnnt_cpp", "check_lengths"]

@@ -1,0 +1,94 @@
+// gpu_ref_client.cpp -- reference-API GPU client compiled against THIS repository's headers (include/) and linked
+// against libmonotonic_rnnt_amd.so: it drives GpuRNNTWorkspaceManager<float> + GpuRNNTComputer<float> the way the
+// reference's pytorch_binding/monotonic_rnnt.cu:81-152 does, then reads the workspace back through every public
+// host getter of the reference's manager (gpu_workspace_manager.h:87-190), as the reference's own computer and debug
+// paths call them (gpu_rnnt.h:28-35,53-54,118-119,133,166,180). tests/test_ref_client.py compares the read-backs
+// with the golden denom_f64 / alpha_f64 / beta_f64 of the reference itself.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "gpu_rnnt.h"
+#include "gpu_workspace_manager.h"
+
+template <typename T>
+static T *to_gpu(const T *h, size_t n) {
+    T *p = nullptr;
+    if (hipMalloc(&p, std::max<size_t>(1, n) * sizeof(T)) != hipSuccess) return nullptr;
+    if (n && hipMemcpy(p, h, n * sizeof(T), hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+    return p;
+}
+
+template <typename T>
+static int put(const std::vector<T> &v, T *out, size_t expect) {
+    if (!out) return 0;
+    if (v.size() != expect) return 1;
+    std::copy(v.begin(), v.end(), out);
+    return 0;
+}
+
+extern "C" {
+
+// sizes: N = sum_b T_b (S_b+1) rows; labels [B, max S] (the reference's stride), alignment [B, max T] or NULL.
+// Outputs (host, any may be NULL): costs [B], grads [N, V] (NULL: cost() only), denom / alphas / betas [N],
+// ll_fwd / ll_bwd [B], min_s / max_s [B * max T], var_off [B], sizes[4] = {num_denoms, num_fwd_bwd_var_positions,
+// S_max, T_max}, acts_back [N * V]. Returns the number of failed calls / size mismatches (0 = all good).
+int client_gpu_getters(const float *acts, const int *labels, int B, const int *T, const int *S, int V, int blank,
+                       const int *alignment, int max_shift, float *costs, float *grads, float *denom, float *alphas,
+                       float *betas, float *ll_fwd, float *ll_bwd, int *min_s, int *max_s, int *var_off, int *sizes,
+                       float *acts_back) {
+    int64_t N = 0;
+    int S_max = 0, T_max = 0;
+    for (int b = 0; b < B; ++b) {
+        N += (int64_t)T[b] * (S[b] + 1);
+        S_max = std::max(S_max, S[b]);
+        T_max = std::max(T_max, T[b]);
+    }
+    float *d_acts = to_gpu(acts, (size_t)N * V);
+    int *d_labels = to_gpu(labels, (size_t)B * S_max);
+    int *d_T = to_gpu(T, (size_t)B), *d_S = to_gpu(S, (size_t)B);
+    int *d_align = alignment ? to_gpu(alignment, (size_t)B * T_max) : nullptr;
+    float *d_grads = nullptr;
+    if (grads) (void)hipMalloc(&d_grads, (size_t)N * V * sizeof(float));
+    int bad = 0;
+    hipStream_t stream;
+    (void)hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
+    {
+        GpuRNNTWorkspaceManager<float> wm(d_acts, d_labels, B, d_T, d_S, V);
+        bad += wm.create_workspace() != RNNT_STATUS_SUCCESS;
+        if (d_align) wm.restrict_to_alignment(d_align, max_shift, blank);
+        GpuRNNTComputer<float> computer(wm, blank, stream);
+        std::vector<float> c(B);
+        bad += (grads ? computer.cost_and_grad(c.data(), d_grads) : computer.cost(c.data())) != RNNT_STATUS_SUCCESS;
+        if (costs) std::copy(c.begin(), c.end(), costs);
+        if (grads) bad += hipMemcpy(grads, d_grads, (size_t)N * V * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess;
+        const size_t n = (size_t)N;
+        bad += put(wm.denom_host(), denom, n);
+        bad += put(wm.alphas_host(), alphas, n);
+        if (grads) bad += put(wm.betas_host(), betas, n);
+        bad += put(wm.ll_forward_host(), ll_fwd, (size_t)B);
+        if (grads) bad += put(wm.ll_backward_host(), ll_bwd, (size_t)B);
+        bad += put(wm.min_allowed_s_host(), min_s, (size_t)B * T_max);
+        bad += put(wm.max_allowed_s_host(), max_s, (size_t)B * T_max);
+        bad += put(wm.var_start_offsets_host(), var_off, (size_t)B);
+        bad += put(wm.acts_host(), acts_back, n * V);
+        if (sizes) {
+            sizes[0] = wm.num_denoms();
+            sizes[1] = wm.num_fwd_bwd_var_positions();
+            sizes[2] = wm.S_max_host();
+            sizes[3] = wm.T_max_host();
+        }
+        bad += wm.B_host() != B || wm.V_host() != V;
+        const std::vector<int> Th = wm.T_host(), Sh = wm.S_host();
+        bad += !std::equal(Th.begin(), Th.end(), T) || !std::equal(Sh.begin(), Sh.end(), S);
+        wm.free_workspace();
+    }
+    (void)hipStreamDestroy(stream);
+    for (void *p : {(void *)d_acts, (void *)d_labels, (void *)d_T, (void *)d_S, (void *)d_align, (void *)d_grads})
+        if (p) (void)hipFree(p);
+    return bad;
+}
+}

@@ -267,10 +267,12 @@ def test_grads_placement_arena_on_device(op, dev, monkeypatch):
 
 
 @pytest.mark.parametrize("aligned", [False, True])
-def test_hip_graph_capture_replay(op, dev, aligned):
+@pytest.mark.parametrize("device_lengths", [False, True], ids=["host_T_S", "device_T_S"])
+def test_hip_graph_capture_replay(op, dev, aligned, device_lengths):
     """Forward + backward captured once in a HIP graph (torch.cuda.graph) and replayed on new logits written
     into the captured input: costs and gradients equal an eager call on the same logits and the oracle (the
-    op makes no host synchronisation and allocates only through torch, so it is capture-safe)."""
+    op makes no host synchronisation and allocates only through torch, so it is capture-safe). With device T / S
+    (the reference's calling convention) nothing is planned from the lengths on the host at all."""
     rng = np.random.default_rng(40 + aligned)
     acts1, labels, T, S = random_problem(rng, 5, (30, 120), 25, 128)
     acts2 = rng.standard_normal(acts1.shape).astype(np.float32) * 2
@@ -283,6 +285,8 @@ def test_hip_graph_capture_replay(op, dev, aligned):
         al = _t(al_np, dev)
     a = _t(acts1, dev).requires_grad_(True)
     lab, Tt, St = _t(labels, dev), torch.from_numpy(T), torch.from_numpy(S)
+    if device_lengths:
+        Tt, St = Tt.to(dev), St.to(dev)
     k = 3 if aligned else 0
 
     def fwd_bwd():
