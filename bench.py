@@ -494,7 +494,10 @@ def placement_log():
     """The gradient-buffer placement decisions of this process (pytorch_binding/_grads_placement.py): per decision
     the fill rate of each candidate block and the one kept; None when no call was large enough."""
     import _grads_placement as GP
-    return (GP.ARENA.log or None) if GP.enabled() else "disabled"
+    if not GP.enabled():
+        return "disabled"
+    return {"decisions": GP.ARENA.log or None, **GP.ARENA.stats,
+            "fired": GP.ARENA.stats["handed_out"] > 0}
 
 
 def same_buffers_copy_gbps(L, dev, src_t, dst_t, gib=8, reps=5):

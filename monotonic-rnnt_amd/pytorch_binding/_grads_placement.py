@@ -9,13 +9,21 @@ allocator, which hands the same block to every later step, keeps a slow draw for
 
 For gradient outputs of at least MIN_BYTES this module keeps one buffer per (device, dtype), chosen once: a
 candidate from the caching allocator is timed with one nontemporal zero fill over its whole length
-(mrnnt_fill_zero, the gradient pass's store stream: ~8 ms for 52.7 GB); below FAST_GBPS a further candidate is
-allocated while the earlier ones are still held (so it is a different block), up to MAX_CANDIDATES or until HBM
-runs short, and the fastest is kept (the others go back to the caching allocator). Later calls get a view of the
-kept buffer whenever nothing else holds it (storage use count 1: e.g. the previous step's acts.grad was
-dropped), and a plain allocation otherwise, so a caller that keeps gradients across calls never sees them
-overwritten. Under HIP-graph capture the graph's memory pool serves gradients as usual. MRNNT_GRADS_PLACEMENT=0
-turns this off (plain torch.empty_like); release() drops the kept buffers.
+(mrnnt_fill_zero, the gradient pass's store stream: ~8 ms for 52.7 GB); below FAST_GBPS ONE further candidate is
+allocated while the first is still held (so it is a different block) when free memory allows (>= 3x the need),
+and the faster is kept; the other candidate is released to the driver (torch.cuda.empty_cache), so the caching
+allocator holds no second block of that size.
+
+Reuse is safe by construction: the kept buffer is only ever caching-allocator memory, and it goes back through the
+allocator at every reuse. Each call hands out a view of the kept storage; on the next call, if nothing else holds
+it (storage use count 1: the caller dropped the previous gradient), the module drops its own reference -- the
+allocator then honours every stream the caller recorded on it (Tensor.record_stream: the block is not reusable
+until those streams pass their events) -- and immediately asks the allocator for the same size on the current
+stream. When the block is ready the allocator's best fit returns that very block (a "hit": the fast placement is
+kept); when a side stream still uses it, or the stream differs, it returns another block, which becomes the kept
+one (a "miss", counted). A gradient the caller still holds is never reused (plain allocation). Under HIP-graph
+capture the graph's memory pool serves gradients as usual. MRNNT_GRADS_PLACEMENT=0 turns this off (plain
+torch.empty_like), and so does a torch without the storage use count; release() drops the kept buffers.
 """
 from __future__ import annotations
 
@@ -28,8 +36,8 @@ import torch
 
 MIN_BYTES = 4 << 30        # below this a slow draw costs under a millisecond: plain allocations
 FAST_GBPS = 6300.0         # whole-buffer nontemporal fill rate of the fast classes (6.5-7.2 TB/s measured)
-MAX_CANDIDATES = 5         # HBM is the usual limit: 4 candidates of 52.7 GB beside the headline's acts
-HBM_RESERVE = 4 << 30      # free device memory left untouched when trying a further candidate
+MAX_CANDIDATES = 2         # the first draw and at most one more
+FREE_FACTOR = 3            # a further candidate only while free memory is >= FREE_FACTOR x its size
 
 
 # storage use count (private torch API, present in 2.x): without it a kept buffer could not be proven unshared,
@@ -42,10 +50,10 @@ def enabled() -> bool:
 
 
 class _Kept:
-    __slots__ = ("storage", "nbytes", "gbps")
+    __slots__ = ("storage", "ptr", "nbytes", "gbps")
 
-    def __init__(self, storage, nbytes: int, gbps: float):
-        self.storage, self.nbytes, self.gbps = storage, nbytes, gbps
+    def __init__(self, storage, nbytes: int, gbps: Optional[float]):
+        self.storage, self.ptr, self.nbytes, self.gbps = storage, storage.data_ptr(), nbytes, gbps
 
 
 def _fill_gbps(buf: torch.Tensor) -> float:
@@ -78,15 +86,22 @@ class GradsArena:
     def __init__(self, probe: Callable[[torch.Tensor], float] = _fill_gbps,
                  free_bytes: Callable[[torch.device], int] = _free_bytes,
                  alloc: Optional[Callable[[int, torch.device], torch.Tensor]] = None,
+                 release_unused: Optional[Callable[[], None]] = None,
                  fast_gbps: float = FAST_GBPS, max_candidates: int = MAX_CANDIDATES, min_bytes: int = MIN_BYTES,
-                 require_cuda: bool = True):
+                 require_cuda: bool = True, allocator_refs: int = 0,
+                 on_release: Optional[Callable[[int], None]] = None):
         self._probe, self._free = probe, free_bytes
         self._alloc = alloc or (lambda n, dev: torch.empty(n, dtype=torch.uint8, device=dev))
+        self._release_unused = release_unused or (lambda: torch.cuda.empty_cache())
         self.fast_gbps, self.max_candidates, self.min_bytes = fast_gbps, max_candidates, min_bytes
         self.require_cuda = require_cuda
+        self._on_release = on_release  # test hook: told the address of every block this arena lets go of
+        self._held = 1 + allocator_refs  # storage references when only this arena holds the block (a test
+        #                                 allocator may keep one of its own)
         self._kept: Dict[Tuple[torch.device, torch.dtype], _Kept] = {}
         self._lock = threading.Lock()
         self.log: List[dict] = []  # one record per placement decision (bench.py reports it)
+        self.stats = {"handed_out": 0, "reuse_hits": 0, "reuse_misses": 0, "held_by_caller": 0}
 
     def like(self, acts: torch.Tensor) -> torch.Tensor:
         """A contiguous uninitialised tensor of acts' shape, dtype and device."""
@@ -96,15 +111,33 @@ class GradsArena:
         key = (acts.device, acts.dtype)
         with self._lock:
             kept = self._kept.get(key)
-            if kept is not None and _use_count(kept.storage._cdata) > 1:
+            if kept is not None and _use_count(kept.storage._cdata) > self._held:
+                self.stats["held_by_caller"] += 1
                 return torch.empty_like(acts, memory_format=torch.contiguous_format)  # still held by the caller
-            if kept is None or kept.nbytes < nbytes:
+            if kept is not None and kept.nbytes >= nbytes:
+                ptr, kb, gbps = kept.ptr, kept.nbytes, kept.gbps
+                del self._kept[key]
+                kept = None  # the last reference: the caching allocator owns the block, with the caller's streams
+                if self._on_release:
+                    self._on_release(ptr)
+                kept = self._kept[key] = self._take_back(ptr, kb, gbps, acts.device)
+            else:
                 if kept is not None:
                     del self._kept[key]
                     kept = None  # the old block goes back to the caching allocator before the new one is chosen
                 kept = self._kept[key] = self._choose(nbytes, acts.device)
-        out = torch.empty(0, dtype=acts.dtype, device=acts.device)
-        return out.set_(kept.storage, 0, acts.shape, _contiguous_strides(acts.shape))
+            self.stats["handed_out"] += 1
+            out = torch.empty(0, dtype=acts.dtype, device=acts.device)
+            return out.set_(kept.storage, 0, acts.shape, _contiguous_strides(acts.shape))
+
+    def _take_back(self, ptr: int, nbytes: int, gbps: Optional[float], dev: torch.device) -> _Kept:
+        """After the kept block went back to the caching allocator: take the same size again (see the module doc)."""
+        buf = self._alloc(nbytes, dev)
+        if buf.data_ptr() == ptr:
+            self.stats["reuse_hits"] += 1
+            return _Kept(buf.untyped_storage(), nbytes, gbps)
+        self.stats["reuse_misses"] += 1  # still in use on another stream (or another stream's pool): a new block
+        return _Kept(buf.untyped_storage(), nbytes, None)
 
     def _choose(self, nbytes: int, dev: torch.device) -> _Kept:
         cands: List[Tuple[float, torch.Tensor]] = []
@@ -114,12 +147,21 @@ class GradsArena:
             best = max(c[0] for c in cands)
             if best >= self.fast_gbps or len(cands) >= self.max_candidates:
                 break
-            if self._free(dev) < nbytes + HBM_RESERVE:
+            if self._free(dev) < FREE_FACTOR * nbytes:
                 break
         rate, buf = max(cands, key=lambda c: c[0])
         self.log.append({"bytes": nbytes, "candidates_gbps": [round(c[0], 1) for c in cands],
                          "kept_gbps": round(rate, 1)})
-        return _Kept(buf.untyped_storage(), nbytes, rate)
+        kept = _Kept(buf.untyped_storage(), nbytes, rate)
+        if len(cands) > 1:
+            slower = [c[1].data_ptr() for c in cands if c[1] is not buf]
+            del buf
+            cands.clear()  # the slower candidate is unused now: back to the driver, not left cached beside ours
+            for q in slower:
+                if self._on_release:
+                    self._on_release(q)
+            self._release_unused()
+        return kept
 
     def release(self) -> None:
         with self._lock:

@@ -13,49 +13,81 @@ import _grads_placement as GP  # noqa: E402
 
 
 class Fake:
+    """A caching-allocator stand-in: it keeps every block it made (one tensor each, so a block the arena keeps has
+    storage use count 2 when nothing else uses it: allocator_refs=1); a block the arena lets go of (on_release) is
+    free again unless `busy` (another stream still uses it: the device allocator holds such a block back until
+    that stream passes its event), and alloc() hands a free block of the size back, as the device allocator's best
+    fit does."""
+
     def __init__(self, rates, free=1 << 60):
         self.rates = list(rates)
         self.free = free
-        self.allocs = []
+        self.blocks = {}    # data_ptr -> tensor
+        self.freed = set()
+        self.allocs = []    # data_ptr of every block handed out, in order
+        self.busy = set()
+        self.released = 0
 
     def probe(self, buf):
         return self.rates.pop(0)
 
     def alloc(self, n, dev):
-        t = torch.empty(n, dtype=torch.uint8)
-        self.allocs.append(t.data_ptr())
-        return t
+        for q in sorted(self.freed):
+            if self.blocks[q].numel() == n and q not in self.busy:
+                self.freed.discard(q)
+                blk = self.blocks[q]
+                break
+        else:
+            blk = torch.empty(n, dtype=torch.uint8)
+            self.blocks[blk.data_ptr()] = blk
+        self.allocs.append(blk.data_ptr())
+        return torch.empty(0, dtype=torch.uint8).set_(blk.untyped_storage())
+
+    def on_release(self, ptr):
+        self.freed.add(ptr)
+
+    def release_unused(self):
+        self.released += 1
+        for q in [q for q in self.freed if q not in self.busy]:
+            self.freed.discard(q)
+            del self.blocks[q]
 
     def arena(self, **kw):
-        return GP.GradsArena(probe=self.probe, free_bytes=lambda d: self.free, alloc=self.alloc, min_bytes=64,
-                             require_cuda=False, **kw)
+        return GP.GradsArena(probe=self.probe, free_bytes=lambda d: self.free, alloc=self.alloc,
+                             release_unused=self.release_unused, min_bytes=64, require_cuda=False, allocator_refs=1,
+                             on_release=self.on_release, **kw)
 
 
 def acts(rows=8, V=16, dtype=torch.float32):
     return torch.randn(rows, V).to(dtype)
 
 
-def test_keeps_fastest_of_candidates_and_stops_when_fast():
-    f = Fake([5000.0, 5400.0, 6900.0, 1.0])
+def test_keeps_faster_of_two_candidates_and_stops_when_fast():
+    f = Fake([5000.0, 5400.0, 1.0])
     ar = f.arena()
     g = ar.like(acts())
-    assert ar.log[-1]["candidates_gbps"] == [5000.0, 5400.0, 6900.0] and ar.log[-1]["kept_gbps"] == 6900.0
-    assert g.data_ptr() == f.allocs[2] and g.shape == (8, 16) and g.dtype == torch.float32 and g.is_contiguous()
+    assert ar.log[-1]["candidates_gbps"] == [5000.0, 5400.0] and ar.log[-1]["kept_gbps"] == 5400.0
+    assert g.data_ptr() == f.allocs[1] and g.shape == (8, 16) and g.dtype == torch.float32 and g.is_contiguous()
+    assert f.released == 1 and list(f.blocks) == [f.allocs[1]]  # the slower candidate went back to the driver
     f2 = Fake([6500.0])
     ar2 = f2.arena()
     ar2.like(acts())
-    assert ar2.log[-1]["candidates_gbps"] == [6500.0]  # fast first draw: no second candidate
+    assert ar2.log[-1]["candidates_gbps"] == [6500.0] and f2.released == 0  # fast first draw: no second candidate
 
 
-def test_max_candidates_and_free_memory_limit():
-    f = Fake([1.0, 3.0, 2.0, 9.0])
-    ar = f.arena(max_candidates=3)
+def test_candidate_limits():
+    f = Fake([1.0, 3.0, 9.0])
+    ar = f.arena(max_candidates=2)
     g = ar.like(acts())
-    assert ar.log[-1]["candidates_gbps"] == [1.0, 3.0, 2.0] and g.data_ptr() == f.allocs[1]
-    f = Fake([1.0, 9.0], free=0)  # no room for a second candidate
+    assert ar.log[-1]["candidates_gbps"] == [1.0, 3.0] and g.data_ptr() == f.allocs[1]
+    f = Fake([1.0, 9.0], free=3 * 512 - 1)  # a second candidate needs free memory >= 3x its size
     ar = f.arena()
     ar.like(acts())
     assert ar.log[-1]["candidates_gbps"] == [1.0]
+    f = Fake([1.0, 9.0], free=3 * 512)
+    ar = f.arena()
+    ar.like(acts())
+    assert ar.log[-1]["candidates_gbps"] == [1.0, 9.0]
 
 
 def test_reused_only_when_not_held():
@@ -113,3 +145,31 @@ def test_views_have_contiguous_strides(shape):
     a = torch.zeros(shape)
     g = ar.like(a)
     assert g.shape == a.shape and g.stride() == a.stride()
+
+
+def test_reuse_goes_back_through_the_allocator():
+    """A reused gradient is the kept block handed back by the allocator (a hit); a block another stream still uses
+    (Tensor.record_stream: the device allocator holds it until that stream passes its event) is not handed back,
+    and the arena takes and keeps the block the allocator gives instead (a miss) -- never the busy one."""
+    f = Fake([7000.0])
+    ar = f.arena()
+    a = acts()
+    g1 = ar.like(a)
+    p = g1.data_ptr()
+    del g1
+    g2 = ar.like(a)
+    assert g2.data_ptr() == p and ar.stats["reuse_hits"] == 1
+    f.busy.add(p)  # a side stream still reads the previous gradient
+    del g2
+    g3 = ar.like(a)
+    q = g3.data_ptr()
+    assert q != p and ar.stats["reuse_misses"] == 1
+    del g3
+    f.busy.clear()
+    assert ar.like(a).data_ptr() in (p, q)  # either free block of the size, as the allocator's best fit picks
+    assert len(ar.log) == 1  # no new probe: placement decisions only at the first choice
+
+
+def test_no_use_count_means_plain(monkeypatch):
+    monkeypatch.setattr(GP, "_use_count", None)
+    assert not GP.enabled()
