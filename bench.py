@@ -207,6 +207,17 @@ def run(args, world):
     def coll(x):  # gloo collectives run on host tensors
         return x.cpu() if gloo else x
 
+    # which device each rank drives (LOCAL_RANK -> device index, PCI bus): under RCCL every rank owns its own GPU
+    props = torch.cuda.get_device_properties(dev)
+    me = {"rank": rank, "local_rank": local_rank, "device": dev_index,
+          "pci_bus": getattr(props, "pci_bus_id", None), "pci_device": getattr(props, "pci_device_id", None)}
+    rank_devices = [me]
+    if world > 1:
+        rank_devices = [None] * world
+        dist.all_gather_object(rank_devices, me)
+        if not gloo and len({(d["device"], d["pci_bus"], d["pci_device"]) for d in rank_devices}) != world:
+            raise SystemExit(f"bench.py: ranks share a GPU under RCCL: {rank_devices}")
+
     def barrier():
         if world > 1:
             dist.barrier()
@@ -413,7 +424,7 @@ def run(args, world):
     achieved = grad_bytes * prof_steps / (g_ms * 1e-3) / 1e9 if g_ms else None
     g_avg = g_ms / g_n if g_ms else None
 
-    traffic = None
+    traffic = traffic_source = None  # PMC traffic is counted by rocprofv3 in its own run (tools/gpu_profile.sh)
     pmc_path = os.path.join(ROOT, "profiles", "pmc_grad_traffic.json")
     if os.path.exists(pmc_path) and mode == "resident" and not args.tune:
         try:
@@ -425,6 +436,8 @@ def run(args, world):
                     and pm.get("kernel", "").startswith(f"grad_staged_kernel<{ek}")
                     and pm.get("algorithmic_bytes_per_launch") == grad_bytes // n_chunks):
                 traffic = pm.get("hbm_bytes_per_launch")
+                traffic_source = {"file": os.path.relpath(pmc_path, ROOT), "run": pm.get("source"),
+                                  "measured_in_this_run": False}
         except Exception:
             traffic = None
 
@@ -456,6 +469,7 @@ def run(args, world):
                        "memory_mode": mode, "chunks_per_step": n_chunks,
                        "execution": "hip_graph_replay" if args.graph else "eager",
                        "lengths": "device" if (args.device_lengths or mode != "resident") else "host",
+                       "rank_devices": rank_devices,
                        **({"window_rows_per_gpu": n_window} if n_window is not None else {}),
                        "parallelism": f"dp{world} (batch-sharded, one 4-byte "
                                       f"{'gloo (rehearsal)' if gloo else 'RCCL'} loss all-reduce)"},
@@ -463,7 +477,8 @@ def run(args, world):
             "roofline": {"kernel": "logit gradient", "bound": "hbm",
                          "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4) if achieved else None,
-                         "traffic": traffic, "algorithmic_bytes_per_launch": grad_bytes // n_chunks,
+                         "traffic": traffic, "traffic_source": traffic_source,
+                         "algorithmic_bytes_per_launch": grad_bytes // n_chunks,
                          "avg_launch_ms": round(g_avg, 4) if g_avg else None,
                          "live_rows": live, "inband_rows": n_band,
                          "formula_bytes_per_launch": formula_grad_bytes // n_chunks,

@@ -255,6 +255,10 @@ DevProblem make_dev(const mrnnt_problem *p, const Plan &pl, const void *ws) {
     d.llb = reinterpret_cast<double *>(w + pl.off_llb);
     d.dyn = pl.dyn ? reinterpret_cast<DynWords *>(w + pl.off_dyn) : nullptr;
     d.steal = 0;
+    d.dyn_fused = 0;
+    d.s_cap = d.t_cap = d.s1_cap = 0;
+    d.scatter_above = INT64_MAX;
+    d.status_host = nullptr;
     return d;
 }
 
@@ -408,7 +412,14 @@ RNNTStatus mrnnt_forward(const mrnnt_problem *p, void *ws, size_t ws_bytes, floa
     DevProblem d = make_dev(p, pl, ws);
     char *w = static_cast<char *>(ws);
     hipError_t e = hipSuccess;
-    if (pl.dyn) {  // device-resident lengths: offsets, column map and validation in one launch, no read-back
+    // device-resident lengths of a small batch without an alignment: planned inside the log-softmax launch itself
+    // (every wave holds the lengths in registers, walk_columns in mrnnt_device.h) -- no separate setup kernel, whose
+    // ~4.7 us launch would be 5 % of a configs[1] step; otherwise one setup kernel before the passes
+    const bool fused = pl.dyn && pl.B <= 64 && !pl.align && tuning().softmax_grid_per_cu <= 0 && tuning().dyn_fused;
+    const int64_t scatter_above = ((tuning().col_scatter & 3) != 0 && !(tuning().col_xcd & 3))
+                                      ? (int64_t)streaming_grid(pl.cols, tuning().grad_grid_per_cu)
+                                      : INT64_MAX;
+    if (pl.dyn && !fused) {  // device-resident lengths: offsets, column map and validation in one launch, no read-back
         DynSetupArgs a;
         std::memset(&a, 0, sizeof(a));
         if ((st = status_device_ptr(p, &a.status_host)) != RNNT_STATUS_SUCCESS) return st;
@@ -422,7 +433,9 @@ RNNTStatus mrnnt_forward(const mrnnt_problem *p, void *ws, size_t ws_bytes, floa
         a.T_cap = pl.pad_S1 ? pl.pad_T : 0;
         if (p->alignment) a.T_cap = a.T_cap ? std::min<int64_t>(a.T_cap, p->align_stride) : p->align_stride;
         a.S1_cap = pl.pad_S1;
-        a.scatter = (tuning().col_scatter & 3) != 0 && !(tuning().col_xcd & 3);
+        // the scattered order only matters where a workgroup walks several columns: the gradient's persistent grid
+        // (the log-softmax's default is in order)
+        a.scatter_above = scatter_above;
         a.row_off = reinterpret_cast<int64_t *>(w + pl.off_row);
         a.col_off = reinterpret_cast<int64_t *>(w + pl.off_col);
         a.col_b = reinterpret_cast<int *>(w + pl.off_colb);
@@ -431,7 +444,7 @@ RNNTStatus mrnnt_forward(const mrnnt_problem *p, void *ws, size_t ws_bytes, floa
         a.dyn = d.dyn;
         e = timed(K_SETUP, stream, [&] { return launch_setup_dyn(a, stream); });
         if (e != hipSuccess) return fail_hip(e, "device-lengths setup kernel");
-    } else if (!p->lattice) {  // lattice offsets on the device (the log-softmax kernel zeroes the lp pads itself)
+    } else if (!pl.dyn && !p->lattice) {  // lattice offsets on the device (the log-softmax kernel zeroes the lp pads)
         e = timed(K_SETUP, stream, [&] {
             return launch_setup(p->T_dev, p->S_dev, pl.B, reinterpret_cast<int64_t *>(w + pl.off_row),
                                 reinterpret_cast<int64_t *>(w + pl.off_col),
@@ -448,12 +461,25 @@ RNNTStatus mrnnt_forward(const mrnnt_problem *p, void *ws, size_t ws_bytes, floa
         if (e != hipSuccess) return fail_hip(e, "alignment band kernels");
     }
     int grid = streaming_grid(pl.cols, tuning().softmax_grid_per_cu);
-    if (pl.dyn && tuning().softmax_grid_per_cu <= 0) {  // one workgroup per column needs the column count
+    DevProblem ds = d;  // the log-softmax launch's view
+    ds.col_mul = column_order(pl, 1);
+    if (fused) {
+        // one workgroup per column at the lower bound of the column count, rows / (label stride + 1) (exact when every
+        // S_b equals the stride; more columns are walked grid-stride), or B * pad_T for the padded layout
+        const int64_t lower = pl.pad_S1 ? pl.cols : (pl.N + pl.S_max) / (pl.S_max + 1);
+        grid = (int)std::max<int64_t>(1, std::min<int64_t>(lower, 1 << 22));
+        ds.dyn_fused = 1;
+        ds.s_cap = pl.S_max;
+        ds.t_cap = pl.pad_S1 ? pl.pad_T : 0;
+        ds.s1_cap = pl.pad_S1;
+        ds.scatter_above = scatter_above;
+        ds.col_mul = 0;
+        if ((st = status_device_ptr(p, &ds.status_host)) != RNNT_STATUS_SUCCESS) return st;
+    } else if (pl.dyn && tuning().softmax_grid_per_cu <= 0) {  // one workgroup per column needs the column count
         grid = streaming_grid(pl.cols, kStealGridPerCU);
-        d.steal = grid < pl.cols;
+        ds.steal = grid < pl.cols;
     }
-    d.col_mul = column_order(pl, 1);
-    e = timed(K_SOFTMAX, stream, [&] { return launch_softmax(d, pl.elem, grid, stream); });
+    e = timed(K_SOFTMAX, stream, [&] { return launch_softmax(ds, pl.elem, grid, stream); });
     if (e != hipSuccess) return fail_hip(e, "log-softmax kernel");
     e = timed(K_DP, stream, [&] { return launch_dp(d, pl.S_max, with_beta ? 1 : 0, costs_dev, stream); });
     if (e != hipSuccess) return fail_hip(e, "alpha/beta kernel");
@@ -560,6 +586,7 @@ RNNTStatus mrnnt_read_band(const mrnnt_problem *p, void *ws, int *min_dev, int *
         a.T_cap = pl.pad_S1 ? pl.pad_T : 0;
         if (p->alignment) a.T_cap = a.T_cap ? std::min<int64_t>(a.T_cap, p->align_stride) : p->align_stride;
         a.S1_cap = pl.pad_S1;
+        a.scatter_above = INT64_MAX;
         a.row_off = reinterpret_cast<int64_t *>(w + pl.off_row);
         a.col_off = reinterpret_cast<int64_t *>(w + pl.off_col);
         a.col_b = reinterpret_cast<int *>(w + pl.off_colb);
@@ -900,6 +927,7 @@ __attribute__((visibility("default"))) int mrnnt_tune(const char *key, int value
         return prev;
     }
     else if (!std::strcmp(key, "nt_store")) slot = &t.nt_store;
+    else if (!std::strcmp(key, "dyn_fused")) slot = &t.dyn_fused;
     else if (!std::strcmp(key, "nt_load")) slot = &t.nt_load;
     else if (!std::strcmp(key, "occ_skip")) slot = &t.occ_skip;
     else if (!std::strcmp(key, "joint_nbuf")) slot = &t.joint_nbuf;

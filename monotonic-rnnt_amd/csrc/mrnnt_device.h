@@ -111,9 +111,10 @@ __device__ __forceinline__ int64_t visit_col(const DevProblem &p, int64_t ci) {
 
 // Device-resident lengths: the real column / row counts and the column-order multiplier published by the call's
 // setup kernel replace the host bounds in the kernel's copy of the problem. Returns false when the lengths failed
-// validation (then num_cols = 0: column walks do nothing). Without device lengths: a no-op returning true.
+// validation (then num_cols = 0: column walks do nothing). Without device lengths, and in the log-softmax launch
+// that plans them itself (dyn_fused, before the words exist): a no-op returning true.
 __device__ __forceinline__ bool resolve_dyn(DevProblem &p) {
-    if (!p.dyn) return true;
+    if (!p.dyn || p.dyn_fused) return true;
     const int st = __builtin_amdgcn_readfirstlane(p.dyn->status);
     if (st) {
         p.num_cols = 0;
@@ -131,16 +132,152 @@ __device__ __forceinline__ int64_t uniform64(int64_t v) {
     return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 
+__device__ __forceinline__ int64_t readlane64(int64_t v, int lane) {
+    const int lo = __builtin_amdgcn_readlane((int)(uint32_t)v, lane);
+    const int hi = __builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), lane);
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+// One lattice column as a streaming kernel walks it: column c = (utterance b, frame t), lattice row of (t, 0).
+struct ColRef {
+    int64_t c;
+    int b, T, S, t;
+    int64_t rowc;
+};
+
+__device__ __forceinline__ ColRef col_ref(const DevProblem &p, int64_t c) {
+    ColRef k;
+    k.c = c;
+    k.b = p.col_b[c];
+    k.T = p.T[k.b];
+    k.S = p.S[k.b];
+    k.t = (int)(c - p.col_off[k.b]);
+    k.rowc = p.row_off[k.b] + (int64_t)k.t * (k.S + 1);
+    return k;
+}
+
+// dyn_fused: the lengths of a batch of <= 64 utterances in the registers of every wave -- lane b holds T_b, S_b and
+// the inclusive prefix sums of the columns and rows -- so a column's utterance is one ballot away.
+struct WaveLengths {
+    int T, S;
+    int64_t cols, rows;  // inclusive prefix sums at lane b (lanes >= B: the totals)
+    int64_t C, R;        // totals (uniform)
+    bool ok;             // every length valid and the totals inside the host's plan (uniform)
+};
+
+__device__ __forceinline__ int64_t wave_incl_scan64(int64_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int64_t u = __shfl_up(v, off);
+        if (lane >= off) v += u;
+    }
+    return v;
+}
+
+__device__ __forceinline__ WaveLengths wave_lengths(const DevProblem &p) {
+    const int lane = threadIdx.x & 63;
+    const bool in = lane < p.B;
+    WaveLengths w;
+    w.T = in ? p.T[lane] : 0;
+    w.S = in ? p.S[lane] : 0;
+    const bool good = !in || (w.T > 0 && w.S >= 0 && w.T >= w.S && w.S <= p.s_cap && (p.t_cap == 0 || w.T <= p.t_cap) &&
+                              (p.s1_cap == 0 || (int64_t)w.S + 1 <= p.s1_cap));
+    w.cols = wave_incl_scan64((in && good) ? w.T : 0);
+    w.rows = wave_incl_scan64((in && good) ? (int64_t)w.T * (w.S + 1) : 0);
+    w.C = readlane64(w.cols, 63);
+    w.R = readlane64(w.rows, 63);
+    w.ok = __ballot(!good) == 0 && (p.pad_S1 ? w.R <= p.num_rows : w.R == p.num_rows) && w.C <= p.num_cols;
+    return w;
+}
+
+__device__ __forceinline__ ColRef wave_locate(const WaveLengths &w, int64_t c) {
+    ColRef k;
+    k.c = c;
+    k.b = __popcll(__ballot(w.cols <= c));  // utterances whose columns all lie before c
+    k.T = __builtin_amdgcn_readlane(w.T, k.b);
+    k.S = __builtin_amdgcn_readlane(w.S, k.b);
+    const int64_t c0 = k.b ? readlane64(w.cols, k.b - 1) : 0;
+    const int64_t r0 = k.b ? readlane64(w.rows, k.b - 1) : 0;
+    k.t = (int)(c - c0);
+    k.rowc = r0 + (int64_t)k.t * (k.S + 1);
+    return k;
+}
+
+// dyn_fused, workgroup 0 (wave 0): what the setup kernel would have written -- lattice offsets, DynWords, status
+// report, the lp pads around [0, R) -- for the recursion and gradient kernels that follow in the stream.
+__device__ __forceinline__ void publish_lengths(const DevProblem &p, const WaveLengths &w) {
+    const int lane = threadIdx.x & 63;
+    if (threadIdx.x >= 64) return;
+    int64_t *row_off = const_cast<int64_t *>(p.row_off);
+    int64_t *col_off = const_cast<int64_t *>(p.col_off);
+    if (lane < p.B) {
+        row_off[lane + 1] = w.ok ? w.rows : 0;
+        col_off[lane + 1] = w.ok ? w.cols : 0;
+    }
+    int64_t mul = 0;
+    if (w.ok && w.C > p.scatter_above && w.C >= 3 && w.C < (1ll << 31)) {  // as setup_dyn_kernel
+        for (uint32_t base = max(2u, (uint32_t)(0.6180339887 * (double)w.C));; base += 64) {
+            uint32_t x = base + lane, y = (uint32_t)w.C;
+            while (y) {
+                const uint32_t rem = x % y;
+                x = y;
+                y = rem;
+            }
+            const unsigned long long hit = __ballot(x == 1);
+            if (hit) {
+                mul = (int64_t)base + __ffsll((long long)hit) - 1;
+                break;
+            }
+        }
+    }
+    if (lane == 0) {
+        row_off[0] = 0;
+        col_off[0] = 0;
+        DynWords *d = p.dyn;
+        d->status = w.ok ? 0 : (int)RNNT_STATUS_INVALID_VALUE;
+        d->num_cols = w.ok ? w.C : 0;
+        d->num_rows = w.ok ? w.R : 0;
+        d->col_mul = mul;
+        d->steal = 0;
+        if (!w.ok && p.status_host)  // a plain system-scope store into the caller's host-mapped word
+            __hip_atomic_store(p.status_host, (int)RNNT_STATUS_INVALID_VALUE, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    const int64_t end = w.ok ? w.R : 0;
+    p.lpb[lane - 64] = 0.0;
+    p.lpe[lane - 64] = 0.0;
+    p.lpb[end + lane] = 0.0;
+    p.lpe[end + lane] = 0.0;
+}
+
 // Column walk of a workgroup of a streaming kernel: visits ci = blockIdx.x, blockIdx.x + gridDim.x, ... < num_cols,
-// calling body(ci) (the whole workgroup, uniform ci). With p.steal (device-resident lengths, whose column count the
-// host does not know: the grid is sized to the CUs, not to the columns) the first gridDim.x columns go to the
-// workgroups in order and every later one to the workgroup that finishes first -- a shared counter the setup kernel
-// zeroed, the next index requested at the start of a column and handed over through LDS at its end (one barrier per
-// column), so a persistent grid balances like the hardware-scheduled one-workgroup-per-column launch.
+// calling body(ColRef) for column visit_col(ci) (the whole workgroup, uniform). With p.steal (device-resident lengths
+// with a separate setup kernel, whose column count the host does not know: the grid is sized to the CUs) the first
+// gridDim.x columns go to the workgroups in order and every later one to the workgroup that finishes first -- a
+// shared counter the setup kernel zeroed, the next index requested at the start of a column and handed over through
+// LDS at its end (one barrier per column), so a persistent grid balances like the hardware-scheduled
+// one-workgroup-per-column launch. With p.dyn_fused the walk locates its columns from the lengths in registers (no
+// column map yet: it writes one for the later kernels) over a grid the host sized to the lower bound of the column
+// count (rows / (label stride + 1)): exactly one column per workgroup when every S_b equals the bound.
 template <class F>
 __device__ __forceinline__ void walk_columns(const DevProblem &p, F &&body) {
-    if (!p.steal) {
-        for (int64_t ci = blockIdx.x; ci < p.num_cols; ci += gridDim.x) body(ci);
+    if (p.dyn_fused) {
+        const WaveLengths w = wave_lengths(p);
+        if (blockIdx.x == 0) publish_lengths(p, w);
+        if (!w.ok) return;
+        int *col_b = const_cast<int *>(p.col_b);
+        for (int64_t c = blockIdx.x; c < w.C; c += gridDim.x) {
+            const ColRef k = wave_locate(w, c);
+            if (threadIdx.x == 0) col_b[c] = k.b;  // the column map of the recursion / gradient kernels
+            body(k);
+        }
+        return;
+    }
+    // (a grid that covers every column -- known here, after resolve_dyn -- needs no counter: one atomic per workgroup
+    // on one address would serialise thousands of workgroups for nothing)
+    if (!p.steal || (int64_t)gridDim.x >= p.num_cols) {
+        for (int64_t ci = blockIdx.x; ci < p.num_cols; ci += gridDim.x) body(col_ref(p, visit_col(p, ci)));
         return;
     }
     __shared__ int64_t next_col[2];
@@ -149,7 +286,7 @@ __device__ __forceinline__ void walk_columns(const DevProblem &p, F &&body) {
     while (ci < p.num_cols) {
         unsigned long long mine = 0;
         if (threadIdx.x == 0) mine = atomicAdd(&p.dyn->steal, 1ull);
-        body(ci);
+        body(col_ref(p, visit_col(p, ci)));
         if (threadIdx.x == 0) next_col[par] = (int64_t)gridDim.x + (int64_t)mine;
         __syncthreads();
         ci = uniform64(next_col[par]);

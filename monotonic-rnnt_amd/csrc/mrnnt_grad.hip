@@ -378,20 +378,27 @@ static bool vec_ok(const DevProblem &p, const void *grads) {
 
 template <class IO, bool NTL, bool NTS, int U>
 static void launch_u(const DevProblem &p, const float *scale, void *grads, int grid, hipStream_t stream) {
-    const int variant = tuning().grad_variant;
     constexpr int RD = U == 4 ? 1 : (U == 2 ? 2 : 4);  // rows per wave: >= 4 KiB of acts in flight per wave
-    if (variant == 3 && p.pad_S1 == 0)
-        grad_rows_kernel<IO, U, NTL, NTS><<<grid, 256, 0, stream>>>(p, scale, grads);
-    else if (variant == 0)
-        grad_kernel<IO, U, RD, NTL, NTS><<<grid, 256, 0, stream>>>(p, scale, grads);
-    else if (variant == 2 || (variant == 5 && U == 1 && NTL))
-        // 1 KiB rows streamed from HBM: per-row coefficients, 2 rows per wave (configs[1] shape with nontemporal
-        // loads: 50.0 us against 56.3 for 4 rows and 60.2 staged, profiles/r02/kbench/grad_short_rows_c2*.json)
-        grad_kernel<IO, U, 2, NTL, NTS><<<grid, 256, 0, stream>>>(p, scale, grads);
-    else if (variant == 6)
-        grad_staged_kernel<IO, U, 2, NTL, NTS><<<grid, 256, 0, stream>>>(p, scale, grads);
-    else  // (1 KiB rows resident in the Infinity Cache, configs[1]: staged, 4 rows per wave, 40.2 against 47.6 us)
-        grad_staged_kernel<IO, U, RD, NTL, NTS><<<grid, 256, 0, stream>>>(p, scale, grads);
+    if constexpr (!kVariants) {  // the product library: the tuned default (grad_variant 5) only
+        if constexpr (U == 1 && NTL)
+            grad_kernel<IO, U, 2, NTL, NTS><<<grid, 256, 0, stream>>>(p, scale, grads);
+        else
+            grad_staged_kernel<IO, U, RD, NTL, NTS><<<grid, 256, 0, stream>>>(p, scale, grads);
+    } else {
+        const int variant = tuning().grad_variant;
+        if (variant == 3 && p.pad_S1 == 0)
+            grad_rows_kernel<IO, U, NTL, NTS><<<grid, 256, 0, stream>>>(p, scale, grads);
+        else if (variant == 0)
+            grad_kernel<IO, U, RD, NTL, NTS><<<grid, 256, 0, stream>>>(p, scale, grads);
+        else if (variant == 2 || (variant == 5 && U == 1 && NTL))
+            // 1 KiB rows streamed from HBM: per-row coefficients, 2 rows per wave (configs[1] shape with nontemporal
+            // loads: 50.0 us against 56.3 for 4 rows and 60.2 staged, profiles/r02/kbench/grad_short_rows_c2*.json)
+            grad_kernel<IO, U, 2, NTL, NTS><<<grid, 256, 0, stream>>>(p, scale, grads);
+        else if (variant == 6)
+            grad_staged_kernel<IO, U, 2, NTL, NTS><<<grid, 256, 0, stream>>>(p, scale, grads);
+        else  // (1 KiB rows resident in the Infinity Cache, configs[1]: staged, 4 rows per wave, 40.2 against 47.6 us)
+            grad_staged_kernel<IO, U, RD, NTL, NTS><<<grid, 256, 0, stream>>>(p, scale, grads);
+    }
 }
 
 // U = 16-byte vectors per lane per chunk: 4 KiB chunks for rows of >= 192 vectors, 2 KiB for >= 96, else 1 KiB

@@ -57,6 +57,13 @@ struct DevProblem {
     DynWords *dyn;              // device-resident lengths: num_cols / num_rows / col_mul above are host bounds and
                                 // the kernels take the real values from here (resolve_dyn); nullptr otherwise
     int steal;                  // log-softmax: columns past the grid handed out by dyn->steal (work stealing)
+    // device-resident lengths planned inside the log-softmax launch itself (dyn_fused; B <= 64, no alignment):
+    // every wave validates the lengths and locates its columns from registers, and the launch publishes the
+    // lattice offsets, the column map and the DynWords for the later kernels -- no separate setup kernel
+    int dyn_fused;
+    int64_t s_cap, t_cap, s1_cap;  // validation limits (S_b <= s_cap; T_b <= t_cap, S_b + 1 <= s1_cap when > 0)
+    int64_t scatter_above;         // publish a scattered-order multiplier when there are more columns than this
+    int *status_host;              // device address of the caller's host-mapped status word, or nullptr
 };
 
 // Fused joint network (mrnnt_joint.hip): logits z(b,t,s,:) = W * tanh(enc[b,t,:] + pred[b,s,:]) + bias are
@@ -118,10 +125,21 @@ struct Tuning {
                                   // per frame + lane offsets, bound-ctrl DPP shifts, no band mask); 0 -> masked step
     int col_scatter = 2;          // visit columns in a scattered order (DevProblem::col_mul): bit 0 log-softmax,
                                   // bit 1 gradient
+    int dyn_fused = 1;            // device-resident lengths, B <= 64, no alignment: plan inside the log-softmax launch
+                                  // (0: a separate setup kernel)
     int col_xcd = 0;              // XCD-chunked column order (visit_col, col_mul < 0; overrides col_scatter): bit 0
                                   // log-softmax, bit 1 gradient
 };
 Tuning &tuning();
+
+// The launch variants the knobs above select besides the tuned defaults are compiled into the development build
+// only (libmonotonic_rnnt_amd_dev.so, -DMRNNT_DEVTOOLS, where mrnnt_tune can reach them); the product library,
+// whose knobs never change, carries the default kernels alone.
+#ifdef MRNNT_DEVTOOLS
+constexpr bool kVariants = true;
+#else
+constexpr bool kVariants = false;
+#endif
 
 // Acts tensors up to this size stay in the 256 MiB Infinity Cache between the log-softmax pass and the gradient
 // pass's re-read when both load them with the default policy (MI355X_MICROARCH.md, Infinity Cache residency:
@@ -153,7 +171,8 @@ struct DynSetupArgs {
     int64_t S_cap;      // S_b <= S_cap (the label row stride)
     int64_t T_cap;      // T_b <= T_cap (alignment row stride / pad_T), 0 = unbounded
     int64_t S1_cap;     // S_b + 1 <= S1_cap (pad_S1), 0 = unbounded
-    int scatter;        // publish a scattered column-order multiplier
+    int64_t scatter_above;  // publish a scattered column-order multiplier when there are more columns than this
+                            // (the gradient's grid); INT64_MAX: never
     int64_t *row_off;
     int64_t *col_off;
     int *col_b;

@@ -695,8 +695,10 @@ template <int KS>
 static hipError_t launch_kh(const DevProblem &p, const JointArgs &j, bool bwd, hipStream_t stream) {
     const size_t bias = sizeof(float) * ((p.V + 31) / 32 * 32);
     const size_t tile = sizeof(unsigned short) * WTile<KS>::ELEMS;
-    if (tuning().joint_nbuf >= 3 && 3 * tile + bias <= 160 * 1024)
-        return launch_knw<KS, 3, 8>(p, j, bwd, 3 * tile + bias, stream);
+    if constexpr (kVariants) {  // three DMA buffers: development build only (joint_nbuf = 3)
+        if (tuning().joint_nbuf >= 3 && 3 * tile + bias <= 160 * 1024)
+            return launch_knw<KS, 3, 8>(p, j, bwd, 3 * tile + bias, stream);
+    }
     if (2 * tile + bias <= 160 * 1024) return launch_knw<KS, 2, 8>(p, j, bwd, 2 * tile + bias, stream);
     return hipErrorInvalidValue;
 }

@@ -475,21 +475,28 @@ __global__ __launch_bounds__(64 * NW) void recursion_halo_kernel(DevProblem p, i
 template <int NW, int HL = 8>
 static void launch_halo(const DevProblem &p, int with_beta, float *costs, hipStream_t stream) {
     const int blocks = with_beta ? 2 * p.B : p.B;
-    if (tuning().dp_lean && tuning().dp_halo == 2 && !p.min_s) {  // unrestricted: the lean step
-        recursion_halo_kernel<16, NW, HL, false, 1><<<blocks, 64 * NW, 0, stream>>>(p, with_beta, costs);
-        return;
-    }
-    if (tuning().dp_halo == 2) {  // 16-step prefetch blocks
+    if constexpr (!kVariants) {  // the product library: 16-step prefetch blocks, the lean step when unrestricted
         if (p.min_s)
             recursion_halo_kernel<16, NW, HL, true><<<blocks, 64 * NW, 0, stream>>>(p, with_beta, costs);
         else
-            recursion_halo_kernel<16, NW, HL, false><<<blocks, 64 * NW, 0, stream>>>(p, with_beta, costs);
-        return;
+            recursion_halo_kernel<16, NW, HL, false, 1><<<blocks, 64 * NW, 0, stream>>>(p, with_beta, costs);
+    } else {
+        if (tuning().dp_lean && tuning().dp_halo == 2 && !p.min_s) {  // unrestricted: the lean step
+            recursion_halo_kernel<16, NW, HL, false, 1><<<blocks, 64 * NW, 0, stream>>>(p, with_beta, costs);
+            return;
+        }
+        if (tuning().dp_halo == 2) {  // 16-step prefetch blocks
+            if (p.min_s)
+                recursion_halo_kernel<16, NW, HL, true><<<blocks, 64 * NW, 0, stream>>>(p, with_beta, costs);
+            else
+                recursion_halo_kernel<16, NW, HL, false><<<blocks, 64 * NW, 0, stream>>>(p, with_beta, costs);
+            return;
+        }
+        if (p.min_s)
+            recursion_halo_kernel<8, NW, HL, true><<<blocks, 64 * NW, 0, stream>>>(p, with_beta, costs);
+        else
+            recursion_halo_kernel<8, NW, HL, false><<<blocks, 64 * NW, 0, stream>>>(p, with_beta, costs);
     }
-    if (p.min_s)
-        recursion_halo_kernel<8, NW, HL, true><<<blocks, 64 * NW, 0, stream>>>(p, with_beta, costs);
-    else
-        recursion_halo_kernel<8, NW, HL, false><<<blocks, 64 * NW, 0, stream>>>(p, with_beta, costs);
 }
 
 template <int K, int NW>
@@ -523,10 +530,13 @@ hipError_t launch_dp(const DevProblem &p, int S_max, int with_beta, float *costs
         }
         return hipGetLastError();
     }
-    if (W <= 64) launch_k<1, 1>(p, with_beta, costs, stream);
-    else if (W <= 128) launch_k<1, 2>(p, with_beta, costs, stream);
-    else if (W <= 256) launch_k<1, 4>(p, with_beta, costs, stream);
-    else if (W <= 512) launch_k<1, 8>(p, with_beta, costs, stream);
+    if constexpr (kVariants) {  // dp_halo = 0 (development build): the per-step-barrier kernel for short rows too
+        if (W <= 64) launch_k<1, 1>(p, with_beta, costs, stream);
+        else if (W <= 128) launch_k<1, 2>(p, with_beta, costs, stream);
+        else if (W <= 256) launch_k<1, 4>(p, with_beta, costs, stream);
+        if (W <= 256) return hipGetLastError();
+    }
+    if (W <= 512) launch_k<1, 8>(p, with_beta, costs, stream);
     else if (W <= 1024) launch_k<2, 8>(p, with_beta, costs, stream);
     else if (W <= 1536) launch_k<3, 8>(p, with_beta, costs, stream);
     else if (W <= kMaxLabelsPlusOne) launch_k<4, 8>(p, with_beta, costs, stream);

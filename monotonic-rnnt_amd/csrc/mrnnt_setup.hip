@@ -159,17 +159,27 @@ __device__ __forceinline__ bool dyn_len_ok(const DynSetupArgs &a, int T, int S) 
            (a.S1_cap == 0 || (int64_t)S + 1 <= a.S1_cap);
 }
 
-__device__ __forceinline__ int64_t block_sum64(int64_t v, int64_t *red) {  // 256 threads, every thread gets the sum
+// Block sums of (rows, columns, invalid count) in one LDS round (256 threads; every thread gets the sums)
+__device__ __forceinline__ void block_sum3(int64_t &r, int64_t &c, int64_t &bad, int64_t (*red)[4]) {
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
-    __syncthreads();  // red is reused by consecutive sums
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    for (int off = 32; off >= 1; off >>= 1) {
+        r += __shfl_xor(r, off);
+        c += __shfl_xor(c, off);
+        bad += __shfl_xor(bad, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = r;
+        red[1][threadIdx.x >> 6] = c;
+        red[2][threadIdx.x >> 6] = bad;
+    }
     __syncthreads();
-    return red[0] + red[1] + red[2] + red[3];
+    r = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    c = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+    bad = red[2][0] + red[2][1] + red[2][2] + red[2][3];
 }
 
 __global__ __launch_bounds__(256) void setup_dyn_kernel(DynSetupArgs a) {
-    __shared__ int64_t red[4];
+    __shared__ int64_t red[3][4];
     const int b = blockIdx.x;
     const bool last = b == a.B - 1;
     int64_t r = 0, c = 0, bad = 0;
@@ -183,9 +193,7 @@ __global__ __launch_bounds__(256) void setup_dyn_kernel(DynSetupArgs a) {
             c += T;
         }
     }
-    r = block_sum64(r, red);
-    c = block_sum64(c, red);
-    if (last) bad = block_sum64(bad, red);
+    block_sum3(r, c, bad, red);
     const int T = a.T[b], S = a.S[b];
     const bool ok = dyn_len_ok(a, T, S);
     const int64_t rb = ok ? (int64_t)T * (S + 1) : 0, cb = ok ? T : 0;
@@ -202,10 +210,11 @@ __global__ __launch_bounds__(256) void setup_dyn_kernel(DynSetupArgs a) {
     if (!last) return;
     const int64_t R = r + rb, C = c + cb;
     const bool fail = bad != 0 || (a.packed ? R != a.rows : R > a.rows) || C > a.cols_cap;
-    // scattered column order (the gradient's visit_col): the first multiplier >= 0.618 C coprime with C, 64
-    // candidates per pass with lane-parallel Euclid (any coprime multiplier makes i -> i * m mod C a permutation)
+    // scattered column order (visit_col), only where a streaming grid walks more than one column per workgroup: the
+    // first multiplier >= 0.618 C coprime with C, 64 candidates per pass with lane-parallel Euclid (any coprime
+    // multiplier makes i -> i * m mod C a permutation)
     int64_t mul = 0;
-    if (!fail && a.scatter && C >= 3 && C < (1ll << 31) && threadIdx.x < 64) {
+    if (!fail && C > a.scatter_above && C >= 3 && C < (1ll << 31) && threadIdx.x < 64) {
         for (uint32_t base = max(2u, (uint32_t)(0.6180339887 * (double)C));; base += 64) {
             uint32_t x = base + threadIdx.x, y = (uint32_t)C;
             while (y) {

@@ -55,11 +55,10 @@ __global__ __launch_bounds__(256) void softmax_kernel(DevProblem p) {
     const int bj = blank / E, bc = blank % E, blane = bj & 63;
     const Vec ninf = splat<IO>(NEG_INF_F);
 
-    walk_columns(p, [&](int64_t c) {
-        const int b = p.col_b[c];
-        const int T = p.T[b], S = p.S[b];
-        const int t = (int)(c - p.col_off[b]);
-        const int64_t rowc = p.row_off[b] + (int64_t)t * (S + 1);
+    walk_columns(p, [&](const ColRef &k) {
+        const int64_t c = k.c;
+        const int b = k.b, T = k.T, S = k.S, t = k.t;
+        const int64_t rowc = k.rowc;
         const int64_t arow = acts_col_base(p, b, t, rowc);
         int lo = max(0, t - (T - S)), hi = min(t, S);
         align_window(p, c, t, lo, hi);
@@ -162,12 +161,10 @@ __global__ __launch_bounds__(256) void softmax_lean_kernel(DevProblem p) {
     const int blank = p.blank;
     const Vec ninf = splat<IO>(NEG_INF_F);
 
-    walk_columns(p, [&](int64_t ci) {
-        const int64_t c = visit_col(p, ci);
-        const int b = p.col_b[c];
-        const int T = p.T[b], S = p.S[b];
-        const int t = (int)(c - p.col_off[b]);
-        const int64_t rowc = p.row_off[b] + (int64_t)t * (S + 1);
+    walk_columns(p, [&](const ColRef &k) {
+        const int64_t c = k.c;
+        const int b = k.b, T = k.T, S = k.S, t = k.t;
+        const int64_t rowc = k.rowc;
         const int64_t arow = acts_col_base(p, b, t, rowc);
         int lo = max(0, t - (T - S)), hi = min(t, S);
         align_window(p, c, t, lo, hi);
@@ -357,12 +354,10 @@ __global__ __launch_bounds__(256) void softmax_row16_kernel(DevProblem p) {
     const int blank = p.blank;
     const Vec ninf = splat<IO>(NEG_INF_F);
 
-    walk_columns(p, [&](int64_t ci) {
-        const int64_t c = visit_col(p, ci);
-        const int b = p.col_b[c];
-        const int T = p.T[b], S = p.S[b];
-        const int t = (int)(c - p.col_off[b]);
-        const int64_t rowc = p.row_off[b] + (int64_t)t * (S + 1);
+    walk_columns(p, [&](const ColRef &k) {
+        const int64_t c = k.c;
+        const int b = k.b, T = k.T, S = k.S, t = k.t;
+        const int64_t rowc = k.rowc;
         const int64_t arow = acts_col_base(p, b, t, rowc);
         int lo = max(0, t - (T - S)), hi = min(t, S);
         align_window(p, c, t, lo, hi);
@@ -443,11 +438,10 @@ __global__ __launch_bounds__(256) void softmax_scalar_kernel(DevProblem p) {
     const int V = p.V;
     const int blank = p.blank;
     const Sc *__restrict__ acts = reinterpret_cast<const Sc *>(p.acts);
-    walk_columns(p, [&](int64_t c) {
-        const int b = p.col_b[c];
-        const int T = p.T[b], S = p.S[b];
-        const int t = (int)(c - p.col_off[b]);
-        const int64_t rowc = p.row_off[b] + (int64_t)t * (S + 1);
+    walk_columns(p, [&](const ColRef &k) {
+        const int64_t c = k.c;
+        const int b = k.b, T = k.T, S = k.S, t = k.t;
+        const int64_t rowc = k.rowc;
         const int64_t arow = acts_col_base(p, b, t, rowc);
         int lo = max(0, t - (T - S)), hi = min(t, S);
         align_window(p, c, t, lo, hi);
@@ -486,34 +480,48 @@ __global__ __launch_bounds__(256) void softmax_scalar_kernel(DevProblem p) {
 template <class IO, bool NTL, int U>
 static void launch_u(const DevProblem &p, int grid, hipStream_t stream) {
     const int VL = p.V / IO::E;
-    const int v = tuning().softmax_variant;
     const bool full = VL % (64 * U) == 0;
-    if (v == 0 || v == 2) {  // first kernel (shuffle butterflies), 1 or 2 rows per wave
-        if (v == 0) softmax_kernel<IO, U, 1, NTL><<<grid, 256, 0, stream>>>(p);
-        else softmax_kernel<IO, U, 2, NTL><<<grid, 256, 0, stream>>>(p);
-        return;
+    constexpr int RD = U == 1 ? 4 : 2;  // rows per wave of the default (softmax_variant 13)
+    if constexpr (!kVariants) {  // the product library: the tuned default only
+        if (VL <= 64)
+            softmax_row16_kernel<IO, 1, NTL><<<grid, 256, 0, stream>>>(p);
+        else if (VL <= 64 * U && full)
+            softmax_lean_kernel<IO, U, RD, NTL, true, true><<<grid, 256, 0, stream>>>(p);
+        else if (VL <= 64 * U)
+            softmax_lean_kernel<IO, U, RD, NTL, false, true><<<grid, 256, 0, stream>>>(p);
+        else if (full)
+            softmax_lean_kernel<IO, U, RD, NTL, true><<<grid, 256, 0, stream>>>(p);
+        else
+            softmax_lean_kernel<IO, U, RD, NTL, false><<<grid, 256, 0, stream>>>(p);
+    } else {
+        const int v = tuning().softmax_variant;
+        if (v == 0 || v == 2) {  // first kernel (shuffle butterflies), 1 or 2 rows per wave
+            if (v == 0) softmax_kernel<IO, U, 1, NTL><<<grid, 256, 0, stream>>>(p);
+            else softmax_kernel<IO, U, 2, NTL><<<grid, 256, 0, stream>>>(p);
+            return;
+        }
+        if ((v == 13 || v == 22 || v == 23) && VL <= 64) {  // 16-lane rows (the default), 1 / 2 rows per group per pass
+            if (v != 23) softmax_row16_kernel<IO, 1, NTL><<<grid, 256, 0, stream>>>(p);
+            else softmax_row16_kernel<IO, 2, NTL><<<grid, 256, 0, stream>>>(p);
+            return;
+        }
+        if ((v == 13 || v == 21) && VL <= 64 * U) {  // single-chunk rows (the default): wave max first, 4 / 2 rows per wave
+            constexpr int RO = U == 1 ? 4 : 2;
+            if (full) softmax_lean_kernel<IO, U, RO, NTL, true, true><<<grid, 256, 0, stream>>>(p);
+            else softmax_lean_kernel<IO, U, RO, NTL, false, true><<<grid, 256, 0, stream>>>(p);
+            return;
+        }
+        // running-max lean kernel: 13 (rows of several chunks) / 16 (any row) -> 2 rows per wave (4 for rows of < 96
+        // vectors), 14 -> 1, 15 -> 4
+        const int R = v == 14 ? 1 : (v == 15 || ((v == 13 || v == 16) && U == 1)) ? 4 : 2;
+    #define MRNNT_LEAN(RR)                                                                              \
+        (full ? softmax_lean_kernel<IO, U, RR, NTL, true><<<grid, 256, 0, stream>>>(p)                 \
+              : softmax_lean_kernel<IO, U, RR, NTL, false><<<grid, 256, 0, stream>>>(p))
+        if (R == 1) MRNNT_LEAN(1);
+        else if (R == 4) MRNNT_LEAN(4);
+        else MRNNT_LEAN(2);
+    #undef MRNNT_LEAN
     }
-    if ((v == 13 || v == 22 || v == 23) && VL <= 64) {  // 16-lane rows (the default), 1 / 2 rows per group per pass
-        if (v != 23) softmax_row16_kernel<IO, 1, NTL><<<grid, 256, 0, stream>>>(p);
-        else softmax_row16_kernel<IO, 2, NTL><<<grid, 256, 0, stream>>>(p);
-        return;
-    }
-    if ((v == 13 || v == 21) && VL <= 64 * U) {  // single-chunk rows (the default): wave max first, 4 / 2 rows per wave
-        constexpr int RO = U == 1 ? 4 : 2;
-        if (full) softmax_lean_kernel<IO, U, RO, NTL, true, true><<<grid, 256, 0, stream>>>(p);
-        else softmax_lean_kernel<IO, U, RO, NTL, false, true><<<grid, 256, 0, stream>>>(p);
-        return;
-    }
-    // running-max lean kernel: 13 (rows of several chunks) / 16 (any row) -> 2 rows per wave (4 for rows of < 96
-    // vectors), 14 -> 1, 15 -> 4
-    const int R = v == 14 ? 1 : (v == 15 || ((v == 13 || v == 16) && U == 1)) ? 4 : 2;
-#define MRNNT_LEAN(RR)                                                                              \
-    (full ? softmax_lean_kernel<IO, U, RR, NTL, true><<<grid, 256, 0, stream>>>(p)                 \
-          : softmax_lean_kernel<IO, U, RR, NTL, false><<<grid, 256, 0, stream>>>(p))
-    if (R == 1) MRNNT_LEAN(1);
-    else if (R == 4) MRNNT_LEAN(4);
-    else MRNNT_LEAN(2);
-#undef MRNNT_LEAN
 }
 
 // U = 16-byte loads per lane per chunk: a 4 KiB chunk for rows of >= 192 vectors, 2 KiB for >= 96, else 1 KiB

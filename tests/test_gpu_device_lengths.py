@@ -18,7 +18,7 @@ import pytest
 import torch
 
 import oracle as O
-from _parity import FIXTURES, assert_costs, assert_grads, random_problem
+from _parity import FIXTURES, assert_costs, assert_grads, knobs, random_problem
 
 pytestmark = pytest.mark.gpu
 
@@ -68,13 +68,25 @@ CASES = {
     "bf16_v512": (5, 4, (20, 70), 25, 512, torch.bfloat16, "packed", False),
     "padded_v64": (6, 5, (10, 40), 12, 64, torch.float32, "padded", False),
     "aligned_k2": (7, 5, (30, 100), 20, 96, torch.float32, "packed", True),
-    "steal_many_columns": (8, 8, (600, 800), 6, 16, torch.float32, "packed", False),
+    "many_columns_b8": (8, 8, (600, 800), 6, 16, torch.float32, "packed", False),
+    "steal_b80": (10, 80, (60, 90), 5, 16, torch.float32, "packed", False),  # > 64 utterances: setup kernel + stealing
     "long_labels_halo": (9, 2, (300, 320), 250, 8, torch.float32, "packed", False),
 }
 
 
+@pytest.mark.parametrize("separate_setup", [False, True], ids=["default", "setup_kernel"])
 @pytest.mark.parametrize("name", list(CASES))
-def test_device_lengths_bit_identical_to_host_lengths(op, dev, name):
+def test_device_lengths_bit_identical_to_host_lengths(op, dev, name, separate_setup):
+    """default: batches of <= 64 utterances without an alignment plan inside the log-softmax launch; setup_kernel
+    (development build, dyn_fused = 0): the separate setup kernel for every case."""
+    if separate_setup:
+        with knobs(dyn_fused=0):
+            _bit_identical(op, dev, name)
+    else:
+        _bit_identical(op, dev, name)
+
+
+def _bit_identical(op, dev, name):
     seed, B, Tr, Smax, V, dt, layout, aligned = CASES[name]
     rng = np.random.default_rng(seed)
     acts, labels, T, S = random_problem(rng, B, Tr, Smax, V)
@@ -179,6 +191,9 @@ def _bad_cases():
         "S_negative": (4, 2, [4], [-1], None, None),
         "padded_T_above_pad": (0, 2, [5, 2], [1, 1], (4, 3), None),
         "alignment_narrower_than_T": (12, 2, [4], [2], None, 3),
+        "b70_one_bad": (70 * 8, 2, [4] * 69 + [1], [1] * 69 + [2], None, None),
+        "huge_T": (12, 2, [1 << 30], [2], None, None),
+        "huge_T_b70": (70 * 8, 2, [4] * 69 + [1 << 30], [1] * 70, None, None),
     }
 
 
@@ -231,3 +246,22 @@ def test_pybind_names_with_device_lengths(op, dev, path):
     assert rc == 0
     assert_costs(costs.numpy().astype(np.float64), fx["costs_f64"])
     assert_grads(grads.cpu().numpy(), fx["grads_f64"])
+
+
+@pytest.mark.parametrize("B", [16, 70])
+def test_device_lengths_launch_count(op, dev, B):
+    """A batch of <= 64 utterances plans its lengths inside the log-softmax launch (no setup kernel at all); a larger
+    one runs exactly one setup kernel per forward -- never the host-lengths setup kernels."""
+    import _mrnnt_lib as L
+    rng = np.random.default_rng(B)
+    acts, labels, T, S = random_problem(rng, B, (5, 12), 4, 16)
+    a = _t(acts, dev).requires_grad_(True)
+    L.profile_enable(True)
+    try:
+        op.monotonic_rnnt_loss(a, _t(labels, dev), _t(T, dev), _t(S, dev)).sum().backward()
+        torch.cuda.synchronize()
+        prof = L.profile_read()
+    finally:
+        L.profile_enable(False)
+    assert prof["setup"][1] == (0 if B <= 64 else 1), prof
+    assert prof["log_softmax"][1] == 1 and prof["alpha_beta"][1] == 1 and prof["grad"][1] == 1

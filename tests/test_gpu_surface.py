@@ -58,26 +58,29 @@ def test_golden_denominators_alpha_beta(op, dev, path):
 
 
 @pytest.mark.parametrize("bad", [3, 7, -5, 1 << 30])
-def test_device_label_out_of_range_is_nan_not_a_fault(op, dev, bad):
-    """A device label outside [0, V) is not read back (no sync); the kernels read no logit with it (its label
-    log-prob is NaN, so the transitions through it carry no probability) and that utterance's cost and gradient
-    are not finite (+inf / NaN), the other utterances are exact (no access past the row)."""
+def test_device_label_out_of_range_gives_inf_cost_nan_grads(op, dev, bad):
+    """A device label outside [0, V) is not read back (no sync) and never used as an index: its log-softmax pick is
+    NaN, and the recursion's LSE turns a NaN transition into no probability (fmax drops the NaN; both directions
+    stay -inf past that label position, which every path of the utterance crosses). So, pinned exactly, whatever
+    the bad value: that utterance's cost is +inf and every element of its gradient NaN (exp(... - ll), ll = -inf,
+    as the reference's cpu_rnnt.h forms it); the other utterances are exact (no access past a row)."""
     rng = np.random.default_rng(abs(bad) % 97)
     acts, labels, T, S = random_problem(rng, 3, (6, 14), 4, 3, force={0: (10, 3), 1: (9, 2), 2: (12, 4)})
     labels = np.where(labels >= 3, 1, labels).astype(np.int32)
-    lab_bad = labels.copy()
-    lab_bad[1, 1] = bad
-    a = _t(acts, dev).requires_grad_(True)
-    costs = op.monotonic_rnnt_loss(a, _t(lab_bad, dev), _t(T, dev), _t(S, dev))
-    costs.sum().backward()
-    torch.cuda.synchronize()
-    c, g = costs.detach().cpu().numpy().astype(np.float64), a.grad.cpu().numpy()
-    assert not np.isfinite(c[1]) and np.isfinite(c[[0, 2]]).all()
     cr, gr = O.oracle_rnnt(acts, labels, T, S)
     r0, r1 = T[0] * (S[0] + 1), T[0] * (S[0] + 1) + T[1] * (S[1] + 1)
-    assert_costs(c[[0, 2]], cr[[0, 2]])
-    assert_grads(np.concatenate([g[:r0], g[r1:]]), np.concatenate([gr[:r0], gr[r1:]]))
-    assert not np.isfinite(g[r0:r1]).all()
+    for pos in range(S[1]):  # the bad label at every position of utterance 1
+        lab_bad = labels.copy()
+        lab_bad[1, pos] = bad
+        a = _t(acts, dev).requires_grad_(True)
+        costs = op.monotonic_rnnt_loss(a, _t(lab_bad, dev), _t(T, dev), _t(S, dev))
+        costs.sum().backward()
+        torch.cuda.synchronize()
+        c, g = costs.detach().cpu().numpy().astype(np.float64), a.grad.cpu().numpy()
+        assert np.isposinf(c[1]) and np.isfinite(c[[0, 2]]).all(), (pos, c)
+        assert np.isnan(g[r0:r1]).all(), pos
+        assert_costs(c[[0, 2]], cr[[0, 2]])
+        assert_grads(np.concatenate([g[:r0], g[r1:]]), np.concatenate([gr[:r0], gr[r1:]]))
 
 
 def test_host_labels_and_strides_validated(op, dev):
@@ -377,6 +380,24 @@ def test_bench_graph_mode_matches_eager():
     assert graph["config"]["execution"] == "hip_graph_replay" and eager["config"]["execution"] == "eager"
     assert abs(graph["loss_check"] - eager["loss_check"]) <= 1e-6 * abs(eager["loss_check"])
     assert graph["kernels"]["grad"]["avg_ms"] > 0 and graph["ms_per_step"] > 0
+
+
+def test_bench_eight_rank_rehearsal():
+    """`bench.py --gpus 8` rehearsed with 8 gloo ranks sharing this GPU: configs[1]
+    weak-scaled (8 x 16 utterances) and configs[3] strong-scaled in in-place chunks under a small HBM budget, whose
+    all-reduced loss equals the one-rank run over the same 512 utterances. Every rank reports its device."""
+    c2 = _bench(["--gpus", "8", "--dist-backend", "gloo", "--config", "c2", "--steps", "2", "--warmup", "1",
+                 "--no-cpu"], 400)
+    assert c2["n_gpus"] == 8 and c2["config"]["global_batch"] == 128 and c2["scaling"] == "weak"
+    assert sorted(d["rank"] for d in c2["config"]["rank_devices"]) == list(range(8))
+    assert {d["local_rank"] for d in c2["config"]["rank_devices"]} == set(range(8))
+    one = _bench(["--config", "ragged", "--steps", "1", "--warmup", "0", "--no-cpu", "--hbm-budget-gb", "30"], 400)
+    eight = _bench(["--gpus", "8", "--dist-backend", "gloo", "--config", "ragged", "--steps", "1", "--warmup", "0",
+                    "--no-cpu", "--hbm-budget-gb", "8"], 600)
+    assert eight["n_gpus"] == 8 and eight["scaling"] == "strong"
+    assert eight["config"]["global_batch"] == one["config"]["global_batch"] == 512
+    assert eight["config"]["memory_mode"] == "inplace"
+    assert abs(one["loss_check"] - eight["loss_check"]) <= 1e-6 * abs(one["loss_check"])
 
 
 def test_bench_ragged_sharded_two_ranks_equals_one():
