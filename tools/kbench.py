@@ -42,6 +42,9 @@ def main():
     ap.add_argument("--buffers", type=int, default=1,
                     help="allocate this many acts and grads buffers (variant knobs acts_buf / grads_buf pick one): "
                          "does the gradient kernel's speed depend on where a buffer sits?")
+    ap.add_argument("--acts-buffers", type=int, default=0,
+                    help="allocate this many acts buffers but one grads buffer (variant knob acts_buf picks one): the "
+                         "log-softmax read side over several physical placements in one process")
     ap.add_argument("--acts-dtype", default="f32", choices=["f32", "bf16", "f16"],
                     help="element type of acts / grads (the kernels' IoBF16 / IoF16 paths)")
     ap.add_argument("--ws-first", action="store_true",
@@ -106,6 +109,8 @@ def main():
     for _ in range(args.buffers - 1):
         acts_list.append(acts.clone())
         grads_list.append(torch.empty(rows * V, dtype=tdt, device=dev))
+    for _ in range(max(0, args.acts_buffers - len(acts_list))):
+        acts_list.append(acts.clone())
     out_alloc = {"acts": acts.data_ptr(), "grads": grads_store.data_ptr(), "ws": ws.data_ptr()}
 
     def run_once():
