@@ -62,6 +62,7 @@ struct Plan {
     int64_t pad_T = 0, pad_S1 = 0;
     bool align = false;
     bool dyn = false;
+    size_t off_flags = 0, flags_bytes = 0;  // the chase launch's ready flags (host lengths: 2 words per column)
     size_t off_row, off_col, off_colb, off_mtmp, off_min, off_max, off_den, off_lpb, off_lpe, off_alpha, off_beta, off_ll,
         off_llb, off_dyn, total;
 };
@@ -161,6 +162,13 @@ RNNTStatus make_plan(const mrnnt_problem *p, Plan *pl) {
         o = align_up(o + bytes);
         return at;
     };
+    // first: the chase launch's flags (mrnnt_chase.hip), a block of its own starting at the workspace's start and
+    // padded to 16 bytes -- the memset that clears them every call is cheapest so (cdna_hip_programming.md
+    // Guideline 16, Re-initialise every call)
+    if (!q.dyn) {
+        q.flags_bytes = (sizeof(unsigned) * 2 * (size_t)q.cols + 15) / 16 * 16;
+        q.off_flags = take(q.flags_bytes);
+    }
     q.off_row = take(sizeof(int64_t) * (q.B + 1));
     q.off_col = take(sizeof(int64_t) * (q.B + 1));
     q.off_colb = take(sizeof(int) * q.cols);
@@ -459,6 +467,22 @@ RNNTStatus mrnnt_forward(const mrnnt_problem *p, void *ws, size_t ws_bytes, floa
                                 reinterpret_cast<int *>(w + pl.off_max), stream);
         });
         if (e != hipSuccess) return fail_hip(e, "alignment band kernels");
+    }
+    // host lengths, no alignment: the forward as one launch, the recursion chasing the log-softmax (mrnnt_chase.hip),
+    // where it has a body for these rows
+    if (!pl.dyn && !pl.align && tuning().chase && chase_body(d, pl.elem) >= 0 && pl.S_max + 1 <= 4 * 56 &&
+        chase_grid(d, pl.T_max, with_beta ? 1 : 0) <= ((int64_t)1 << 22)) {
+        ChaseArgs ca;
+        ca.flags = reinterpret_cast<unsigned *>(w + pl.off_flags);
+        ca.cols = pl.cols;
+        // the ready flags are zeroed before every launch (a memset node under graph capture): a launch's producers
+        // store 1, its consumers wait for 1
+        if ((e = hipMemsetAsync(ca.flags, 0, pl.flags_bytes, stream)) != hipSuccess) return fail_hip(e, "flag reset");
+        e = timed(K_CHASE, stream, [&] {
+            return launch_chase(d, ca, pl.elem, pl.S_max, pl.T_max, with_beta ? 1 : 0, costs_dev, stream);
+        });
+        if (e != hipSuccess) return fail_hip(e, "chase kernel");
+        return RNNT_STATUS_SUCCESS;
     }
     int grid = streaming_grid(pl.cols, tuning().softmax_grid_per_cu);
     DevProblem ds = d;  // the log-softmax launch's view
@@ -928,6 +952,8 @@ __attribute__((visibility("default"))) int mrnnt_tune(const char *key, int value
     }
     else if (!std::strcmp(key, "nt_store")) slot = &t.nt_store;
     else if (!std::strcmp(key, "dyn_fused")) slot = &t.dyn_fused;
+    else if (!std::strcmp(key, "chase")) slot = &t.chase;
+    else if (!std::strcmp(key, "chase_depth")) slot = &t.chase_depth;
     else if (!std::strcmp(key, "nt_load")) slot = &t.nt_load;
     else if (!std::strcmp(key, "occ_skip")) slot = &t.occ_skip;
     else if (!std::strcmp(key, "joint_nbuf")) slot = &t.joint_nbuf;

@@ -491,6 +491,32 @@ __device__ __forceinline__ void vstore(V *ptr, const V &v) {
         *ptr = v;
 }
 
+// ---- in-launch hand-off words (the chase launch, mrnnt_chase.hip; cdna_hip_programming.md Guideline 16, R1) ----
+// 4- / 8-byte accesses through the GLOBAL address space at agent scope: relaxed atomic stores are write-through
+// (`sc1`) and relaxed atomic loads read past this CU's L1 and this XCD's L2 (`sc1`), so a payload stored this way,
+// drained (s_waitcnt vmcnt(0)) before a flag store of the same kind, is seen by a consumer on any XCD that loads it
+// this way after seeing the flag -- no release / acquire fence.
+template <int N> struct WordOf;
+template <> struct WordOf<4> { typedef unsigned T; };
+template <> struct WordOf<8> { typedef unsigned long long T; };
+
+template <class T>
+__device__ __forceinline__ void store_wt(T *ptr, T v) {
+    typedef typename WordOf<sizeof(T)>::T W;
+    __hip_atomic_store((__attribute__((address_space(1))) W *)ptr, __builtin_bit_cast(W, v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <class T>
+__device__ __forceinline__ T load_wt(const T *ptr) {
+    typedef typename WordOf<sizeof(T)>::T W;
+    return __builtin_bit_cast(
+        T, __hip_atomic_load((__attribute__((address_space(1))) W *)ptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// every store this wave issued has completed (the drain before a hand-off flag)
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 template <class IO>
 __device__ __forceinline__ typename IO::V splat(float f) {
     float x[IO::E];

@@ -127,6 +127,9 @@ struct Tuning {
                                   // bit 1 gradient
     int dyn_fused = 1;            // device-resident lengths, B <= 64, no alignment: plan inside the log-softmax launch
                                   // (0: a separate setup kernel)
+    int chase = 1;                // forward as one launch, the recursion chasing the log-softmax (mrnnt_chase.hip) where
+                                  // it applies (host lengths, no alignment, f32 rows of <= 256 vectors, S + 1 <= 224)
+    int chase_depth = 16;         // lp rows the chase recursion prefetches (16; 8 in the development build)
     int col_xcd = 0;              // XCD-chunked column order (visit_col, col_mul < 0; overrides col_scatter): bit 0
                                   // log-softmax, bit 1 gradient
 };
@@ -155,7 +158,7 @@ inline bool nt_acts_loads(const DevProblem &p, int elem_bytes) {
 
 // Kernel-family ids for the profiling counters (mrnnt_profile_read order).
 enum KernelId { K_BAND = 0, K_SOFTMAX = 1, K_DP = 2, K_GRAD = 3, K_SETUP = 4, K_JOINT_FWD = 5, K_JOINT_BWD = 6,
-                K_JOINT_RED = 7, K_COUNT = 8 };
+                K_JOINT_RED = 7, K_CHASE = 8, K_COUNT = 9 };
 
 // lpb / lpe (may be null): zero their 64 pad entries either side of [0, n)
 hipError_t launch_setup(const int *T, const int *S, int B, int64_t *row_off, int64_t *col_off, int *col_b,
@@ -192,6 +195,18 @@ hipError_t launch_softmax(const DevProblem &p, int elem, int grid, hipStream_t s
 // mrnnt_read_state: alpha / beta cells outside the compute band set to -inf (either may be null)
 hipError_t launch_mask_state(const DevProblem &p, double *alpha, double *beta, hipStream_t stream);
 hipError_t launch_dp(const DevProblem &p, int S_max, int with_beta, float *costs, hipStream_t stream);
+
+// The chase launch (mrnnt_chase.hip): log-softmax and alpha / beta recursion in one launch, the recursion consuming
+// columns as they are published. Ready flags: `cols` words for alpha, then `cols` for beta, zeroed before every launch.
+struct ChaseArgs {
+    unsigned *flags;
+    int64_t cols;  // the flag stride between the directions
+};
+// the log-softmax body the chase launch has for this problem, -1 for none (f32 rows of <= 256 vectors only)
+int chase_body(const DevProblem &p, int elem);
+int64_t chase_grid(const DevProblem &p, int T_max, int with_beta);
+hipError_t launch_chase(const DevProblem &p, const ChaseArgs &c, int elem, int S_max, int T_max, int with_beta,
+                        float *costs, hipStream_t stream);
 hipError_t launch_grad(const DevProblem &p, int elem, const float *scale, void *grads, int grid, hipStream_t stream);
 hipError_t launch_count_live(const DevProblem &p, unsigned long long *count, hipStream_t stream);
 hipError_t launch_pad_zero(const DevProblem &p, int elem, void *grads, hipStream_t stream);

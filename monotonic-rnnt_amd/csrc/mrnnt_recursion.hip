@@ -8,7 +8,7 @@
 //   beta(t, s)  = lse(beta(t+1, s) + lpb(t, s), beta(t+1, s+1) + lpe(t, s))
 // restricted to the band s <= t+1, S-s <= T-1-t (and the alignment band min_s/max_s when given).
 // State and LSE are fp64 (the reference's accumulation type, rnnt_helper.h:16-30).
-#include "mrnnt_device.h"
+#include "mrnnt_dp.h"
 
 namespace mrnnt {
 
@@ -18,31 +18,6 @@ namespace mrnnt {
 // one s_barrier per step. The lp arrays are finite on every row of [0, S] (the log-softmax kernels
 // zero-fill out-of-band rows), so a predecessor at -inf stays -inf without guards; the only
 // non-finite case left in the LSE is both inputs at -inf.
-
-__device__ __forceinline__ double dpp_shr1(double v) {  // lane i <- lane i-1 (lane 0 <- 0)
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x138, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x138, 0xf, 0xf, false);
-    return __hiloint2double(hi, lo);
-}
-
-__device__ __forceinline__ double dpp_shl1(double v) {  // lane i <- lane i+1 (lane 63 <- 0)
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x130, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x130, 0xf, 0xf, false);
-    return __hiloint2double(hi, lo);
-}
-
-// Shifts with bound_ctrl: the lane without a source reads 0 (no "old" operand to initialise).
-__device__ __forceinline__ double dpp_shr1_bc(double v) {
-    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x138, 0xf, 0xf, true);
-    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x138, 0xf, 0xf, true);
-    return __hiloint2double(hi, lo);
-}
-
-__device__ __forceinline__ double dpp_shl1_bc(double v) {
-    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x130, 0xf, 0xf, true);
-    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x130, 0xf, 0xf, true);
-    return __hiloint2double(hi, lo);
-}
 
 template <int K, int D, int NW, bool BAND>
 __device__ __forceinline__ void alpha_pass(const DevProblem &p, int b, float *__restrict__ costs, double (*xb)[8]) {
@@ -226,238 +201,6 @@ __global__ __launch_bounds__(64 * NW) void recursion_kernel(DevProblem p, int wi
         alpha_pass<K, D, NW, BAND>(p, b, costs, xb);
 }
 
-
-// Halo recursion (64 < S+1 <= 8 * (64 - HL)): NW waves, one cell per lane, and no per-step barrier. Wave w
-// owns C = 64 - HL consecutive cells and its remaining HL lanes recompute the HL cells next to them that the
-// neighbouring wave owns (alpha: the cells below, beta: the cells above). Those halo lanes lose one valid lane
-// per step (their outer neighbour is not in the wave), so the own cells stay exact for HL steps; then the
-// neighbour's HL boundary cells are copied in through LDS (one barrier per HL steps instead of one per step).
-template <int D, int NW, int HL, bool BAND, int LEAN>
-__device__ __forceinline__ void alpha_pass_halo(const DevProblem &p, int b, float *__restrict__ costs,
-                                                double (*xh)[8][HL > 0 ? HL : 1]) {
-    static_assert((HL == 0 ? NW == 1 : D % HL == 0) && NW <= 8,
-                  "halo refreshes at prefetch-block positions (HL = 0: one wave, no halo); xh sized for <= 8 waves");
-    constexpr int C = 64 - HL;
-    constexpr int HLD = HL > 0 ? HL : 1;  // divisor for the (compiled-out when HL == 0) refresh logic
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int T = p.T[b], S = p.S[b], W = S + 1;
-    const int64_t r0 = p.row_off[b], c0 = p.col_off[b];
-    const int s0 = wave * C - HL + lane;  // negative for the halo lanes of wave 0 (always out of band)
-    const bool own = lane >= HL && s0 < W;
-    // LEAN: every row access is a uniform row pointer (SGPRs) + an unsigned lane offset; the halo lanes of wave 0
-    // (s0 < 0, never in band) read cell 0
-    const unsigned sl = (unsigned)max(s0, 0);
-
-    double a = (s0 == 0) ? 0.0 : NEG_INF_D;
-    double pb[D], pe[D];
-    int mn[D], mx[D];
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-        const int tt = min(d, T - 1);
-        if (LEAN) {
-            pb[d] = (p.lpb + (r0 + (int64_t)tt * W))[sl];
-            pe[d] = (p.lpe + (r0 + (int64_t)tt * W - 1))[sl];
-        } else {
-            pb[d] = p.lpb[r0 + (int64_t)tt * W + s0];
-            pe[d] = p.lpe[r0 + (int64_t)tt * W + s0 - 1];
-        }
-        mn[d] = BAND ? p.min_s[c0 + tt] : 0;
-        mx[d] = BAND ? p.max_s[c0 + tt] : S;
-    }
-    double *ap = p.alpha + r0;                                           // alpha row of the next frame
-    const double *pbp = p.lpb + r0 + (int64_t)min(D, T - 1) * W;         // lp rows of the next prefetch
-    const double *pep = p.lpe + r0 + (int64_t)min(D, T - 1) * W - 1;
-    auto step_lean = [&](int t, int d) {
-        // unrestricted: no band mask -- a cell above the band only ever sees -inf predecessors (so it is -inf), a
-        // cell below it only feeds cells below it and is never read (mrnnt_read_state masks it for inspection);
-        // halo lanes are garbage between refreshes exactly as in the masked step (they only feed halo lanes)
-        double carry = dpp_shr1_bc(a);
-        if (HL == 0 && lane == 0) carry = NEG_INF_D;
-        const double v = lse2(a + pb[d], carry + pe[d]);
-        if (BAND) {
-            const int lo = max(max(t - (T - 1 - S), mn[d]), 0);
-            const int hi = min(min(t + 1, S), mx[d]);
-            a = (s0 >= lo && s0 <= hi) ? v : NEG_INF_D;
-        } else {
-            // the halo lanes of wave 0 stand for cells s < 0 and feed cell 0: they stay -inf
-            a = (HL > 0 && s0 < 0) ? NEG_INF_D : v;
-        }
-        // row pointers advance by W per frame (no per-frame 64-bit multiply on the scalar unit)
-        if (own) ap[sl] = a;
-        ap += W;
-        pb[d] = pbp[sl];
-        pe[d] = pep[sl];
-        if (t + D < T - 1) {
-            pbp += W;
-            pep += W;
-        }
-        if (BAND) {
-            const int tn = min(t + D, T - 1);
-            mn[d] = p.min_s[c0 + tn];
-            mx[d] = p.max_s[c0 + tn];
-        }
-    };
-    auto step = [&](int t, int d) {
-        if (LEAN) {
-            step_lean(t, d);
-            return;
-        }
-        const int lo = max(max(t - (T - 1 - S), mn[d]), 0);
-        const int hi = min(min(t + 1, S), mx[d]);
-        double carry = dpp_shr1(a);  // lane 0: garbage that only ever feeds halo lanes ...
-        if (HL == 0 && lane == 0) carry = NEG_INF_D;  // ... or, with no halo, alpha(t-1, -1)
-        const double v = lse2(a + pb[d], carry + pe[d]);
-        a = (s0 >= lo && s0 <= hi) ? v : NEG_INF_D;
-        if (own) p.alpha[r0 + (int64_t)t * W + s0] = a;
-        const int tn = min(t + D, T - 1);
-        pb[d] = p.lpb[r0 + (int64_t)tn * W + s0];
-        pe[d] = p.lpe[r0 + (int64_t)tn * W + s0 - 1];
-        mn[d] = BAND ? p.min_s[c0 + tn] : 0;
-        mx[d] = BAND ? p.max_s[c0 + tn] : S;
-    };
-    // whole blocks of D == HL steps (no early exit inside: the vmcnt waits stay D steps deep), a halo refresh from
-    // the wave below (its top HL own cells) after each, then the tail
-    int t0 = 0;
-    for (; t0 + D <= T; t0 += D) {
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-            step(t0 + d, d);
-            if (HL > 0 && (d + 1) % HLD == 0 && (d + 1 < D || t0 + D < T)) {
-                const int par = ((t0 + d) / HLD) & 1;
-                if (lane >= C) xh[par][wave][lane - C] = a;
-                __syncthreads();
-                if (wave > 0 && lane < HL) a = xh[par][wave - 1][lane];
-            }
-        }
-    }
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-        if (t0 + d >= T) break;
-        step(t0 + d, d);
-        if (HL > 0 && (d + 1) % HLD == 0 && t0 + d + 1 < T) {
-            const int par = ((t0 + d) / HLD) & 1;
-            if (lane >= C) xh[par][wave][lane - C] = a;
-            __syncthreads();
-            if (wave > 0 && lane < HL) a = xh[par][wave - 1][lane];
-        }
-    }
-    if (own && s0 == S) {
-        p.ll[b] = a;
-        if (costs) costs[b] = (float)(-a);
-    }
-}
-
-template <int D, int NW, int HL, bool BAND, int LEAN>
-__device__ __forceinline__ void beta_pass_halo(const DevProblem &p, int b, double (*xh)[8][HL > 0 ? HL : 1]) {
-    static_assert((HL == 0 ? NW == 1 : D % HL == 0) && NW <= 8,
-                  "halo refreshes at prefetch-block positions (HL = 0: one wave, no halo); xh sized for <= 8 waves");
-    constexpr int C = 64 - HL;
-    constexpr int HLD = HL > 0 ? HL : 1;  // divisor for the (compiled-out when HL == 0) refresh logic
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int T = p.T[b], S = p.S[b], W = S + 1;
-    const int64_t r0 = p.row_off[b], c0 = p.col_off[b];
-    const int s0 = wave * C + lane;  // lanes >= C: halo, the first HL cells of the wave above
-    const bool own = lane < C && s0 < W;
-    const unsigned sl = (unsigned)s0;
-
-    double bn = (s0 == S) ? 0.0 : NEG_INF_D;  // beta(T, s)
-    double pb[D], pe[D];
-    int mn[D], mx[D];
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-        const int tt = max(T - 1 - d, 0);
-        pb[d] = (p.lpb + (r0 + (int64_t)tt * W))[sl];
-        pe[d] = (p.lpe + (r0 + (int64_t)tt * W))[sl];
-        mn[d] = (BAND && tt > 0) ? p.min_s[c0 + tt - 1] : 0;
-        mx[d] = (BAND && tt > 0) ? p.max_s[c0 + tt - 1] : S;
-    }
-    double *bp_ = p.beta + r0 + (int64_t)(T - 1) * W;                   // beta row of the next frame (downwards)
-    const double *pbp = p.lpb + r0 + (int64_t)max(T - 1 - D, 0) * W;     // lp rows of the next prefetch
-    const double *pep = p.lpe + r0 + (int64_t)max(T - 1 - D, 0) * W;
-    auto step_lean = [&](int t, int d) {
-        // unrestricted: no band mask -- a cell below the band only sees -inf successors, one above it (s > t) only
-        // feeds cells above it and is never read (mrnnt_read_state masks it for inspection)
-        double carry = dpp_shl1_bc(bn);
-        if (HL == 0 && lane == 63) carry = NEG_INF_D;
-        const double v = lse2(bn + pb[d], carry + pe[d]);
-        if (BAND) {
-            int lo = 0, hi = 0;
-            if (t > 0) {
-                lo = max(max(t - (T - S), mn[d]), 0);
-                hi = min(min(t, S), mx[d]);
-            }
-            bn = (s0 >= lo && s0 <= hi) ? v : NEG_INF_D;
-        } else {
-            // lanes past S (halo lanes of the top wave) feed cell S from above: they stay -inf (with one wave, lane
-            // 63's successor is -inf and so are they)
-            bn = (HL > 0 && s0 > S) ? NEG_INF_D : v;
-        }
-        if (own) bp_[sl] = bn;
-        bp_ -= W;
-        pb[d] = pbp[sl];
-        pe[d] = pep[sl];
-        if (t - D > 0) {
-            pbp -= W;
-            pep -= W;
-        }
-        if (BAND) {
-            const int tn = max(t - D, 0);
-            mn[d] = tn > 0 ? p.min_s[c0 + tn - 1] : 0;
-            mx[d] = tn > 0 ? p.max_s[c0 + tn - 1] : S;
-        }
-    };
-    auto step = [&](int t, int d) {
-        if (LEAN) {
-            step_lean(t, d);
-            return;
-        }
-        int lo, hi;
-        if (t == 0) {
-            lo = 0;
-            hi = 0;
-        } else {
-            lo = max(max(t - (T - S), mn[d]), 0);
-            hi = min(min(t, S), mx[d]);
-        }
-        double carry = dpp_shl1(bn);  // lane 63: garbage that only ever feeds halo lanes ...
-        if (HL == 0 && lane == 63) carry = NEG_INF_D;  // ... or, with no halo, beta(t+1, 64) (S + 1 <= 64)
-        const double v = lse2(bn + pb[d], carry + pe[d]);
-        bn = (s0 >= lo && s0 <= hi) ? v : NEG_INF_D;
-        if (own) p.beta[r0 + (int64_t)t * W + s0] = bn;
-        const int tn = max(t - D, 0);
-        pb[d] = p.lpb[r0 + (int64_t)tn * W + s0];
-        pe[d] = p.lpe[r0 + (int64_t)tn * W + s0];
-        mn[d] = (BAND && tn > 0) ? p.min_s[c0 + tn - 1] : 0;
-        mx[d] = (BAND && tn > 0) ? p.max_s[c0 + tn - 1] : S;
-    };
-    int t0 = T - 1;
-    for (; t0 - D + 1 >= 0; t0 -= D) {
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-            step(t0 - d, d);
-            if (HL > 0 && (d + 1) % HLD == 0 && (d + 1 < D || t0 - D >= 0)) {  // refresh from the wave above
-                const int par = ((T - 1 - t0 + d) / HLD) & 1;
-                if (lane < HL) xh[par][wave][lane] = bn;
-                __syncthreads();
-                if (wave < NW - 1 && lane >= C) bn = xh[par][wave + 1][lane - C];
-            }
-        }
-    }
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-        if (t0 - d < 0) break;
-        step(t0 - d, d);
-        if (HL > 0 && (d + 1) % HLD == 0 && t0 - d - 1 >= 0) {
-            const int par = ((T - 1 - t0 + d) / HLD) & 1;
-            if (lane < HL) xh[par][wave][lane] = bn;
-            __syncthreads();
-            if (wave < NW - 1 && lane >= C) bn = xh[par][wave + 1][lane - C];
-        }
-    }
-    if (threadIdx.x == 0) p.llb[b] = bn;
-}
 
 template <int D, int NW, int HL, bool BAND, int LEAN = 0>
 __global__ __launch_bounds__(64 * NW) void recursion_halo_kernel(DevProblem p, int with_beta,

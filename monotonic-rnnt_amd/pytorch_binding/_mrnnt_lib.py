@@ -40,7 +40,7 @@ MRNNT_BF16 = 1
 MRNNT_F16 = 2
 
 # kernel-family order of mrnnt_profile_read
-KERNELS = ("band", "log_softmax", "alpha_beta", "grad", "setup", "joint_fwd", "joint_bwd", "joint_reduce")
+KERNELS = ("band", "log_softmax", "alpha_beta", "grad", "setup", "joint_fwd", "joint_bwd", "joint_reduce", "chase")
 
 
 class MrnntProblem(ctypes.Structure):

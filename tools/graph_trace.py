@@ -15,7 +15,7 @@ import os
 
 def short(name):
     n = name.split("(")[0]
-    for k in ("softmax", "recursion", "grad", "setup", "reduce_kernel", "Fill", "elementwise"):
+    for k in ("chase", "softmax", "recursion", "grad", "setup", "reduce_kernel", "Fill", "fill", "elementwise"):
         if k in n:
             return k + ("" if k not in ("softmax", "grad", "recursion") else ":" + n.split("<")[0].split("::")[-1])
     return n[-40:]
@@ -34,10 +34,11 @@ def main():
     rows.sort()
     steps, cur = [], []
     for r in rows:
-        if r[2].startswith("softmax") and cur:
+        first = r[2].startswith("softmax") or r[2].startswith("chase")  # the forward's first kernel of the path
+        if first and cur:
             steps.append(cur)
             cur = []
-        if r[2].startswith("softmax") or cur:
+        if first or cur:
             cur.append(r)
     if cur:
         steps.append(cur)
@@ -51,7 +52,9 @@ def main():
             gaps[f"{n0} -> {n1}"].append((b1 - e0) / 1e3)
         for b, e, n in s:
             dur[n].append((e - b) / 1e3)
+    period = [(b[0][0] - a[0][0]) / 1e3 for a, b in zip(steps, steps[1:])]  # start to start: the whole step
     out = {"trace": path, "steps": len(steps),
+           "step_period_us": round(sum(period) / len(period), 2) if period else None,
            "step_span_us": round(sum(spans) / len(spans), 2), "step_busy_us": round(sum(busy) / len(busy), 2),
            "kernel_us": {k: round(sum(v) / len(v), 2) for k, v in dur.items()},
            "gap_us": {k: round(sum(v) / len(v), 2) for k, v in gaps.items()}}
