@@ -9,9 +9,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <random>
 #include <string>
 #include <vector>
 
@@ -62,8 +65,8 @@ struct Plan {
     int64_t pad_T = 0, pad_S1 = 0;
     bool align = false;
     bool dyn = false;
-    size_t off_flags = 0, flags_bytes = 0;  // the chase launch's ready flags (host lengths: 2 words per column)
-    size_t off_row, off_col, off_colb, off_mtmp, off_min, off_max, off_den, off_lpb, off_lpe, off_alpha, off_beta, off_ll,
+    size_t off_flags = 0, flags_bytes = 0;  // the chase launch's ready flags (host lengths: 2 x 8 bytes per column)
+    size_t off_row, off_col, off_colb, off_mtmp, off_min, off_max, off_den, off_lp, off_alpha, off_beta, off_ll,
         off_llb, off_dyn, total;
 };
 
@@ -162,19 +165,16 @@ RNNTStatus make_plan(const mrnnt_problem *p, Plan *pl) {
         o = align_up(o + bytes);
         return at;
     };
-    // first: the chase launch's flags (mrnnt_chase.hip), a block of its own starting at the workspace's start and
-    // padded to 16 bytes -- the memset that clears them every call is cheapest so (cdna_hip_programming.md
-    // Guideline 16, Re-initialise every call)
+    // the chase launch's ready flags (mrnnt_chase.hip; host lengths only)
     if (!q.dyn) {
-        q.flags_bytes = (sizeof(unsigned) * 2 * (size_t)q.cols + 15) / 16 * 16;
+        q.flags_bytes = sizeof(unsigned long long) * 2 * (size_t)q.cols;
         q.off_flags = take(q.flags_bytes);
     }
     q.off_row = take(sizeof(int64_t) * (q.B + 1));
     q.off_col = take(sizeof(int64_t) * (q.B + 1));
     q.off_colb = take(sizeof(int) * q.cols);
     q.off_den = take(sizeof(float) * q.N);
-    q.off_lpb = take(sizeof(double) * (q.N + 2 * kLpPad));
-    q.off_lpe = take(sizeof(double) * (q.N + 2 * kLpPad));
+    q.off_lp = take(sizeof(Lp) * (q.N + 2 * kLpPad));
     q.off_alpha = take(sizeof(double) * q.N);
     q.off_beta = take(sizeof(double) * q.N);
     q.off_ll = take(sizeof(double) * q.B);
@@ -224,6 +224,20 @@ int64_t scatter_mul(int64_t cols) {
     }
 }
 
+// A fresh 64-bit tag per chase launch (mrnnt_chase.hip): a bijective mix of a process-wide counter whose start is
+// random per process, so no two calls of a process share one and a stale word matches with probability 2^-64.
+uint64_t chase_epoch() {
+    static std::atomic<uint64_t> ctr{((uint64_t)std::random_device{}() << 32) ^ (uint64_t)std::random_device{}() ^
+                                     (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count()};
+    uint64_t x = ctr.fetch_add(1, std::memory_order_relaxed) * 0x9E3779B97F4A7C15ull;
+    x ^= x >> 30;
+    x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 27;
+    x *= 0x94D049BB133111EBull;
+    x ^= x >> 31;
+    return x ? x : 1;
+}
+
 DevProblem make_dev(const mrnnt_problem *p, const Plan &pl, const void *ws) {
     char *w = static_cast<char *>(const_cast<void *>(ws));
     DevProblem d;
@@ -255,8 +269,7 @@ DevProblem make_dev(const mrnnt_problem *p, const Plan &pl, const void *ws) {
     d.scale_stride = p->grad_scale_broadcast ? 0 : 1;
     d.col_mul = 0;  // set per pass by mrnnt_forward / mrnnt_backward (tuning().col_scatter)
     d.den = reinterpret_cast<float *>(w + pl.off_den);
-    d.lpb = reinterpret_cast<double *>(w + pl.off_lpb) + kLpPad;
-    d.lpe = reinterpret_cast<double *>(w + pl.off_lpe) + kLpPad;
+    d.lp = reinterpret_cast<Lp *>(w + pl.off_lp) + kLpPad;
     d.alpha = reinterpret_cast<double *>(w + pl.off_alpha);
     d.beta = reinterpret_cast<double *>(w + pl.off_beta);
     d.ll = reinterpret_cast<double *>(w + pl.off_ll);
@@ -306,6 +319,22 @@ int streaming_grid(int64_t cols, int per_cu) {
     // every streaming kernel walks its columns grid-stride, so larger problems just take more than one turn)
     const int64_t g = per_cu <= 0 ? std::min<int64_t>(cols, 1 << 22) : (int64_t)cu_count[dev] * per_cu;
     return (int)std::max<int64_t>(1, std::min<int64_t>(g, cols));
+}
+
+// The chase launch (mrnnt_chase.hip) where it pays and is safe:
+// * its recursion workgroups spin while they wait, so together they must leave the chip room for the log-softmax
+//   workgroups they wait for: at most one per CU (B or 2B <= CUs, whatever the dispatch order);
+// * one 4-wave workgroup runs the halo recursion (S + 1 <= 4 * 56), and the lp array is one buffer descriptor
+//   (N * 16 bytes < 2^31);
+// * it saves the recursion's time (~T_max steps of ~0.1 us) at the price of a slightly slower log-softmax pass
+//   (+5-10 %, the hand-off and the production order): taken when the recursion is at least a quarter of the pass's
+//   streaming time (configs[1]: 20 vs 22 us; the headline: 0.16 vs 6.5 ms, not taken).
+bool chase_pays(const Plan &pl, bool with_beta) {
+    if ((with_beta ? 2 * pl.B : pl.B) > streaming_grid((int64_t)1 << 40, 1)) return false;
+    if (pl.S_max + 1 > 4 * 56 || pl.N * (int64_t)sizeof(Lp) >= ((int64_t)1 << 31)) return false;
+    const double elem = pl.elem == ELEM_F32 ? 4.0 : 2.0;
+    const double pass_s = (double)pl.N * pl.V * elem / 6.0e12, recursion_s = (double)pl.T_max * 1.0e-7;
+    return recursion_s >= 0.25 * pass_s;
 }
 
 // ---- profiling ---------------------------------------------------------------------------------
@@ -447,8 +476,7 @@ RNNTStatus mrnnt_forward(const mrnnt_problem *p, void *ws, size_t ws_bytes, floa
         a.row_off = reinterpret_cast<int64_t *>(w + pl.off_row);
         a.col_off = reinterpret_cast<int64_t *>(w + pl.off_col);
         a.col_b = reinterpret_cast<int *>(w + pl.off_colb);
-        a.lpb = d.lpb;
-        a.lpe = d.lpe;
+        a.lp = d.lp;
         a.dyn = d.dyn;
         e = timed(K_SETUP, stream, [&] { return launch_setup_dyn(a, stream); });
         if (e != hipSuccess) return fail_hip(e, "device-lengths setup kernel");
@@ -456,7 +484,7 @@ RNNTStatus mrnnt_forward(const mrnnt_problem *p, void *ws, size_t ws_bytes, floa
         e = timed(K_SETUP, stream, [&] {
             return launch_setup(p->T_dev, p->S_dev, pl.B, reinterpret_cast<int64_t *>(w + pl.off_row),
                                 reinterpret_cast<int64_t *>(w + pl.off_col),
-                                reinterpret_cast<int *>(w + pl.off_colb), nullptr, nullptr, 0, stream);
+                                reinterpret_cast<int *>(w + pl.off_colb), nullptr, 0, stream);
         });
         if (e != hipSuccess) return fail_hip(e, "setup kernel");
     }
@@ -469,17 +497,19 @@ RNNTStatus mrnnt_forward(const mrnnt_problem *p, void *ws, size_t ws_bytes, floa
         if (e != hipSuccess) return fail_hip(e, "alignment band kernels");
     }
     // host lengths, no alignment: the forward as one launch, the recursion chasing the log-softmax (mrnnt_chase.hip),
-    // where it has a body for these rows
-    if (!pl.dyn && !pl.align && tuning().chase && chase_body(d, pl.elem) >= 0 && pl.S_max + 1 <= 4 * 56 &&
-        chase_grid(d, pl.T_max, with_beta ? 1 : 0) <= ((int64_t)1 << 22)) {
+    // where it has a body for these rows and pays (chase_pays)
+    if (!pl.dyn && !pl.align && tuning().chase && chase_body(d, pl.elem) >= 0 && chase_pays(pl, with_beta)) {
         ChaseArgs ca;
-        ca.flags = reinterpret_cast<unsigned *>(w + pl.off_flags);
+        ca.flags = reinterpret_cast<unsigned long long *>(w + pl.off_flags);
         ca.cols = pl.cols;
-        // the ready flags are zeroed before every launch (a memset node under graph capture): a launch's producers
-        // store 1, its consumers wait for 1
-        if ((e = hipMemsetAsync(ca.flags, 0, pl.flags_bytes, stream)) != hipSuccess) return fail_hip(e, "flag reset");
+        ca.slots = chase_slots(d, pl.T_max, with_beta ? 1 : 0);
+        ca.epoch = chase_epoch();
+        ca.probe = kVariants ? tuning().chase_probe : 0;
+        const int nrec = with_beta ? 2 * pl.B : pl.B;
+        const int producers = (int)std::min<int64_t>(streaming_grid(ca.slots, tuning().chase_grid_per_cu),
+                                                     ((int64_t)1 << 22) - nrec);
         e = timed(K_CHASE, stream, [&] {
-            return launch_chase(d, ca, pl.elem, pl.S_max, pl.T_max, with_beta ? 1 : 0, costs_dev, stream);
+            return launch_chase(d, ca, pl.elem, pl.S_max, with_beta ? 1 : 0, producers, costs_dev, stream);
         });
         if (e != hipSuccess) return fail_hip(e, "chase kernel");
         return RNNT_STATUS_SUCCESS;
@@ -618,8 +648,8 @@ RNNTStatus mrnnt_read_band(const mrnnt_problem *p, void *ws, int *min_dev, int *
         e = launch_setup_dyn(a, stream);
     } else if (!p->lattice) {
         e = launch_setup(p->T_dev, p->S_dev, pl.B, reinterpret_cast<int64_t *>(w + pl.off_row),
-                         reinterpret_cast<int64_t *>(w + pl.off_col), reinterpret_cast<int *>(w + pl.off_colb), nullptr,
-                         nullptr, 0, stream);
+                         reinterpret_cast<int64_t *>(w + pl.off_col), reinterpret_cast<int *>(w + pl.off_colb), nullptr, 0,
+                         stream);
     }
     if (e != hipSuccess) return fail_hip(e, "setup kernel");
     if (pl.align) {
@@ -790,7 +820,7 @@ RNNTStatus mrnnt_joint_forward(const mrnnt_joint_problem *jp, void *ws, size_t w
     hipError_t e = timed(K_SETUP, stream, [&] {
         return launch_setup(jp->T_dev, jp->S_dev, pl.B, reinterpret_cast<int64_t *>(w + pl.off_row),
                             reinterpret_cast<int64_t *>(w + pl.off_col),
-                            reinterpret_cast<int *>(w + pl.off_colb), nullptr, nullptr, 0, stream);
+                            reinterpret_cast<int *>(w + pl.off_colb), nullptr, 0, stream);
     });
     if (e != hipSuccess) return fail_hip(e, "setup kernel");
     if (pl.align) {
@@ -802,7 +832,7 @@ RNNTStatus mrnnt_joint_forward(const mrnnt_joint_problem *jp, void *ws, size_t w
         if (e != hipSuccess) return fail_hip(e, "alignment band kernels");
     }
     // out-of-band lp entries must be finite for the recursion (the acts path zero-fills them in its pass)
-    if ((e = launch_zero(w + pl.off_lpb, pl.off_alpha - pl.off_lpb, stream)) != hipSuccess)
+    if ((e = launch_zero(w + pl.off_lp, pl.off_alpha - pl.off_lp, stream)) != hipSuccess)
         return fail_hip(e, "lp zero fill");
     e = launch_row_list(d, 0, reinterpret_cast<int64_t *>(w + jl.off_cnt), reinterpret_cast<int *>(w + jl.off_lcol),
                         reinterpret_cast<int *>(w + jl.off_ls), reinterpret_cast<unsigned long long *>(w + jl.off_total),
@@ -954,6 +984,8 @@ __attribute__((visibility("default"))) int mrnnt_tune(const char *key, int value
     else if (!std::strcmp(key, "dyn_fused")) slot = &t.dyn_fused;
     else if (!std::strcmp(key, "chase")) slot = &t.chase;
     else if (!std::strcmp(key, "chase_depth")) slot = &t.chase_depth;
+    else if (!std::strcmp(key, "chase_probe")) slot = &t.chase_probe;
+    else if (!std::strcmp(key, "chase_grid_per_cu")) slot = &t.chase_grid_per_cu;
     else if (!std::strcmp(key, "nt_load")) slot = &t.nt_load;
     else if (!std::strcmp(key, "occ_skip")) slot = &t.occ_skip;
     else if (!std::strcmp(key, "joint_nbuf")) slot = &t.joint_nbuf;

@@ -245,10 +245,8 @@ __device__ __forceinline__ void publish_lengths(const DevProblem &p, const WaveL
                                __HIP_MEMORY_SCOPE_SYSTEM);
     }
     const int64_t end = w.ok ? w.R : 0;
-    p.lpb[lane - 64] = 0.0;
-    p.lpe[lane - 64] = 0.0;
-    p.lpb[end + lane] = 0.0;
-    p.lpe[end + lane] = 0.0;
+    p.lp[lane - 64] = Lp{0.0, 0.0};
+    p.lp[end + lane] = Lp{0.0, 0.0};
 }
 
 // Column walk of a workgroup of a streaming kernel: visits ci = blockIdx.x, blockIdx.x + gridDim.x, ... < num_cols,
@@ -347,8 +345,7 @@ __device__ __forceinline__ double log_row_sum(float s) {
 __device__ __forceinline__ void write_row(const DevProblem &p, int64_t row, float m, float sum, float zb, float ze) {
     const double den = -(double)m - log_row_sum(sum);
     p.den[row] = (float)den;
-    p.lpb[row] = (double)zb + den;
-    p.lpe[row] = (double)ze + den;
+    p.lp[row] = Lp{(double)zb + den, (double)ze + den};
 }
 
 // ---- element-type traits of the acts / grads I/O (math is fp32 in registers) ----------------------
@@ -456,8 +453,9 @@ __device__ __forceinline__ RowCoef row_coef(const DevProblem &p, int t, int T, i
     rc.c2 = (float)(((double)p.den[row] + base + b0) * kLog2eD);
     // the exponents are O(10) after the fp64 cancellation of alpha + beta - ll: fp32 v_exp_f32 on the
     // rounded exponent (relative error ~1e-6 of a coefficient <= 1)
-    rc.cb = fast_exp2((float)((p.lpb[row] + base + b1) * kLog2eD));
-    rc.ce = (s < S) ? fast_exp2((float)((p.lpe[row] + base + b2) * kLog2eD)) : 0.0f;
+    const Lp l = p.lp[row];
+    rc.cb = fast_exp2((float)((l.b + base + b1) * kLog2eD));
+    rc.ce = (s < S) ? fast_exp2((float)((l.e + base + b2) * kLog2eD)) : 0.0f;
     const int lab = (s < S) ? lab_b[s] : -1;
     rc.lab = (lab == p.blank || (unsigned)lab >= (unsigned)p.V) ? -1 : lab;  // out of range: never matched / written
     return rc;
@@ -512,6 +510,21 @@ __device__ __forceinline__ T load_wt(const T *ptr) {
     typedef typename WordOf<sizeof(T)>::T W;
     return __builtin_bit_cast(
         T, __hip_atomic_load((__attribute__((address_space(1))) W *)ptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// The lp array as a buffer resource: 16-byte write-through stores and L1-bypassing loads of whole Lp rows (an
+// agent-scope atomic covers 8 bytes at most; 8-byte sc1 loads run at about half the 16-byte rate). Rows [0, N) only
+// (the chase launch checks N * 16 < 2^31 on the host); the descriptor is built from kernel-argument values only.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t lp_rsrc(const DevProblem &p) {
+    return __builtin_amdgcn_make_buffer_rsrc(static_cast<void *>(p.lp), (short)0, (int)(p.num_rows * (int64_t)sizeof(Lp)),
+                                             0x00020000);
+}
+constexpr int kAuxSc1 = 16;  // buffer instruction cache-policy bits: sc1
+__device__ __forceinline__ Lp load_lp_wt(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
+    return __builtin_bit_cast(Lp, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, kAuxSc1));
+}
+__device__ __forceinline__ void store_lp_wt(__amdgpu_buffer_rsrc_t r, unsigned voff, Lp v) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), r, voff, 0, kAuxSc1);
 }
 
 // every store this wave issued has completed (the drain before a hand-off flag)

@@ -34,43 +34,64 @@ __device__ __forceinline__ double dpp_shl1_bc(double v) {
 }
 
 // The recursion side of the chase launch (mrnnt_chase.hip). A lattice column of the utterance may be read once its
-// log-softmax workgroup has published it: its ready flag (one 32-bit word per column and direction) reads `want`.
-// One wave polls the flags of the next 64 frames of its walk in one vector load and keeps the run of ready frames
-// (rdy), so a wave that runs behind the producers polls once per 64 frames. Spins are bounded: a wave that gives up
-// marks the workgroup failed (its costs become NaN) and stops waiting.
+// log-softmax workgroup has published it: its ready flag (one 64-bit word per column and direction) reads `want`.
+// A wave keeps the run of walk positions known ready (rdy). At the start of every prefetch block it reads the poll
+// it issued one block earlier -- the flags of the 64 positions from rdy, one vector load -- and issues the next:
+// unconditional, so the compiler's wait for it counts the lp loads issued since and does not drain them, and a
+// wave that runs behind the producers never stalls on a poll round trip. A frame beyond rdy waits in a blocking
+// poll. Spins are bounded: a wave that gives up marks the workgroup failed (its costs become NaN) and stops waiting.
 constexpr unsigned kChaseSpins = 1u << 20;
 
 struct Chase {
-    const unsigned *flags;  // ready flag of frame 0 of this utterance, this direction
-    unsigned want;          // the value this launch's producers store
+    const unsigned long long *flags;  // ready flag of frame 0 of this utterance, this direction
+    unsigned long long want;          // the value this launch's producers store (its epoch)
     int T;
     bool fwd;               // alpha walks t = 0, 1, ...; beta t = T - 1, T - 2, ...
     int rdy;                // walk positions [0, rdy) known ready (wave-uniform)
+    int ahead_at;           // `ahead`: this lane's flag of walk position ahead_at + lane (a poll issued earlier)
+    unsigned long long ahead;
     unsigned spins;
     bool failed;
+    bool nowait;            // (development probe: never wait)
     int *fail_lds;          // the workgroup's failure word (LDS)
 
-    __device__ __forceinline__ void init(const unsigned *f, unsigned w, int T_, bool forward, int *lds) {
+    __device__ __forceinline__ void init(const unsigned long long *f, unsigned long long w, int T_, bool forward,
+                                         int *lds) {
         flags = f;
         want = w;
         T = T_;
         fwd = forward;
         rdy = 0;
+        ahead_at = 0;
+        ahead = 0;  // (no poll yet: reads as not ready)
         spins = 0;
         failed = false;
+        nowait = false;
         fail_lds = lds;
+    }
+    // this lane's flag of walk position u + lane (positions past the walk read as ready)
+    __device__ __forceinline__ unsigned long long poll(int u) const {
+        const int i = u + (int)(threadIdx.x & 63);
+        return i < T ? load_wt(&flags[fwd ? i : T - 1 - i]) : want;
+    }
+    __device__ __forceinline__ int run_of(unsigned long long v) const {
+        const unsigned long long miss = ~__ballot(v == want);
+        return miss ? __builtin_ctzll(miss) : 64;
+    }
+    // start of a prefetch block: take the earlier poll's run, issue the next poll
+    __device__ __forceinline__ void refresh() {
+        const int run = run_of(ahead);
+        if (ahead_at <= rdy) rdy = max(rdy, ahead_at + run);
+        ahead_at = min(rdy, T);
+        ahead = poll(ahead_at);
     }
     // frame f is about to be read
     __device__ __forceinline__ void gate(int f) {
         const int u = fwd ? f : T - 1 - f;
         if (u < rdy) return;
-        const int lane = threadIdx.x & 63;
+        if (kVariants && nowait) return;
         for (;;) {
-            const int i = u + lane;
-            bool ok = true;
-            if (i < T) ok = load_wt(&flags[fwd ? i : T - 1 - i]) == want;
-            const unsigned long long miss = ~__ballot(ok);
-            const int run = miss ? __builtin_ctzll(miss) : 64;
+            const int run = run_of(poll(u));
             if (run > 0) {
                 rdy = u + run;
                 return;
@@ -93,7 +114,7 @@ struct Chase {
 // neighbouring wave owns (alpha: the cells below, beta: the cells above). Those halo lanes lose one valid lane
 // per step (their outer neighbour is not in the wave), so the own cells stay exact for HL steps; then the
 // neighbour's HL boundary cells are copied in through LDS (one barrier per HL steps instead of one per step).
-template <int D, int NW, int HL, bool BAND, int LEAN, bool CH = false>
+template <int D, int NW, int HL, bool BAND, int LEAN, bool CH = false, bool SC1 = CH>
 __device__ __forceinline__ void alpha_pass_halo(const DevProblem &p, int b, float *__restrict__ costs,
                                                 double (*xh)[8][HL > 0 ? HL : 1], Chase *ch = nullptr) {
     static_assert(!CH || (LEAN && !BAND), "the chase launch runs the lean, unrestricted step");
@@ -110,15 +131,18 @@ __device__ __forceinline__ void alpha_pass_halo(const DevProblem &p, int b, floa
     // LEAN: every row access is a uniform row pointer (SGPRs) + an unsigned lane offset; the halo lanes of wave 0
     // (s0 < 0, never in band) read cell 0
     const unsigned sl = (unsigned)max(s0, 0);
-    // CH: lp rows are read only inside this utterance's column (s in [0, S]; lpe of s - 1 from s = 1): rows of other
-    // columns may not be published yet, and cell 0 (whose predecessor is -inf) and the cells above S (which feed only
-    // cells above S) would read them.
-    // Those lanes read a row of the column instead (clamped offsets, unconditional loads -- a load under an exec
-    // branch would cost the prefetch its overlap): a finite lp that only ever meets a -inf predecessor or feeds cells
-    // above S, as the rows of the neighbouring columns do in the two-kernel path.
-    const unsigned slb = CH ? min(sl, (unsigned)S) : sl, sle = CH ? min(max(sl, 1u), (unsigned)max(S, 1)) : sl;
-    auto ldb = [&](const double *row) { return CH ? load_wt(row + slb) : row[sl]; };
-    auto lde = [&](const double *row) { return CH ? load_wt(row + sle) : row[sl]; };
+    // Every lane reads the lp of its own row (t, s): lpb for its own transition and lpe for its upper neighbour's,
+    // which gets alpha(t-1, s) + lpe(t, s) shifted up one lane -- one 16-byte load per lane and frame.
+    // CH: lp rows are read only inside this utterance's column: rows of other columns may not be published yet. The
+    // lanes above S (which feed only cells above S) read row S instead (clamped offset, unconditional load -- a load
+    // under an exec branch would cost the prefetch its overlap); the halo lanes of wave 0 read row 0 as before.
+    const unsigned slc = CH ? min(sl, (unsigned)S) : sl;
+    auto ld = [&](const Lp *row) -> Lp {
+        if constexpr (CH && SC1)
+            return load_lp_wt(lp_rsrc(p), slc * (unsigned)sizeof(Lp), (unsigned)((row - p.lp) * (int64_t)sizeof(Lp)));
+        else
+            return row[slc];
+    };
 
     double a = (s0 == 0) ? 0.0 : NEG_INF_D;
     double pb[D], pe[D];
@@ -127,26 +151,21 @@ __device__ __forceinline__ void alpha_pass_halo(const DevProblem &p, int b, floa
     for (int d = 0; d < D; ++d) {
         const int tt = min(d, T - 1);
         if (CH) ch->gate(tt);
-        if (LEAN) {
-            pb[d] = ldb(p.lpb + (r0 + (int64_t)tt * W));
-            pe[d] = lde(p.lpe + (r0 + (int64_t)tt * W - 1));
-        } else {
-            pb[d] = p.lpb[r0 + (int64_t)tt * W + s0];
-            pe[d] = p.lpe[r0 + (int64_t)tt * W + s0 - 1];
-        }
+        const Lp l = LEAN ? ld(p.lp + (r0 + (int64_t)tt * W)) : p.lp[r0 + (int64_t)tt * W + s0];
+        pb[d] = l.b;
+        pe[d] = l.e;
         mn[d] = BAND ? p.min_s[c0 + tt] : 0;
         mx[d] = BAND ? p.max_s[c0 + tt] : S;
     }
     double *ap = p.alpha + r0;                                           // alpha row of the next frame
-    const double *pbp = p.lpb + r0 + (int64_t)min(D, T - 1) * W;         // lp rows of the next prefetch
-    const double *pep = p.lpe + r0 + (int64_t)min(D, T - 1) * W - 1;
+    const Lp *lpp = p.lp + r0 + (int64_t)min(D, T - 1) * W;              // lp row of the next prefetch
     auto step_lean = [&](int t, int d) {
         // unrestricted: no band mask -- a cell above the band only ever sees -inf predecessors (so it is -inf), a
         // cell below it only feeds cells below it and is never read (mrnnt_read_state masks it for inspection);
         // halo lanes are garbage between refreshes exactly as in the masked step (they only feed halo lanes)
-        double carry = dpp_shr1_bc(a);
-        if (HL == 0 && lane == 0) carry = NEG_INF_D;
-        const double v = lse2(a + pb[d], carry + pe[d]);
+        double y = dpp_shr1_bc(a + pe[d]);  // alpha(t-1, s-1) + lpe(t, s-1), from lane s-1
+        if (HL == 0 && lane == 0) y = NEG_INF_D;
+        const double v = lse2(a + pb[d], y);
         if (BAND) {
             const int lo = max(max(t - (T - 1 - S), mn[d]), 0);
             const int hi = min(min(t + 1, S), mx[d]);
@@ -159,12 +178,10 @@ __device__ __forceinline__ void alpha_pass_halo(const DevProblem &p, int b, floa
         if (own) ap[sl] = a;
         ap += W;
         if (CH) ch->gate(min(t + D, T - 1));
-        pb[d] = ldb(pbp);
-        pe[d] = lde(pep);
-        if (t + D < T - 1) {
-            pbp += W;
-            pep += W;
-        }
+        const Lp l = ld(lpp);
+        pb[d] = l.b;
+        pe[d] = l.e;
+        if (t + D < T - 1) lpp += W;
         if (BAND) {
             const int tn = min(t + D, T - 1);
             mn[d] = p.min_s[c0 + tn];
@@ -178,14 +195,15 @@ __device__ __forceinline__ void alpha_pass_halo(const DevProblem &p, int b, floa
         }
         const int lo = max(max(t - (T - 1 - S), mn[d]), 0);
         const int hi = min(min(t + 1, S), mx[d]);
-        double carry = dpp_shr1(a);  // lane 0: garbage that only ever feeds halo lanes ...
-        if (HL == 0 && lane == 0) carry = NEG_INF_D;  // ... or, with no halo, alpha(t-1, -1)
-        const double v = lse2(a + pb[d], carry + pe[d]);
+        double y = dpp_shr1(a + pe[d]);  // lane 0: garbage that only ever feeds halo lanes ...
+        if (HL == 0 && lane == 0) y = NEG_INF_D;  // ... or, with no halo, alpha(t-1, -1) + lpe
+        const double v = lse2(a + pb[d], y);
         a = (s0 >= lo && s0 <= hi) ? v : NEG_INF_D;
         if (own) p.alpha[r0 + (int64_t)t * W + s0] = a;
         const int tn = min(t + D, T - 1);
-        pb[d] = p.lpb[r0 + (int64_t)tn * W + s0];
-        pe[d] = p.lpe[r0 + (int64_t)tn * W + s0 - 1];
+        const Lp l = p.lp[r0 + (int64_t)tn * W + s0];
+        pb[d] = l.b;
+        pe[d] = l.e;
         mn[d] = BAND ? p.min_s[c0 + tn] : 0;
         mx[d] = BAND ? p.max_s[c0 + tn] : S;
     };
@@ -195,6 +213,7 @@ __device__ __forceinline__ void alpha_pass_halo(const DevProblem &p, int b, floa
     for (; t0 + D <= T; t0 += D) {
 #pragma unroll
         for (int d = 0; d < D; ++d) {
+            if (CH && d == 0) ch->refresh();
             step(t0 + d, d);
             if (HL > 0 && (d + 1) % HLD == 0 && (d + 1 < D || t0 + D < T)) {
                 const int par = ((t0 + d) / HLD) & 1;
@@ -222,7 +241,7 @@ __device__ __forceinline__ void alpha_pass_halo(const DevProblem &p, int b, floa
     if (CH) ch->finish();
 }
 
-template <int D, int NW, int HL, bool BAND, int LEAN, bool CH = false>
+template <int D, int NW, int HL, bool BAND, int LEAN, bool CH = false, bool SC1 = CH>
 __device__ __forceinline__ void beta_pass_halo(const DevProblem &p, int b, double (*xh)[8][HL > 0 ? HL : 1],
                                                Chase *ch = nullptr) {
     static_assert(!CH || (LEAN && !BAND), "the chase launch runs the lean, unrestricted step");
@@ -240,7 +259,12 @@ __device__ __forceinline__ void beta_pass_halo(const DevProblem &p, int b, doubl
     // CH: lp rows read only inside this utterance's column: the cells above S (which stay -inf) read row S instead
     // (clamped offset, unconditional load; as alpha_pass_halo)
     const unsigned slc = CH ? min(sl, (unsigned)S) : sl;
-    auto ld = [&](const double *row) { return CH ? load_wt(row + slc) : row[sl]; };
+    auto ld = [&](const Lp *row) -> Lp {
+        if constexpr (CH && SC1)
+            return load_lp_wt(lp_rsrc(p), slc * (unsigned)sizeof(Lp), (unsigned)((row - p.lp) * (int64_t)sizeof(Lp)));
+        else
+            return row[slc];
+    };
 
     double bn = (s0 == S) ? 0.0 : NEG_INF_D;  // beta(T, s)
     double pb[D], pe[D];
@@ -249,14 +273,14 @@ __device__ __forceinline__ void beta_pass_halo(const DevProblem &p, int b, doubl
     for (int d = 0; d < D; ++d) {
         const int tt = max(T - 1 - d, 0);
         if (CH) ch->gate(tt);
-        pb[d] = ld(p.lpb + (r0 + (int64_t)tt * W));
-        pe[d] = ld(p.lpe + (r0 + (int64_t)tt * W));
+        const Lp l = ld(p.lp + (r0 + (int64_t)tt * W));
+        pb[d] = l.b;
+        pe[d] = l.e;
         mn[d] = (BAND && tt > 0) ? p.min_s[c0 + tt - 1] : 0;
         mx[d] = (BAND && tt > 0) ? p.max_s[c0 + tt - 1] : S;
     }
     double *bp_ = p.beta + r0 + (int64_t)(T - 1) * W;                   // beta row of the next frame (downwards)
-    const double *pbp = p.lpb + r0 + (int64_t)max(T - 1 - D, 0) * W;     // lp rows of the next prefetch
-    const double *pep = p.lpe + r0 + (int64_t)max(T - 1 - D, 0) * W;
+    const Lp *lpp = p.lp + r0 + (int64_t)max(T - 1 - D, 0) * W;          // lp row of the next prefetch
     auto step_lean = [&](int t, int d) {
         // unrestricted: no band mask -- a cell below the band only sees -inf successors, one above it (s > t) only
         // feeds cells above it and is never read (mrnnt_read_state masks it for inspection)
@@ -278,12 +302,10 @@ __device__ __forceinline__ void beta_pass_halo(const DevProblem &p, int b, doubl
         if (own) bp_[sl] = bn;
         bp_ -= W;
         if (CH) ch->gate(max(t - D, 0));
-        pb[d] = ld(pbp);
-        pe[d] = ld(pep);
-        if (t - D > 0) {
-            pbp -= W;
-            pep -= W;
-        }
+        const Lp l = ld(lpp);
+        pb[d] = l.b;
+        pe[d] = l.e;
+        if (t - D > 0) lpp -= W;
         if (BAND) {
             const int tn = max(t - D, 0);
             mn[d] = tn > 0 ? p.min_s[c0 + tn - 1] : 0;
@@ -309,8 +331,9 @@ __device__ __forceinline__ void beta_pass_halo(const DevProblem &p, int b, doubl
         bn = (s0 >= lo && s0 <= hi) ? v : NEG_INF_D;
         if (own) p.beta[r0 + (int64_t)t * W + s0] = bn;
         const int tn = max(t - D, 0);
-        pb[d] = p.lpb[r0 + (int64_t)tn * W + s0];
-        pe[d] = p.lpe[r0 + (int64_t)tn * W + s0];
+        const Lp l = p.lp[r0 + (int64_t)tn * W + s0];
+        pb[d] = l.b;
+        pe[d] = l.e;
         mn[d] = (BAND && tn > 0) ? p.min_s[c0 + tn - 1] : 0;
         mx[d] = (BAND && tn > 0) ? p.max_s[c0 + tn - 1] : S;
     };
@@ -318,6 +341,7 @@ __device__ __forceinline__ void beta_pass_halo(const DevProblem &p, int b, doubl
     for (; t0 - D + 1 >= 0; t0 -= D) {
 #pragma unroll
         for (int d = 0; d < D; ++d) {
+            if (CH && d == 0) ch->refresh();
             step(t0 - d, d);
             if (HL > 0 && (d + 1) % HLD == 0 && (d + 1 < D || t0 - D >= 0)) {  // refresh from the wave above
                 const int par = ((T - 1 - t0 + d) / HLD) & 1;

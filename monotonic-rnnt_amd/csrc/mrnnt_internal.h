@@ -14,6 +14,13 @@ enum ElemType { ELEM_F32 = 0, ELEM_BF16 = 1, ELEM_F16 = 2 };
 
 // Device-resident lengths (mrnnt_problem.lengths_on_device): the setup kernel of the call validates the lengths
 // and publishes what the host could not plan, for the later kernels of the same call (one 64-byte line).
+// The two log-probabilities of a lattice row the recursion reads, side by side: one 16-byte access per row (the
+// alpha step takes lpe(t, s - 1) as the shifted sum alpha(t - 1, s - 1) + lpe(t, s - 1) formed in lane s - 1).
+struct alignas(16) Lp {
+    double b;  // lpb = z[r, blank] + den[r]
+    double e;  // lpe = z[r, label(s)] + den[r] (s < S; s == S: den[r])
+};
+
 struct DynWords {
     int status;                // 0, or RNNT_STATUS_INVALID_VALUE: the lengths failed validation (nothing runs)
     int pad_;
@@ -48,8 +55,7 @@ struct DevProblem {
     int64_t col_mul;            // column visiting order of the streaming kernels (visit_col): 0 in order, > 0 the
                                 // i-th column visited is (i * col_mul) % num_cols (coprime), < 0 XCD-chunked
     float *den;                 // [N]  log-softmax denominator  -max - log sum exp(z - max)
-    double *lpb;                // [N]  z[r, blank] + den[r]
-    double *lpe;                // [N]  z[r, label(s)] + den[r]   (s < S)
+    Lp *lp;                     // [N]  {z[r, blank] + den[r], z[r, label(s)] + den[r] (s < S)}; 64 pads either side
     double *alpha;              // [N]  alpha(t, s), masked cells = -inf
     double *beta;               // [N]  beta(t, s)
     double *ll;                 // [B]  alpha(T-1, S)
@@ -129,7 +135,9 @@ struct Tuning {
                                   // (0: a separate setup kernel)
     int chase = 1;                // forward as one launch, the recursion chasing the log-softmax (mrnnt_chase.hip) where
                                   // it applies (host lengths, no alignment, f32 rows of <= 256 vectors, S + 1 <= 224)
-    int chase_depth = 16;         // lp rows the chase recursion prefetches (16; 8 in the development build)
+    int chase_depth = 8;          // lp rows the chase recursion prefetches (8; 16 in the development build)
+    int chase_grid_per_cu = 0;    // log-softmax workgroups of the chase launch per CU (0: one per slot)
+    int chase_probe = 0;          // development build: 1 -> the chase's log-softmax side alone, 2 -> also no hand-off
     int col_xcd = 0;              // XCD-chunked column order (visit_col, col_mul < 0; overrides col_scatter): bit 0
                                   // log-softmax, bit 1 gradient
 };
@@ -160,9 +168,9 @@ inline bool nt_acts_loads(const DevProblem &p, int elem_bytes) {
 enum KernelId { K_BAND = 0, K_SOFTMAX = 1, K_DP = 2, K_GRAD = 3, K_SETUP = 4, K_JOINT_FWD = 5, K_JOINT_BWD = 6,
                 K_JOINT_RED = 7, K_CHASE = 8, K_COUNT = 9 };
 
-// lpb / lpe (may be null): zero their 64 pad entries either side of [0, n)
+// lp (may be null): zero its 64 pad entries either side of [0, n)
 hipError_t launch_setup(const int *T, const int *S, int B, int64_t *row_off, int64_t *col_off, int *col_b,
-                        double *lpb, double *lpe, int64_t n, hipStream_t stream);
+                        Lp *lp, int64_t n, hipStream_t stream);
 // Device-resident lengths: lattice offsets, column map, validation and the DynWords in one launch (B workgroups).
 struct DynSetupArgs {
     const int *T;
@@ -179,8 +187,7 @@ struct DynSetupArgs {
     int64_t *row_off;
     int64_t *col_off;
     int *col_b;
-    double *lpb;        // lp arrays: their 64 entries either side of [0, rows) are zeroed
-    double *lpe;
+    Lp *lp;             // lp array: its 64 entries either side of [0, rows) are zeroed
     DynWords *dyn;
     int *status_host;   // device address of the caller's host-mapped status word, or nullptr
 };
@@ -197,15 +204,20 @@ hipError_t launch_mask_state(const DevProblem &p, double *alpha, double *beta, h
 hipError_t launch_dp(const DevProblem &p, int S_max, int with_beta, float *costs, hipStream_t stream);
 
 // The chase launch (mrnnt_chase.hip): log-softmax and alpha / beta recursion in one launch, the recursion consuming
-// columns as they are published. Ready flags: `cols` words for alpha, then `cols` for beta, zeroed before every launch.
+// columns as they are published. Ready flags: `cols` 64-bit words for alpha, then `cols` for beta, tagged with the
+// launch's epoch.
 struct ChaseArgs {
-    unsigned *flags;
-    int64_t cols;  // the flag stride between the directions
+    unsigned long long *flags;
+    int64_t cols;              // the flag stride between the directions
+    int64_t slots;             // of the production order (chase_slots)
+    unsigned long long epoch;  // fresh per call (never 0)
+    int probe;                 // development build only (tuning().chase_probe): 1 no recursion, 2 no hand-off either,
+                               // 3 recursion without waiting, 4 recursion alone without waiting
 };
 // the log-softmax body the chase launch has for this problem, -1 for none (f32 rows of <= 256 vectors only)
 int chase_body(const DevProblem &p, int elem);
-int64_t chase_grid(const DevProblem &p, int T_max, int with_beta);
-hipError_t launch_chase(const DevProblem &p, const ChaseArgs &c, int elem, int S_max, int T_max, int with_beta,
+int64_t chase_slots(const DevProblem &p, int T_max, int with_beta);
+hipError_t launch_chase(const DevProblem &p, const ChaseArgs &c, int elem, int S_max, int with_beta, int producers,
                         float *costs, hipStream_t stream);
 hipError_t launch_grad(const DevProblem &p, int elem, const float *scale, void *grads, int grid, hipStream_t stream);
 hipError_t launch_count_live(const DevProblem &p, unsigned long long *count, hipStream_t stream);

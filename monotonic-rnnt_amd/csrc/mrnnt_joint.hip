@@ -416,8 +416,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     if (q.valid && half == 0) {
         const double den = -(double)mn - log_row_sum(sum);
         p.den[q.row] = (float)den;
-        p.lpb[q.row] = (double)zb + den;
-        p.lpe[q.row] = (q.lab >= 0 ? (double)ze : (q.lab == -2 ? __builtin_nan("") : 0.0)) + den;
+        p.lp[q.row] = Lp{(double)zb + den, (q.lab >= 0 ? (double)ze : (q.lab == -2 ? __builtin_nan("") : 0.0)) + den};
     }
 }
 

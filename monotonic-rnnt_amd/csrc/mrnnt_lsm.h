@@ -8,15 +8,15 @@
 
 namespace mrnnt {
 
-// Per-row outputs of the pass. WT (the chase launch, mrnnt_chase.hip): write-through stores (`sc1`, agent scope), the
+// Per-row lp output of the pass. WT (the chase launch, mrnnt_chase.hip): a 16-byte write-through store (`sc1`), the
 // producer half of a hand-off to workgroups of the same launch on other XCDs (cdna_hip_programming.md Guideline 16,
-// R1); otherwise plain stores, read by later launches.
-template <bool WT, class T>
-__device__ __forceinline__ void st(T *ptr, T v) {
+// R1); otherwise a plain store, read by later launches. (den is read by later launches only: plain either way.)
+template <bool WT>
+__device__ __forceinline__ void st_lp(const DevProblem &p, int64_t row, Lp v) {
     if constexpr (WT)
-        store_wt(ptr, v);
+        store_lp_wt(lp_rsrc(p), (unsigned)(row * (int64_t)sizeof(Lp)), v);
     else
-        *ptr = v;
+        p.lp[row] = v;
 }
 
 // rows of the column that are not reduced: finite lp (the recursion reads them, masked) and den (the gradient's
@@ -25,9 +25,8 @@ template <bool WT>
 __device__ __forceinline__ void zero_fill_outside_band(const DevProblem &p, int64_t rowc, int S, int lo, int hi) {
     for (int s = threadIdx.x; s <= S; s += blockDim.x)
         if (s < lo || s > hi) {
-            st<WT>(&p.lpb[rowc + s], 0.0);
-            st<WT>(&p.lpe[rowc + s], 0.0);
-            st<WT>(&p.den[rowc + s], 0.0f);
+            st_lp<WT>(p, rowc + s, Lp{0.0, 0.0});
+            p.den[rowc + s] = 0.0f;
         }
 }
 
@@ -37,10 +36,8 @@ __device__ __forceinline__ void zero_fill_outside_band(const DevProblem &p, int6
 __device__ __forceinline__ void zero_lp_pads(const DevProblem &p) {
     if (blockIdx.x == 0 && threadIdx.x < 64) {
         const int i = threadIdx.x;
-        p.lpb[i - 64] = 0.0;
-        p.lpe[i - 64] = 0.0;
-        p.lpb[p.num_rows + i] = 0.0;
-        p.lpe[p.num_rows + i] = 0.0;
+        p.lp[i - 64] = Lp{0.0, 0.0};
+        p.lp[p.num_rows + i] = Lp{0.0, 0.0};
     }
 }
 
@@ -142,9 +139,8 @@ __device__ __forceinline__ void lean_column(const DevProblem &p, const ColRef &k
             if (lane < nrow) {
                 const int64_t row = rowc + s + lane;
                 const double den = -(double)em - log_row_sum(es);
-                st<WT>(&p.den[row], (float)den);
-                st<WT>(&p.lpb[row], (double)ezb + den);
-                st<WT>(&p.lpe[row], (double)eze + den);
+                p.den[row] = (float)den;
+                st_lp<WT>(p, row, Lp{(double)ezb + den, (double)eze + den});
             }
         }
         return;  // next column
@@ -231,9 +227,8 @@ __device__ __forceinline__ void lean_column(const DevProblem &p, const ColRef &k
         if (lane < nrow) {
             const int64_t row = rowc + s + lane;
             const double den = -(double)em - log_row_sum(es);
-            st<WT>(&p.den[row], (float)den);
-            st<WT>(&p.lpb[row], (double)ezb + den);
-            st<WT>(&p.lpe[row], (double)eze + den);
+            p.den[row] = (float)den;
+            st_lp<WT>(p, row, Lp{(double)ezb + den, (double)eze + den});
         }
     }
 }
@@ -326,9 +321,8 @@ __device__ __forceinline__ void row16_column(const DevProblem &p, const ColRef &
             if (ok[r] && l16 == 0) {
                 const int64_t row = rowc + s0 + 4 * r + g;
                 const double den = -(double)m - log_row_sum(acc);
-                st<WT>(&p.den[row], (float)den);
-                st<WT>(&p.lpb[row], (double)zb[r] + den);
-                st<WT>(&p.lpe[row], (double)ze[r] + den);
+                p.den[row] = (float)den;
+                st_lp<WT>(p, row, Lp{(double)zb[r] + den, (double)ze[r] + den});
             }
         }
     }

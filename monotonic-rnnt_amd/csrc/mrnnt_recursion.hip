@@ -39,12 +39,11 @@ __device__ __forceinline__ void alpha_pass(const DevProblem &p, int b, float *__
 #pragma unroll
     for (int d = 0; d < D; ++d) {
         const int tt = min(d, T - 1);
-        const double *rb = p.lpb + r0 + (int64_t)tt * W + s0;
-        const double *re = p.lpe + r0 + (int64_t)tt * W + s0 - 1;
+        const Lp *rl = p.lp + r0 + (int64_t)tt * W + s0;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            pb[d][k] = rb[k];
-            pe[d][k] = re[k];
+            pb[d][k] = rl[k].b;
+            pe[d][k] = rl[k - 1].e;
         }
         mn[d] = band ? p.min_s[c0 + tt] : 0;
         mx[d] = band ? p.max_s[c0 + tt] : S;
@@ -76,12 +75,11 @@ __device__ __forceinline__ void alpha_pass(const DevProblem &p, int b, float *__
             }
             if (NW > 1 && lane == 63) xb[t & 1][wave] = na[K - 1];
             const int tn = min(t + D, T - 1);
-            const double *rb = p.lpb + r0 + (int64_t)tn * W + s0;
-            const double *re = p.lpe + r0 + (int64_t)tn * W + s0 - 1;
+            const Lp *rl = p.lp + r0 + (int64_t)tn * W + s0;
 #pragma unroll
             for (int k = 0; k < K; ++k) {
-                pb[d][k] = rb[k];
-                pe[d][k] = re[k];
+                pb[d][k] = rl[k].b;
+                pe[d][k] = rl[k - 1].e;
             }
             mn[d] = band ? p.min_s[c0 + tn] : 0;
             mx[d] = band ? p.max_s[c0 + tn] : S;
@@ -116,12 +114,11 @@ __device__ __forceinline__ void beta_pass(const DevProblem &p, int b, double (*x
 #pragma unroll
     for (int d = 0; d < D; ++d) {
         const int tt = max(T - 1 - d, 0);
-        const double *rb = p.lpb + r0 + (int64_t)tt * W + s0;
-        const double *re = p.lpe + r0 + (int64_t)tt * W + s0;
+        const Lp *rl = p.lp + r0 + (int64_t)tt * W + s0;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            pb[d][k] = rb[k];
-            pe[d][k] = re[k];
+            pb[d][k] = rl[k].b;
+            pe[d][k] = rl[k].e;
         }
         mn[d] = (band && tt > 0) ? p.min_s[c0 + tt - 1] : 0;
         mx[d] = (band && tt > 0) ? p.max_s[c0 + tt - 1] : S;
@@ -159,12 +156,11 @@ __device__ __forceinline__ void beta_pass(const DevProblem &p, int b, double (*x
             }
             if (NW > 1 && lane == 0) xb[t & 1][wave] = nb[0];
             const int tn = max(t - D, 0);
-            const double *rb = p.lpb + r0 + (int64_t)tn * W + s0;
-            const double *re = p.lpe + r0 + (int64_t)tn * W + s0;
+            const Lp *rl = p.lp + r0 + (int64_t)tn * W + s0;
 #pragma unroll
             for (int k = 0; k < K; ++k) {
-                pb[d][k] = rb[k];
-                pe[d][k] = re[k];
+                pb[d][k] = rl[k].b;
+                pe[d][k] = rl[k].e;
             }
             mn[d] = (band && tn > 0) ? p.min_s[c0 + tn - 1] : 0;
             mx[d] = (band && tn > 0) ? p.max_s[c0 + tn - 1] : S;

@@ -13,23 +13,21 @@ Tuning &tuning() {
 
 // row_off[b] = sum_{b'<b} T_b'(S_b'+1), col_off[b] = sum_{b'<b} T_b' -- one wave, any B (reference
 // gpu_workspace_manager.h:256-329 computes these on the host and copies them with blocking memcpys).
-// It also zeroes the 64 lp entries either side of the lp arrays: the recursion's in-band cell s = 0 of
-// utterance 0 adds lpe[-1] to its -inf predecessor, and a NaN / +inf left in the (reused) workspace there
-// would turn alpha(0, 0) into NaN (then -inf through fmax in the next LSE: an infinite cost).
+// It also zeroes the 64 lp entries either side of the lp array: rows just outside [0, N) that recursion lanes
+// outside an utterance's column read, and a NaN / +inf left in the (reused) workspace there must not reach a kept
+// cell (it would turn alpha(0, 0) into NaN, then -inf through fmax in the next LSE: an infinite cost).
 __global__ __launch_bounds__(64) void setup_kernel(const int *__restrict__ T, const int *__restrict__ S, int B,
                                                    int64_t *__restrict__ row_off, int64_t *__restrict__ col_off,
-                                                   double *__restrict__ lpb, double *__restrict__ lpe, int64_t n) {
+                                                   Lp *__restrict__ lp, int64_t n) {
     const int lane = threadIdx.x;
     int64_t carry_r = 0, carry_c = 0;
     if (lane == 0) {
         row_off[0] = 0;
         col_off[0] = 0;
     }
-    if (lpb) {
-        lpb[lane - 64] = 0.0;
-        lpe[lane - 64] = 0.0;
-        lpb[n + lane] = 0.0;
-        lpe[n + lane] = 0.0;
+    if (lp) {
+        lp[lane - 64] = Lp{0.0, 0.0};
+        lp[n + lane] = Lp{0.0, 0.0};
     }
     for (int base = 0; base < B; base += 64) {
         const int b = base + lane;
@@ -105,8 +103,8 @@ __global__ __launch_bounds__(256) void col_map_kernel(const int *__restrict__ T,
 }
 
 hipError_t launch_setup(const int *T, const int *S, int B, int64_t *row_off, int64_t *col_off, int *col_b,
-                        double *lpb, double *lpe, int64_t n, hipStream_t stream) {
-    setup_kernel<<<1, 64, 0, stream>>>(T, S, B, row_off, col_off, lpb, lpe, n);
+                        Lp *lp, int64_t n, hipStream_t stream) {
+    setup_kernel<<<1, 64, 0, stream>>>(T, S, B, row_off, col_off, lp, n);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     col_map_kernel<<<B, 256, 0, stream>>>(T, col_off, col_b);
@@ -240,13 +238,11 @@ __global__ __launch_bounds__(256) void setup_dyn_kernel(DynSetupArgs a) {
             __hip_atomic_store(a.status_host, (int)RNNT_STATUS_INVALID_VALUE, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    if (threadIdx.x < 64 && a.lpb) {  // the recursion's reads just outside [0, N) (see setup_kernel)
+    if (threadIdx.x < 64 && a.lp) {  // the recursion's reads just outside [0, N) (see setup_kernel)
         const int i = threadIdx.x;
         const int64_t end = fail ? 0 : R;
-        a.lpb[i - 64] = 0.0;
-        a.lpe[i - 64] = 0.0;
-        a.lpb[end + i] = 0.0;
-        a.lpe[end + i] = 0.0;
+        a.lp[i - 64] = Lp{0.0, 0.0};
+        a.lp[end + i] = Lp{0.0, 0.0};
     }
 }
 
