@@ -989,6 +989,7 @@ __attribute__((visibility("default"))) int mrnnt_tune(const char *key, int value
     else if (!std::strcmp(key, "nt_load")) slot = &t.nt_load;
     else if (!std::strcmp(key, "occ_skip")) slot = &t.occ_skip;
     else if (!std::strcmp(key, "joint_nbuf")) slot = &t.joint_nbuf;
+    else if (!std::strcmp(key, "joint_nw")) slot = &t.joint_nw;
     if (!slot) return -1;
     const int prev = *slot;
     if (value >= 0) *slot = value;

@@ -123,6 +123,7 @@ struct Tuning {
                                   // 2 by size (nt_acts_loads)
     int occ_skip = 1;             // gradient: no acts read for rows with log-occupancy < kDeadLogOcc
     int joint_nbuf = 2;           // fused joint kernels: LDS buffers for the weight chunks (2 or 3)
+    int joint_nw = 8;             // fused joint kernels: waves per workgroup (8: one workgroup per CU; 4: two)
     int joint_reduce_sparse = 0;  // joint d_enc/d_pred reduce: 0 row-parallel kernel below 4 live rows per column,
                                   // 1 always frame by frame, 2 always row-parallel
     int dp_halo = 2;              // alpha/beta: halo recursion (one barrier per 8 steps, 8 / 16-step prefetch

@@ -697,6 +697,11 @@ static hipError_t launch_kh(const DevProblem &p, const JointArgs &j, bool bwd, h
     if constexpr (kVariants) {  // three DMA buffers: development build only (joint_nbuf = 3)
         if (tuning().joint_nbuf >= 3 && 3 * tile + bias <= 160 * 1024)
             return launch_knw<KS, 3, 8>(p, j, bwd, 3 * tile + bias, stream);
+        // 4-wave workgroups, two per CU when their LDS fits twice (joint_nw = 4): each wave still shares its SIMD
+        // with one other, now of ANOTHER workgroup, which started at another time -- one's activation build can
+        // overlap the other's MFMAs; 128 rows share each W chunk
+        if (tuning().joint_nw == 4 && WTile<KS>::NI % 4 == 0 && 2 * (2 * tile + bias) <= 160 * 1024)
+            return launch_knw<KS, 2, 4>(p, j, bwd, 2 * tile + bias, stream);
     }
     if (2 * tile + bias <= 160 * 1024) return launch_knw<KS, 2, 8>(p, j, bwd, 2 * tile + bias, stream);
     return hipErrorInvalidValue;

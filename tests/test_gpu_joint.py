@@ -235,3 +235,17 @@ def test_joint_alignment_restricted(jop, dev, k):
     close(dp, dp_r, name="d_pred")
     close(dw, dw_r, name="d_weight")
     close(db, db_r, name="d_bias")
+
+
+@pytest.mark.parametrize("H,V", [(512, 256), (256, 1000), (128, 64)])
+def test_joint_four_wave_workgroups_bit_identical(dev, H, V):
+    """joint_nw = 4 (development build): two 4-wave workgroups per CU instead of one of 8 -- the same tiles, chunk
+    order and epilogues per wave, so the same bits."""
+    import monotonic_rnnt_joint as jm
+    enc, pred, w, bias, labels, T, S = make_case(7 + H, 5, (10, 60), 20, H, V)
+    ref = run_joint(jm, dev, enc, pred, w, bias, labels, T, S)
+    with knobs(joint_nw=4):
+        got = run_joint(jm, dev, enc, pred, w, bias, labels, T, S)
+    assert np.array_equal(ref[0], got[0])
+    for a, b in zip(ref[1:], got[1:]):
+        assert torch.equal(a, b)
