@@ -61,7 +61,10 @@ typedef struct mrnnt_problem {
     /* --- version 4 --- */
     const void *lattice;     /* optional: device copy of mrnnt_lattice_host's output for these lengths. The lattice
                                 offsets then come from it and mrnnt_forward launches no setup kernel (a caller that
-                                repeats shapes uploads it once); NULL = built on the device in every forward */
+                                repeats shapes uploads it once); NULL = built on the device in every forward. The
+                                workspace then holds no offsets of its own: pass the same lattice to every later
+                                call on that workspace (mrnnt_backward, mrnnt_read_*, mrnnt_grad_live_rows), and
+                                only a lattice built from these lengths (it is not checked against them) */
     /* --- version 6 --- */
     int grad_scale_broadcast; /* 1: grad_scale[0] scales every utterance (a stride-0 upstream gradient, e.g. the
                                 backward of costs.sum(): no copy into a [B] vector); 0: grad_scale[b] */
