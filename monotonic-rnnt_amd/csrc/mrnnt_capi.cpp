@@ -990,6 +990,9 @@ __attribute__((visibility("default"))) int mrnnt_tune(const char *key, int value
     else if (!std::strcmp(key, "occ_skip")) slot = &t.occ_skip;
     else if (!std::strcmp(key, "joint_nbuf")) slot = &t.joint_nbuf;
     else if (!std::strcmp(key, "joint_nw")) slot = &t.joint_nw;
+    else if (!std::strcmp(key, "joint_mfma")) slot = &t.joint_mfma;
+    else if (!std::strcmp(key, "joint_bwd_mfma")) slot = &t.joint_bwd_mfma;
+    else if (!std::strcmp(key, "joint_ring")) slot = &t.joint_ring;
     if (!slot) return -1;
     const int prev = *slot;
     if (value >= 0) *slot = value;

@@ -40,7 +40,9 @@ __device__ __forceinline__ float bf16_hi(unsigned u) { return __uint_as_float(u 
 
 
 // tanh(x) = sign(x) (1 - e) / (1 + e), e = exp(-2|x|) (v_exp_f32 + v_rcp_f32, |error| ~ 1e-7), two at a time on
-// packed f32 (v_pk_*): build_act runs before the MFMA loop, where packing halves its VALU
+// packed f32 (v_pk_*): the build runs before the MFMA loop, where packing halves its VALU. (The form
+// 1 - 2 / (1 + e^{2x}) has 39 % fewer non-transcendental VALU and measured 0.1-0.2 ms slower at H = 512:
+// profiles/r02/joint/joint_tanh_rcp_ab.json.)
 __device__ __forceinline__ f2 fast_tanh2(f2 x) {
     const f2 ax = {fabsf(x.x), fabsf(x.y)};
     const f2 t = ax * (f2){-2.0f * kLog2e, -2.0f * kLog2e};
@@ -168,21 +170,20 @@ __device__ __forceinline__ RowPos row_pos(const DevProblem &p, const JointArgs &
     return q;
 }
 
-// B operand: h = bf16(tanh(enc[b,t] + pred[b,s])) for k = 16 ks + 8 half + [0, 8); optionally stored to Hact.
-// Invalid lanes (past the end of the list) read row 0 and zero the result: no branch around the loads (a
-// branch per load makes hipcc wait vmcnt(0) after each one).
-template <int KS, bool STORE>
-__device__ __forceinline__ void build_act(const JointArgs &j, const RowPos &q, int half, int64_t i,
-                                          bf16x8 (&bfr)[KS]) {
-    constexpr int H = 16 * KS;
+// B operand of one row: h = bf16(tanh(enc[b,t] + pred[b,s])) for k = k0 + KSTEP ks + [0, 8), ks < NK; optionally
+// stored to Hact. Invalid lanes (past the end of the list) read row 0 and zero the result: no branch around the loads
+// (a branch per load makes hipcc wait vmcnt(0) after each one).
+template <int NK, int KSTEP, bool STORE>
+__device__ __forceinline__ void build_row(const JointArgs &j, const RowPos &q, int k0, int64_t i, bf16x8 *bfr) {
+    constexpr int H = NK * KSTEP;
     const bool v = q.valid;
-    const unsigned short *er = j.enc + (v ? (int64_t)q.b * j.enc_sb + (int64_t)q.t * H : 0) + 8 * half;
-    const unsigned short *pr = j.pred + (v ? (int64_t)q.b * j.pred_sb + (int64_t)q.s * H : 0) + 8 * half;
+    const unsigned short *er = j.enc + (v ? (int64_t)q.b * j.enc_sb + (int64_t)q.t * H : 0) + k0;
+    const unsigned short *pr = j.pred + (v ? (int64_t)q.b * j.pred_sb + (int64_t)q.s * H : 0) + k0;
     const float keep = v ? 1.0f : 0.0f;
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-        const u4 ev = *reinterpret_cast<const u4 *>(er + 16 * ks);
-        const u4 pv = *reinterpret_cast<const u4 *>(pr + 16 * ks);
+    for (int ks = 0; ks < NK; ++ks) {
+        const u4 ev = *reinterpret_cast<const u4 *>(er + KSTEP * ks);
+        const u4 pv = *reinterpret_cast<const u4 *>(pr + KSTEP * ks);
         bf16x8 h;
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
@@ -191,16 +192,23 @@ __device__ __forceinline__ void build_act(const JointArgs &j, const RowPos &q, i
             h[2 * w] = (__bf16)y.x;
             h[2 * w + 1] = (__bf16)y.y;
         }
-        if (STORE && v) *reinterpret_cast<bf16x8 *>(j.Hact + i * j.hact_ld + 16 * ks + 8 * half) = h;
+        if (STORE && v) *reinterpret_cast<bf16x8 *>(j.Hact + i * j.hact_ld + KSTEP * ks + k0) = h;
         bfr[ks] = h;
     }
     if (STORE && v) {  // columns past H: a ones column (dbias from the dweight GEMM), then zeros
-        for (int64_t c = H + 8 * half; c < j.hact_ld; c += 16) {
+        for (int64_t c = H + k0; c < j.hact_ld; c += KSTEP) {
             bf16x8 e = {};
             if (c == H) e[0] = (__bf16)1.0f;
             *reinterpret_cast<bf16x8 *>(j.Hact + i * j.hact_ld + c) = e;
         }
     }
+}
+
+// 32x32x16 tile: lane l holds k = 16 ks + 8 (l >> 5) + [0, 8) of row l & 31
+template <int KS, bool STORE>
+__device__ __forceinline__ void build_act(const JointArgs &j, const RowPos &q, int half, int64_t i,
+                                          bf16x8 (&bfr)[KS]) {
+    build_row<KS, 16, STORE>(j, q, 8 * half, i, bfr);
 }
 
 // W chunk (32 vocabulary rows x H bf16) in LDS: unpadded, the 16-byte piece p of row r stored at piece
@@ -253,6 +261,53 @@ struct WTile {
         for (int ks = 0; ks < KS; ++ks) {
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks % D], bfr[ks], acc, 0, 0, 0);
             if (ks + D < KS) a[ks % D] = rd(ks + D);
+        }
+        return acc;
+    }
+};
+
+// The same W chunk as four 16x16 output tiles per wave (v_mfma_f32_16x16x32_bf16: at equal cycles per FLOP the
+// 16x16 shape holds a higher clock than 32x32 on random operands, MI355X_MICROARCH.md 'DVFS give-back' item 7).
+// A wave's 32 rows are two row tiles rt (rows 16 rt + (l & 15)); lane l holds k = 32 kk + 8 (l >> 4) + [0, 8) of
+// both rows (B), and of W row 16 vt + (l & 15) (A: one ds_read_b128 feeds the MFMAs of both row tiles). Output
+// d[vt][rt][r] = z(row 16 rt + (l & 15), vocab 32 c + 16 vt + 4 (l >> 4) + r).
+template <int KS>
+struct WTile16 {
+    static constexpr int H = 16 * KS;
+    static constexpr int K32 = KS / 2;  // MFMA k-steps
+    struct Acc {
+        f4 d[2][2];
+    };
+
+    // piece 4 kk + g of row 16 vt + c16 sits at (4 kk + g) ^ c16 (the WTile swizzle, c16 = row & 15): with
+    // kk = 4 m + kk', that is 16 m + ((4 kk' + g) ^ c16): four base addresses, m and vt in the immediate offset
+    template <int RING = 4>
+    __device__ static __forceinline__ Acc mma(const unsigned short *wbuf, const bf16x8 (&bfr)[2][K32], int lane) {
+        const int c16 = lane & 15, g = lane >> 4;
+        const unsigned short *row = wbuf + c16 * H;
+        const unsigned short *base[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) base[k] = row + 8 * ((4 * k + g) ^ c16);
+        constexpr int NR = 2 * K32;  // A fragments per chunk, in (kk, vt) order
+        auto rd = [&](int n) {
+            const int kk = n >> 1, vt = n & 1;
+            return *reinterpret_cast<const bf16x8 *>(base[kk & 3] + 128 * (kk >> 2) + 16 * H * vt);
+        };
+        constexpr int D = NR < RING ? NR : RING;
+        bf16x8 a[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d) a[d] = rd(d);
+        Acc acc;
+#pragma unroll
+        for (int vt = 0; vt < 2; ++vt)
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt) acc.d[vt][rt] = (f4){0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int n = 0; n < NR; ++n) {
+            const int kk = n >> 1, vt = n & 1;
+            acc.d[vt][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[n % D], bfr[0][kk], acc.d[vt][0], 0, 0, 0);
+            acc.d[vt][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[n % D], bfr[1][kk], acc.d[vt][1], 0, 0, 0);
+            if (n + D < NR) a[n % D] = rd(n + D);
         }
         return acc;
     }
@@ -314,9 +369,9 @@ __device__ __forceinline__ float max3(float a, float b, float c) {
 // on every wave (0 forward, 4 backward; -1 = unknown): the wait before chunk c leaves the later DMAs and the
 // stores of the epilogues issued after chunk c's DMA in flight (vector memory completes in issue order).
 // (Staggering the two waves of a SIMD by one epilogue, and three buffers, both measured slower: registers.)
-template <int KS, int NB, int NW, class Epi>
-__device__ __forceinline__ void chunk_loop(const JointArgs &j, int V, unsigned short *wsh, const bf16x8 (&bfr)[KS],
-                                           int lane, int S, Epi &&epi) {
+template <int KS, int NB, int NW, class Mma, class Epi>
+__device__ __forceinline__ void chunk_loop_with(const JointArgs &j, int V, unsigned short *wsh, int S, Mma &&mma,
+                                                Epi &&epi) {
     using WT = WTile<KS>;
     constexpr int NPW = WT::NI / NW;  // DMA instructions per wave per chunk
     const int nch = (V + 31) / 32;
@@ -335,9 +390,17 @@ __device__ __forceinline__ void chunk_loop(const JointArgs &j, int V, unsigned s
         }
         __builtin_amdgcn_s_barrier();
         if (c + NB - 1 < nch) WT::template stage<NW>(j, V, c + NB - 1, wsh + ((c + NB - 1) % NB) * WT::ELEMS);
-        const f32x16 acc = WT::template mma<2>(wsh + (c % NB) * WT::ELEMS, bfr, lane);
+        const auto acc = mma(wsh + (c % NB) * WT::ELEMS);
         epi(acc, c);
     }
+}
+
+template <int KS, int NB, int NW, int RG, class Epi>
+__device__ __forceinline__ void chunk_loop(const JointArgs &j, int V, unsigned short *wsh, const bf16x8 (&bfr)[KS],
+                                           int lane, int S, Epi &&epi) {
+    chunk_loop_with<KS, NB, NW>(j, V, wsh, S,
+                                [&](const unsigned short *wb) { return WTile<KS>::template mma<RG>(wb, bfr, lane); },
+                                epi);
 }
 
 // LDS: NB W tiles, then the bias padded to whole chunks
@@ -351,7 +414,7 @@ __device__ __forceinline__ float *load_bias(const JointArgs &j, int V, unsigned 
 }
 
 // two waves per SIMD: the compiler keeps each kernel within 256 registers per lane
-template <int KS, int NB, int NW>
+template <int KS, int NB, int NW, int RG>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2))) void joint_fwd_kernel(DevProblem p,
                                                                                              JointArgs j) {
     extern __shared__ __attribute__((aligned(16))) unsigned short wsh[];
@@ -368,7 +431,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const f2 l2e = {kLog2e, kLog2e};
     float m = NEG_INF_F, sum = 0.0f, zb = 0.0f, ze = 0.0f;
     bool fb = false, fe = false;
-    chunk_loop<KS, NB, NW>(j, V, wsh, bfr, lane, 0, [&](const f32x16 &acc, int c) {
+    chunk_loop<KS, NB, NW, RG>(j, V, wsh, bfr, lane, 0, [&](const f32x16 &acc, int c) {
         f2 z[8];
         logits2(acc, bias, c, half, z);
         float cm = fmaxf(z[0].x, z[0].y);
@@ -420,7 +483,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     }
 }
 
-template <int KS, int NB, int NW>
+template <int KS, int NB, int NW, int RG>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2))) void joint_bwd_kernel(DevProblem p,
                                                                                              JointArgs j) {
     extern __shared__ __attribute__((aligned(16))) unsigned short wsh[];
@@ -446,7 +509,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const bool leave = vec_out && __ballot(!q.valid) == 0;
     unsigned short *grow = j.G + (q.valid ? i : 0) * V;
     const f2 l2e = {kLog2e, kLog2e}, c2 = {rc.c2, rc.c2}, sc2 = {sc, sc};
-    chunk_loop<KS, NB, NW>(j, V, wsh, bfr, lane, leave ? 4 : -1, [&](const f32x16 &acc, int c) {
+    chunk_loop<KS, NB, NW, RG>(j, V, wsh, bfr, lane, leave ? 4 : -1, [&](const f32x16 &acc, int c) {
         f2 g[8];
         logits2(acc, bias, c, half, g);
 #pragma unroll
@@ -484,6 +547,196 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
             if (mine) grow[rc.lab] = IoBF16::from_f((gl - rc.ce) * sc);
         }
     });
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// the same passes on the 16x16x32 tile (WTile16): each lane carries two rows (row tiles rt = 0, 1) and 8 of the
+// chunk's 32 vocabulary entries of each; the four lane groups g = l >> 4 hold disjoint vocabulary and merge once.
+
+// x[i] for a per-lane i in [0, 8): a 3-level select tree (v_cndmask; never an indexed register array)
+__device__ __forceinline__ float pick8(const float (&x)[8], int i) {
+    const bool b0 = i & 1, b1 = i & 2, b2 = i & 4;
+    const float a0 = b0 ? x[1] : x[0], a1 = b0 ? x[3] : x[2], a2 = b0 ? x[5] : x[4], a3 = b0 ? x[7] : x[6];
+    const float c0 = b1 ? a1 : a0, c1 = b1 ? a3 : a2;
+    return b2 ? c1 : c0;
+}
+
+// vocabulary offset jj (0..31) of a chunk: held by lane group (jj >> 2) & 3 at index 4 (jj >> 4) + (jj & 3)
+__device__ __forceinline__ int pick8_index(int jj) { return 4 * (jj >> 4) + (jj & 3); }
+
+// z = acc + bias for row tile rt: x[4 vt + r] = vocabulary 32 c + 16 vt + 4 g + r (past V: -inf through the bias)
+template <int KS>
+__device__ __forceinline__ void logits8(const typename WTile16<KS>::Acc &acc, const f4 (&bv)[2], int rt,
+                                        float (&x)[8]) {
+#pragma unroll
+    for (int vt = 0; vt < 2; ++vt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[4 * vt + r] = acc.d[vt][rt][r] + bv[vt][r];
+}
+
+template <int KS, int NB, int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2))) void joint_fwd16_kernel(
+    DevProblem p, JointArgs j) {
+    extern __shared__ __attribute__((aligned(16))) unsigned short wsh[];
+    constexpr int K32 = KS / 2;
+    if ((int64_t)blockIdx.x * (32 * NW) >= list_len(j)) return;  // whole workgroup past a shorter list
+    const int lane = threadIdx.x & 63, c16 = lane & 15, g = lane >> 4;
+    const int64_t i0 = (int64_t)blockIdx.x * (32 * NW) + (threadIdx.x >> 6) * 32 + c16;
+    const RowPos q[2] = {row_pos(p, j, i0), row_pos(p, j, i0 + 16)};
+    const int V = p.V, blank = p.blank;
+    const float *bias = load_bias<KS, NB>(j, V, wsh);
+    __syncthreads();
+    bf16x8 bfr[2][K32];
+    build_row<K32, 32, false>(j, q[0], 8 * g, i0, bfr[0]);
+    build_row<K32, 32, false>(j, q[1], 8 * g, i0 + 16, bfr[1]);
+
+    float m[2] = {NEG_INF_F, NEG_INF_F}, sum[2] = {0.0f, 0.0f}, zb[2] = {0.0f, 0.0f}, ze[2] = {0.0f, 0.0f};
+    bool fb = false, fe[2] = {false, false};
+    chunk_loop_with<KS, NB, NW>(
+        j, V, wsh, 0, [&](const unsigned short *wb) { return WTile16<KS>::template mma<4>(wb, bfr, lane); },
+        [&](const typename WTile16<KS>::Acc &acc, int c) {
+            const f4 bv[2] = {*reinterpret_cast<const f4 *>(bias + 32 * c + 4 * g),
+                              *reinterpret_cast<const f4 *>(bias + 32 * c + 16 + 4 * g)};
+            const int jb = blank - 32 * c;  // wave-uniform: one chunk holds the blank
+            const bool hb = jb >= 0 && jb < 32 && ((jb >> 2) & 3) == g;
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt) {
+                float z[8];
+                logits8<KS>(acc, bv, rt, z);
+                const float cm = max3(max3(z[0], z[1], z[2]), max3(z[3], z[4], z[5]), fmaxf(z[6], z[7]));
+                const float mn = fmaxf(m[rt], cm);
+                const float mr = (mn == NEG_INF_F) ? 0.0f : mn;
+                const float nb = -mr * kLog2e;
+                float s0 = 0.0f, s1 = 0.0f;
+#pragma unroll
+                for (int k = 0; k < 8; k += 2) {
+                    s0 += fast_exp2(fmaf(z[k], kLog2e, nb));
+                    s1 += fast_exp2(fmaf(z[k + 1], kLog2e, nb));
+                }
+                sum[rt] = sum[rt] * fast_exp2((m[rt] - mr) * kLog2e) + (s0 + s1);
+                m[rt] = mn;
+                if (jb >= 0 && jb < 32) {
+                    const float x = pick8(z, pick8_index(jb));
+                    if (hb) zb[rt] = x;
+                }
+                const int jl = q[rt].lab - 32 * c;
+                const bool mine = q[rt].lab >= 0 && jl >= 0 && jl < 32 && ((jl >> 2) & 3) == g;
+                if (__ballot(mine)) {  // most chunks hold some lane's label; skip the select when none does
+                    const float x = pick8(z, pick8_index(jl & 31));
+                    if (mine) {
+                        ze[rt] = x;
+                        fe[rt] = true;
+                    }
+                }
+            }
+            if (hb) fb = true;
+        });
+    // merge the four lane groups (same rows, disjoint vocabulary)
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+        bool fbr = fb;
+#pragma unroll
+        for (int off = 16; off <= 32; off <<= 1) {
+            const float m2 = __shfl_xor(m[rt], off), s2 = __shfl_xor(sum[rt], off);
+            const float zb2 = __shfl_xor(zb[rt], off), ze2 = __shfl_xor(ze[rt], off);
+            const int fb2 = __shfl_xor((int)fbr, off), fe2 = __shfl_xor((int)fe[rt], off);
+            const float mn = fmaxf(m[rt], m2);
+            const float mr = (mn == NEG_INF_F) ? 0.0f : mn;
+            sum[rt] = sum[rt] * fast_exp2((m[rt] - mr) * kLog2e) + s2 * fast_exp2((m2 - mr) * kLog2e);
+            m[rt] = mn;
+            if (!fbr && fb2) {
+                zb[rt] = zb2;
+                fbr = true;
+            }
+            if (!fe[rt] && fe2) {
+                ze[rt] = ze2;
+                fe[rt] = true;
+            }
+        }
+        const RowPos &qr = q[rt];
+        if (qr.valid && g == 0) {
+            const double den = -(double)m[rt] - log_row_sum(sum[rt]);
+            p.den[qr.row] = (float)den;
+            p.lp[qr.row] =
+                Lp{(double)zb[rt] + den, (qr.lab >= 0 ? (double)ze[rt] : (qr.lab == -2 ? __builtin_nan("") : 0.0)) + den};
+        }
+    }
+}
+
+template <int KS, int NB, int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2))) void joint_bwd16_kernel(
+    DevProblem p, JointArgs j) {
+    extern __shared__ __attribute__((aligned(16))) unsigned short wsh[];
+    constexpr int K32 = KS / 2;
+    const int lane = threadIdx.x & 63, c16 = lane & 15, g = lane >> 4;
+    const int64_t i0 = (int64_t)blockIdx.x * (32 * NW) + (threadIdx.x >> 6) * 32 + c16;
+    const RowPos q[2] = {row_pos(p, j, i0), row_pos(p, j, i0 + 16)};
+    RowCoef rc[2];
+    float sc[2];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+        const RowPos &qr = q[rt];
+        const int64_t i = i0 + 16 * rt;
+        rc[rt] = RowCoef{0.0f, 0.0f, 0.0f, -1, false};
+        sc[rt] = 0.0f;
+        if (qr.valid) {
+            rc[rt] = row_coef(p, qr.t, qr.T, qr.S, qr.s, qr.row, p.ll[qr.b], p.labels + (int64_t)qr.b * p.label_stride);
+            sc[rt] = j.scale ? j.scale[qr.b] : 1.0f;
+            if (g == 0 && j.bt_idx) j.bt_idx[i] = (int64_t)qr.b * (j.enc_sb / j.H) + qr.t;
+            if (g == 0 && j.bs_idx) j.bs_idx[i] = (int64_t)qr.b * (j.pred_sb / j.H) + qr.s;
+        }
+    }
+    const int V = p.V, blank = p.blank;
+    const float *bias = load_bias<KS, NB>(j, V, wsh);
+    __syncthreads();
+    bf16x8 bfr[2][K32];
+    build_row<K32, 32, true>(j, q[0], 8 * g, i0, bfr[0]);
+    build_row<K32, 32, true>(j, q[1], 8 * g, i0 + 16, bfr[1]);
+
+    // exactly 4 vector stores per chunk (2 row tiles x 2 vocabulary tiles) on every wave whose lanes are all valid:
+    // leave them in flight at the barrier
+    const bool vec_out = (V & 3) == 0;
+    const bool leave = vec_out && __ballot(!(q[0].valid && q[1].valid)) == 0;
+    unsigned short *grow[2] = {j.G + (q[0].valid ? i0 : 0) * V, j.G + (q[1].valid ? i0 + 16 : 0) * V};
+    chunk_loop_with<KS, NB, NW>(
+        j, V, wsh, leave ? 4 : -1, [&](const unsigned short *wb) { return WTile16<KS>::template mma<4>(wb, bfr, lane); },
+        [&](const typename WTile16<KS>::Acc &acc, int c) {
+            const f4 bv[2] = {*reinterpret_cast<const f4 *>(bias + 32 * c + 4 * g),
+                              *reinterpret_cast<const f4 *>(bias + 32 * c + 16 + 4 * g)};
+            const int jb = blank - 32 * c;
+            const bool hb = jb >= 0 && jb < 32 && ((jb >> 2) & 3) == g;
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt) {
+                float x[8];
+                logits8<KS>(acc, bv, rt, x);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) x[k] = fast_exp2(fmaf(x[k], kLog2e, rc[rt].c2));
+                // the <= 2 corrected entries of the row are rewritten by a second (2-byte) store after the vector store
+                const int jl = rc[rt].lab - 32 * c;
+                const bool mine = rc[rt].lab >= 0 && jl >= 0 && jl < 32 && ((jl >> 2) & 3) == g;
+                float gb = 0.0f, gl = 0.0f;
+                if (jb >= 0 && jb < 32) gb = pick8(x, pick8_index(jb));
+                if (__ballot(mine)) gl = pick8(x, pick8_index(jl & 31));
+                if (q[rt].valid) {
+                    const float s = sc[rt];
+#pragma unroll
+                    for (int vt = 0; vt < 2; ++vt) {
+                        const int v0 = 32 * c + 16 * vt + 4 * g;
+                        const float e4[4] = {x[4 * vt] * s, x[4 * vt + 1] * s, x[4 * vt + 2] * s, x[4 * vt + 3] * s};
+                        if (vec_out && v0 + 3 < V) {
+                            *reinterpret_cast<uint2 *>(grow[rt] + v0) =
+                                make_uint2(IoBF16::pack2(e4[0], e4[1]), IoBF16::pack2(e4[2], e4[3]));
+                        } else {
+#pragma unroll
+                            for (int e = 0; e < 4; ++e)
+                                if (v0 + e < V) grow[rt][v0 + e] = IoBF16::from_f(e4[e]);
+                        }
+                    }
+                    if (hb) grow[rt][blank] = IoBF16::from_f((gb - rc[rt].cb) * s);
+                    if (mine) grow[rt][rc[rt].lab] = IoBF16::from_f((gl - rc[rt].ce) * s);
+                }
+            }
+        });
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -674,11 +927,16 @@ hipError_t launch_joint_reduce(const DevProblem &p, const JointArgs &j, const in
     return hipGetLastError();
 }
 
-template <int KS, int NB, int NW>
-static hipError_t launch_knw(const DevProblem &p, const JointArgs &j, bool bwd, size_t lds, hipStream_t stream) {
+// kernel of a launch shape: MF = MFMA tile (32: 32x32x16, 16: 16x16x32), RG = A-fragment ring of the 32x32 tile
+template <int KS, int NB, int NW, int MF, bool BWD, int RG>
+static hipError_t launch_knw(const DevProblem &p, const JointArgs &j, size_t lds, hipStream_t stream) {
     const int64_t blocks = (j.n + 32 * NW - 1) / (32 * NW);
     if (blocks * 64 * NW > 0xffffffffll) return hipErrorInvalidValue;  // 32-bit dispatch size in work-items
-    auto kern = bwd ? joint_bwd_kernel<KS, NB, NW> : joint_fwd_kernel<KS, NB, NW>;
+    void (*kern)(DevProblem, JointArgs);
+    if constexpr (MF == 16 && BWD) kern = joint_bwd16_kernel<KS, NB, NW>;
+    else if constexpr (MF == 16) kern = joint_fwd16_kernel<KS, NB, NW>;
+    else if constexpr (BWD) kern = joint_bwd_kernel<KS, NB, NW, RG>;
+    else kern = joint_fwd_kernel<KS, NB, NW, RG>;
     if (lds > 65536) {
         const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -688,23 +946,50 @@ static hipError_t launch_knw(const DevProblem &p, const JointArgs &j, bool bwd, 
     return hipGetLastError();
 }
 
-// One workgroup of 8 waves per CU (two per SIMD, 256 rows sharing each W chunk) with three DMA buffers when they
-// fit beside the bias in the CU's 160 KiB, else two.
-template <int KS>
-static hipError_t launch_kh(const DevProblem &p, const JointArgs &j, bool bwd, hipStream_t stream) {
+// One workgroup of 8 waves per CU (two per SIMD, 256 rows sharing each W chunk), two DMA buffers; the development
+// build adds three buffers (joint_nbuf = 3), 4-wave workgroups (joint_nw = 4) and deeper A-fragment rings
+// (joint_ring = 4 / 8) of the 32x32 tile.
+template <int KS, int MF, bool BWD>
+static hipError_t launch_kt(const DevProblem &p, const JointArgs &j, hipStream_t stream) {
     const size_t bias = sizeof(float) * ((p.V + 31) / 32 * 32);
     const size_t tile = sizeof(unsigned short) * WTile<KS>::ELEMS;
-    if constexpr (kVariants) {  // three DMA buffers: development build only (joint_nbuf = 3)
+    if constexpr (kVariants) {
         if (tuning().joint_nbuf >= 3 && 3 * tile + bias <= 160 * 1024)
-            return launch_knw<KS, 3, 8>(p, j, bwd, 3 * tile + bias, stream);
-        // 4-wave workgroups, two per CU when their LDS fits twice (joint_nw = 4): each wave still shares its SIMD
-        // with one other, now of ANOTHER workgroup, which started at another time -- one's activation build can
-        // overlap the other's MFMAs; 128 rows share each W chunk
+            return launch_knw<KS, 3, 8, MF, BWD, 2>(p, j, 3 * tile + bias, stream);
+        // 4-wave workgroups, two per CU when their LDS fits twice: each wave still shares its SIMD with one other,
+        // now of ANOTHER workgroup, which started at another time -- one's activation build can overlap the other's
+        // MFMAs; 128 rows share each W chunk
         if (tuning().joint_nw == 4 && WTile<KS>::NI % 4 == 0 && 2 * (2 * tile + bias) <= 160 * 1024)
-            return launch_knw<KS, 2, 4>(p, j, bwd, 2 * tile + bias, stream);
+            return launch_knw<KS, 2, 4, MF, BWD, 2>(p, j, 2 * tile + bias, stream);
+        if constexpr (MF == 32 && (KS == 16 || KS == 32)) {
+            if (2 * tile + bias <= 160 * 1024 && tuning().joint_ring == 4)
+                return launch_knw<KS, 2, 8, MF, BWD, 4>(p, j, 2 * tile + bias, stream);
+            if (2 * tile + bias <= 160 * 1024 && tuning().joint_ring == 8)
+                return launch_knw<KS, 2, 8, MF, BWD, 8>(p, j, 2 * tile + bias, stream);
+        }
     }
-    if (2 * tile + bias <= 160 * 1024) return launch_knw<KS, 2, 8>(p, j, bwd, 2 * tile + bias, stream);
+    if (2 * tile + bias <= 160 * 1024) return launch_knw<KS, 2, 8, MF, BWD, 2>(p, j, 2 * tile + bias, stream);
     return hipErrorInvalidValue;
+}
+
+// MFMA tile per pass: the tuned defaults only in the product library (forward 32x32x16, backward 16x16x32: the
+// backward's epilogue carries no per-row running state, and there the 16x16 tile's higher clock pays; the forward's
+// two rows of online-softmax state per lane cost more than it gains); both in the development build (joint_mfma,
+// joint_bwd_mfma). H = 640 keeps the 32x32 tile everywhere (the 16x16 one spills there: two rows' state per lane
+// beside 160 B-operand registers).
+template <int KS, bool BWD>
+static hipError_t launch_kb(const DevProblem &p, const JointArgs &j, hipStream_t stream) {
+    constexpr int kDefault = KS > 32 ? 32 : BWD ? Tuning{}.joint_bwd_mfma : Tuning{}.joint_mfma;
+    if constexpr (kVariants && KS <= 32) {
+        const int mf = BWD ? tuning().joint_bwd_mfma : tuning().joint_mfma;
+        return mf == 16 ? launch_kt<KS, 16, BWD>(p, j, stream) : launch_kt<KS, 32, BWD>(p, j, stream);
+    }
+    return launch_kt<KS, kDefault, BWD>(p, j, stream);
+}
+
+template <int KS>
+static hipError_t launch_kh(const DevProblem &p, const JointArgs &j, bool bwd, hipStream_t stream) {
+    return bwd ? launch_kb<KS, true>(p, j, stream) : launch_kb<KS, false>(p, j, stream);
 }
 
 size_t joint_min_lds_bytes(int H, int V) {

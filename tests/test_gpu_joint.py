@@ -249,3 +249,30 @@ def test_joint_four_wave_workgroups_bit_identical(dev, H, V):
     assert np.array_equal(ref[0], got[0])
     for a, b in zip(ref[1:], got[1:]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("tile", ["joint_mfma=16", "joint_bwd_mfma=32", "joint_ring=4", "joint_ring=8"])
+@pytest.mark.parametrize("H,V,blank", [(512, 1024, 517), (512, 1000, 0), (256, 17, 16), (128, 64, 37), (384, 130, 129),
+                                       (256, 2, 1)])
+def test_joint_tile_variants_vs_host(dev, H, V, blank, tile):
+    """The launch variants of the development build against the host reference at this file's tolerances:
+    joint_mfma = 16 (the forward on the v_mfma_f32_16x16x32_bf16 tile: two rows per lane, four lane groups of disjoint
+    vocabulary merged at the end; the product's backward already runs that tile), joint_bwd_mfma = 32 (the backward
+    on the 32x32x16 tile), joint_ring = 4 / 8 (deeper A-fragment rings of the 32x32 tile; H = 256 / 512 only, others
+    run the default). Blank and labels in every lane group and vocabulary tile, tail chunks (V = 1000, 130, 17, 2),
+    ragged rows past the list end."""
+    import monotonic_rnnt_joint as jm
+    enc, pred, w, bias, labels, T, S = make_case(31 + H + V, 4, (10, 50), 16, H, V)
+    labels = np.where(labels == blank, (blank + 1) % V, labels).astype(np.int32)
+    scale = [1.0, -0.5, 2.0, 0.25]
+    k, v = tile.split("=")
+    with knobs(**{k: int(v)}):
+        c, de, dp, dw, db = run_joint(jm, dev, enc, pred, w, bias, labels, T, S, blank=blank, scale=scale)
+    cr, de_r, dp_r, dw_r, db_r = host_reference(enc, pred, w, bias, labels, T, S, blank=blank, scale=scale)
+    assert np.all(np.abs(c - cr) <= 1e-5 * np.maximum(1.0, np.abs(cr))), (c, cr)
+    close(de, de_r, name="d_enc")
+    close(dp, dp_r, name="d_pred")
+    close(dw, dw_r, name="d_weight")
+    close(db, db_r, name="d_bias")
+    for b in range(len(T)):
+        assert torch.all(de[b, T[b]:] == 0) and torch.all(dp[b, S[b] + 1:] == 0)
