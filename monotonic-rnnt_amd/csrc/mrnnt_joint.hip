@@ -19,6 +19,7 @@
 // lane (vocab = (i&3) + 8 (i>>2) + 4 (l>>5)), so the per-row online softmax is register-local and the two
 // lane halves merge once at the end.
 #include <type_traits>
+#include <utility>
 
 #include "mrnnt_device.h"
 
@@ -740,6 +741,343 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
 }
 
 // ---------------------------------------------------------------------------------------------------------
+// Pipelined forward (joint_fwd_pipe): ONE wave per SIMD (4-wave workgroup, 512 registers per lane), persistent over
+// tiles of 128 rows. The activations of the NEXT tile are built while the current tile's MFMAs run: chunk c of the
+// current tile carries fragment c of the next tile's B operand (double-buffered in registers), and the online-softmax
+// epilogue of chunk c - 1 (two accumulators), both in the gaps between the chunk's 32 MFMAs, so the matrix pipe is not
+// left idle during an activation-build phase or an epilogue (the 8-wave kernel above spends ~26 % of a wave's life in
+// the build with both waves of a SIMD building at once). The blank and label logits are not picked from the
+// accumulators (a select tree per chunk) but formed as two dot products per row, fragment by fragment, beside the
+// build: z_blank = W[blank] . h + bias[blank] (fp32, v_dot2c_f32_bf16 -- the same exact bf16 products as the MFMA, in
+// another summation order: ~1e-7 relative).
+
+// scalar tanh (packed f32 beside MFMAs costs more issue time than two scalar ops)
+__device__ __forceinline__ float tanh1(float x) {
+    const float e = fast_exp2(fabsf(x) * (-2.0f * kLog2e));
+    return copysignf((1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e), x);
+}
+
+// one B fragment: 8 bf16 of tanh(enc + pred) (rows past the list read row 0: finite, and only their own discarded
+// output column and dot products see them)
+__device__ __forceinline__ bf16x8 act8(const u4 &ev, const u4 &pv) {
+    bf16x8 h;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        h[2 * w] = (__bf16)tanh1(bf16_lo(ev[w]) + bf16_lo(pv[w]));
+        h[2 * w + 1] = (__bf16)tanh1(bf16_hi(ev[w]) + bf16_hi(pv[w]));
+    }
+    return h;
+}
+
+// acc + h . w over 8 bf16: 4 v_dot2_f32_bf16 (the VOP3P form, explicit accumulator operand: through
+// __builtin_amdgcn_fdot2_f32_bf16 hipcc emits the tied-accumulator v_dot2c form, and inside this kernel that gave
+// wrong dot products -- the tests with the builtin failed, the same kernel with this form or with FMAs passes)
+__device__ __forceinline__ float dot8(const bf16x8 &h, const u4 &w, float acc) {
+    const u4 hu = __builtin_bit_cast(u4, h);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        float r;
+        asm("v_dot2_f32_bf16 %0, %1, %2, %3" : "=v"(r) : "v"(hu[q]), "v"(w[q]), "v"(acc));
+        acc = r;
+    }
+    return acc;
+}
+
+// the same with fp32 FMAs on unpacked bf16 (development check)
+__device__ __forceinline__ float dot8f(const bf16x8 &h, const u4 &w, float acc) {
+    const u4 hu = __builtin_bit_cast(u4, h);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        acc = fmaf(bf16_lo(hu[q]), bf16_lo(w[q]), acc);
+        acc = fmaf(bf16_hi(hu[q]), bf16_hi(w[q]), acc);
+    }
+    return acc;
+}
+
+// the inputs of one fragment of a row: enc / pred slices and the W[label] / W[blank] slices of the same k range
+struct FragIn {
+    u4 e, p, wl, wb;
+};
+
+struct RowSrc {
+    const unsigned short *e, *p, *wl, *wb;  // this lane's k = 8 half + 16 ks slices start here (ks added per load)
+    float keep;
+};
+
+template <int KS>
+__device__ __forceinline__ RowSrc row_src(const JointArgs &j, const RowPos &q, int half, int blank) {
+    constexpr int H = 16 * KS;
+    const bool v = q.valid;
+    RowSrc r;
+    r.e = j.enc + (v ? (int64_t)q.b * j.enc_sb + (int64_t)q.t * H : 0) + 8 * half;
+    r.p = j.pred + (v ? (int64_t)q.b * j.pred_sb + (int64_t)q.s * H : 0) + 8 * half;
+    r.wl = j.W + (int64_t)(q.lab >= 0 ? q.lab : 0) * H + 8 * half;
+    r.wb = j.W + (int64_t)blank * H + 8 * half;
+    r.keep = v ? 1.0f : 0.0f;
+    return r;
+}
+
+__device__ __forceinline__ FragIn frag_load(const RowSrc &r, int ks) {
+    return FragIn{*reinterpret_cast<const u4 *>(r.e + 16 * ks), *reinterpret_cast<const u4 *>(r.p + 16 * ks),
+                  *reinterpret_cast<const u4 *>(r.wl + 16 * ks), *reinterpret_cast<const u4 *>(r.wb + 16 * ks)};
+}
+
+// the per-row online log-sum-exp over one chunk's 16 logits of this lane (branch-free)
+__device__ __forceinline__ void softmax_chunk(const f32x16 &acc, const float *bias, int c, int half, float &m,
+                                              float &sum) {
+    f2 z[8];
+    logits2(acc, bias, c, half, z);
+    float cm = fmaxf(z[0].x, z[0].y);
+#pragma unroll
+    for (int k = 1; k < 8; ++k) cm = max3(cm, z[k].x, z[k].y);
+    const float mn = fmaxf(m, cm);
+    const float mr = (mn == NEG_INF_F) ? 0.0f : mn;
+    const float nb = -mr * kLog2e;
+    float s0 = 0.0f, s1 = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        s0 += fast_exp2(fmaf(z[k].x, kLog2e, nb));
+        s1 += fast_exp2(fmaf(z[k].y, kLog2e, nb));
+    }
+    sum = sum * fast_exp2((m - mr) * kLog2e) + (s0 + s1);
+    m = mn;
+}
+
+template <int KS>
+__device__ __forceinline__ void put_frag(bf16x8 (&b)[KS], int f, const bf16x8 &h) {
+    switch (f) {  // uniform f: a scalar jump, no indexed register access
+#define MRNNT_PUT(k) \
+    case k:          \
+        if constexpr (k < KS) b[k] = h; \
+        break;
+        MRNNT_PUT(0) MRNNT_PUT(1) MRNNT_PUT(2) MRNNT_PUT(3) MRNNT_PUT(4) MRNNT_PUT(5) MRNNT_PUT(6) MRNNT_PUT(7)
+        MRNNT_PUT(8) MRNNT_PUT(9) MRNNT_PUT(10) MRNNT_PUT(11) MRNNT_PUT(12) MRNNT_PUT(13) MRNNT_PUT(14) MRNNT_PUT(15)
+        MRNNT_PUT(16) MRNNT_PUT(17) MRNNT_PUT(18) MRNNT_PUT(19) MRNNT_PUT(20) MRNNT_PUT(21) MRNNT_PUT(22) MRNNT_PUT(23)
+        MRNNT_PUT(24) MRNNT_PUT(25) MRNNT_PUT(26) MRNNT_PUT(27) MRNNT_PUT(28) MRNNT_PUT(29) MRNNT_PUT(30) MRNNT_PUT(31)
+#undef MRNNT_PUT
+        default: break;
+    }
+}
+
+template <class F, int... I>
+__device__ __forceinline__ void static_for_impl(F &f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F &&f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// One pipelined chunk, scheduled by hand: the KS MFMAs of the chunk (A fragments through a 3-deep LDS read ring) and,
+// in their gaps, the online softmax of the previous chunk's accumulator (35 work units, EPI) and the next tile's
+// fragment from its loaded enc / pred slices with its two blank / label dot products (18 work units), spread evenly;
+// a sched_barrier after each gap keeps this order (the compiler otherwise issues the MFMAs back to back and the VALU
+// after them, MI355X_MICROARCH.md 'MFMA gap' rows: <= 5 issues per 32x32x16 gap hide).
+template <int KS, bool EPI>
+__device__ __forceinline__ f32x16 pipe_chunk(const unsigned short *wbuf, const bf16x8 (&bfr)[KS], int lane,
+                                             const f32x16 &accp, const float *bias_c, float &m, float &sum,
+                                             const FragIn &cur, bf16x8 &hout, float &zbd, float &zed) {
+    constexpr int H = 16 * KS, D = 3, NS = 35, NBU = 18;
+    const int r = lane & 31, hf = lane >> 5;
+    const unsigned short *row = wbuf + r * H;
+    const unsigned short *base[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) base[k] = row + 8 * ((2 * k + hf) ^ (r & 15));
+    auto rd = [&](int ks) { return *reinterpret_cast<const bf16x8 *>(base[ks & 7] + 128 * (ks >> 3)); };
+    bf16x8 a[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) a[d] = rd(d);
+    f32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+    // softmax state
+    f4 bv[4];
+    f2 z[8];
+    float cm = 0.0f, mn = 0.0f, mr = 0.0f, nb = 0.0f, s0 = 0.0f, s1 = 0.0f;
+    // build state
+    float xin[8], ex[8];
+    unsigned hu[4];
+    auto sm_unit = [&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        if constexpr (u == 0) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) bv[q] = *reinterpret_cast<const f4 *>(bias_c + 8 * q);
+        } else if constexpr (u <= 8) {
+            constexpr int k = u - 1, q = k >> 1, o = 4 * q + 2 * (k & 1);
+            z[k] = (f2){accp[o] + ((k & 1) ? bv[q].z : bv[q].x), accp[o + 1] + ((k & 1) ? bv[q].w : bv[q].y)};
+        } else if constexpr (u == 9) {
+            cm = fmaxf(z[0].x, z[0].y);
+        } else if constexpr (u <= 16) {
+            cm = max3(cm, z[u - 9].x, z[u - 9].y);
+        } else if constexpr (u == 17) {
+            mn = fmaxf(m, cm);
+            mr = (mn == NEG_INF_F) ? 0.0f : mn;
+            nb = -mr * kLog2e;
+        } else if constexpr (u <= 33) {
+            constexpr int e = u - 18, k = e >> 1;
+            if constexpr (e & 1) s1 += fast_exp2(fmaf(z[k].y, kLog2e, nb));
+            else s0 += fast_exp2(fmaf(z[k].x, kLog2e, nb));
+        } else {
+            sum = sum * fast_exp2((m - mr) * kLog2e) + (s0 + s1);
+            m = mn;
+        }
+    };
+    auto b_unit = [&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        if constexpr (u < 16) {
+            constexpr int w2 = u >> 1, w = w2 >> 1;
+            if constexpr ((u & 1) == 0) {
+                xin[w2] = (w2 & 1) ? bf16_hi(cur.e[w]) + bf16_hi(cur.p[w]) : bf16_lo(cur.e[w]) + bf16_lo(cur.p[w]);
+                ex[w2] = fast_exp2(fabsf(xin[w2]) * (-2.0f * kLog2e));
+            } else {
+                xin[w2] = copysignf((1.0f - ex[w2]) * __builtin_amdgcn_rcpf(1.0f + ex[w2]), xin[w2]);
+                if constexpr (w2 & 1) {
+                    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+                    hu[w] = __builtin_bit_cast(unsigned, __builtin_convertvector((f2){xin[w2 - 1], xin[w2]}, bf16x2));
+                }
+            }
+        } else if constexpr (u == 16) {
+            hout = __builtin_bit_cast(bf16x8, (u4){hu[0], hu[1], hu[2], hu[3]});
+            zbd = dot8(hout, cur.wb, 0.0f);
+        } else {
+            zed = dot8(hout, cur.wl, 0.0f);
+        }
+    };
+    static_for<KS>([&](auto kc) {
+        constexpr int ks = decltype(kc)::value;
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks % D], bfr[ks], acc, 0, 0, 0);
+        if constexpr (ks + D < KS) a[ks % D] = rd(ks + D);
+        if constexpr (EPI) {
+            constexpr int lo = ks * NS / KS, hi = (ks + 1) * NS / KS;
+            static_for<hi - lo>([&](auto ic) { sm_unit(std::integral_constant<int, lo + decltype(ic)::value>{}); });
+        }
+        constexpr int blo = ks * NBU / KS, bhi = (ks + 1) * NBU / KS;
+        static_for<bhi - blo>([&](auto ic) { b_unit(std::integral_constant<int, blo + decltype(ic)::value>{}); });
+        __builtin_amdgcn_sched_barrier(0);
+    });
+    return acc;
+}
+
+template <int KS, int NB, bool PIPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void joint_fwd_pipe_kernel(DevProblem p,
+                                                                                                   JointArgs j) {
+    static_assert(KS <= 32, "put_frag covers 32 fragments");
+    using WT = WTile<KS>;
+    constexpr int NW = 4, ROWS = 32 * NW;
+    extern __shared__ __attribute__((aligned(16))) unsigned short wsh[];
+    const int64_t ntiles = (list_len(j) + ROWS - 1) / ROWS;
+    int64_t tile = blockIdx.x;
+    if (tile >= ntiles) return;
+    const int lane = threadIdx.x & 63, half = lane >> 5, wave = threadIdx.x >> 6;
+    const int V = p.V, blank = p.blank;
+    const int nch = (V + 31) / 32;
+    const float *bias = load_bias<KS, NB>(j, V, wsh);
+    auto row_of = [&](int64_t t) { return t * ROWS + wave * 32 + (lane & 31); };
+
+    // the W chunk stream runs on across tiles (chunk index wrapping at nch, buffer at NB); NB - 1 chunks in flight
+    int c_issue = 0, b_issue = 0, b_use = 0;
+    auto stage_next = [&]() {
+        WT::template stage<NW>(j, V, c_issue, wsh + b_issue * WT::ELEMS);
+        c_issue = c_issue + 1 == nch ? 0 : c_issue + 1;
+        b_issue = b_issue + 1 == NB ? 0 : b_issue + 1;
+    };
+#pragma unroll
+    for (int k = 0; k < NB - 1; ++k) stage_next();
+
+    // prologue: the first tile's activations and blank / label dot products, outside the MFMA loop
+    RowPos q = row_pos(p, j, row_of(tile));
+    bf16x8 bcur[KS], bnext[KS];
+    float zb = 0.0f, ze = 0.0f;
+    {
+        const RowSrc r = row_src<KS>(j, q, half, blank);
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const FragIn in = frag_load(r, ks);
+            bcur[ks] = act8(in.e, in.p);
+            zb = PIPE ? dot8(bcur[ks], in.wb, zb) : dot8f(bcur[ks], in.wb, zb);
+            ze = PIPE ? dot8(bcur[ks], in.wl, ze) : dot8f(bcur[ks], in.wl, ze);
+        }
+    }
+    __syncthreads();  // bias in LDS
+
+    for (;;) {
+        const int64_t tnext = tile + gridDim.x;
+        const RowPos qn = row_pos(p, j, row_of(tnext));  // past the list: builds from row 0, never written
+        const RowSrc rn = row_src<KS>(j, qn, half, blank);
+        float zbn = 0.0f, zen = 0.0f, m = NEG_INF_F, sum = 0.0f;
+        FragIn in = frag_load(rn, 0);
+        f32x16 accp;
+        // chunk c: the 32 MFMAs of chunk c, the softmax of chunk c - 1 and fragment c of the next tile in one basic
+        // block (no branch between them), so the scheduler can place the VALU in the MFMA gaps
+        auto body = [&](int c, auto epi_tag) {
+            wait_dma();  // chunk c's DMA and fragment c's inputs (issued one chunk ago)
+            __builtin_amdgcn_s_barrier();
+            stage_next();
+            const FragIn cur = in;
+            in = frag_load(rn, min(c + 1, KS - 1));
+            bf16x8 h;
+            float zbd, zed;
+            f32x16 acc;
+            if constexpr (PIPE) {
+                acc = pipe_chunk<KS, decltype(epi_tag)::value>(wsh + b_use * WT::ELEMS, bcur, lane, accp,
+                                                               bias + 32 * (c - 1) + 4 * half, m, sum, cur, h, zbd, zed);
+            } else {  // development check: the same stream and build, compiler-scheduled
+                acc = WT::template mma<2>(wsh + b_use * WT::ELEMS, bcur, lane);
+                if constexpr (decltype(epi_tag)::value) softmax_chunk(accp, bias, c - 1, half, m, sum);
+                h = act8(cur.e, cur.p);
+                zbd = dot8f(h, cur.wb, 0.0f);
+                zed = dot8f(h, cur.wl, 0.0f);
+            }
+            b_use = b_use + 1 == NB ? 0 : b_use + 1;
+            {  // keep all of it in the chunk's block (the compiler would sink it past the fragment switch)
+                u4 hv = __builtin_bit_cast(u4, h);
+                asm volatile("" : "+v"(m), "+v"(sum), "+v"(zbd), "+v"(zed), "+v"(hv));
+                h = __builtin_bit_cast(bf16x8, hv);
+            }
+            const float carry = c < KS ? 1.0f : 0.0f;  // chunks past the last fragment carry nothing (branch-free)
+            zbn = fmaf(carry, zbd, zbn);
+            zen = fmaf(carry, zed, zen);
+            put_frag<KS>(bnext, c, h);
+            accp = acc;
+        };
+        body(0, std::false_type{});
+        for (int c = 1; c < nch; ++c) body(c, std::true_type{});
+        softmax_chunk(accp, bias, nch - 1, half, m, sum);
+        for (int f = nch; f < KS; ++f) {  // V < 32 KS: the fragments no chunk carried
+            const FragIn fi = frag_load(rn, f);
+            const bf16x8 h = act8(fi.e, fi.p);
+            zbn = dot8(h, fi.wb, zbn);
+            zen = dot8(h, fi.wl, zen);
+            put_frag<KS>(bnext, f, h);
+        }
+        // finish the current tile: merge the two lane halves (same row, disjoint vocabulary / k)
+        {
+            const float m2 = __shfl_xor(m, 32), s2 = __shfl_xor(sum, 32);
+            const float zbt = zb + __shfl_xor(zb, 32), zet = ze + __shfl_xor(ze, 32);
+            const float mn = fmaxf(m, m2);
+            const float mr = (mn == NEG_INF_F) ? 0.0f : mn;
+            const float st = sum * fast_exp2((m - mr) * kLog2e) + s2 * fast_exp2((m2 - mr) * kLog2e);
+            if (q.valid && half == 0) {
+                const double den = -(double)mn - log_row_sum(st);
+                const float bb = j.bias ? j.bias[blank] : 0.0f;
+                const float bl = (j.bias && q.lab >= 0) ? j.bias[q.lab] : 0.0f;
+                p.den[q.row] = (float)den;
+                p.lp[q.row] = Lp{(double)(zbt + bb) + den,
+                                 (q.lab >= 0 ? (double)(zet + bl) : (q.lab == -2 ? __builtin_nan("") : 0.0)) + den};
+            }
+        }
+        tile = tnext;
+        if (tile >= ntiles) break;
+        q = qn;
+        zb = zbn;
+        ze = zen;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) bcur[ks] = bnext[ks];
+    }
+    wait_dma();  // the stream's last DMA must land before the workgroup's LDS is released
+}
+
+// ---------------------------------------------------------------------------------------------------------
 // backward tail: dpre = dH * (1 - Hact^2) over the live rows, summed into denc[b, t] (over s; written once per
 // column) and dpred[b, s] (over t; accumulated in LDS over a block of TT columns, then one fp32 atomic per
 // (s, h) per block). One workgroup per (utterance, block of TT frames, slice of HS hidden units); 4 hidden
@@ -977,9 +1315,43 @@ static hipError_t launch_kt(const DevProblem &p, const JointArgs &j, hipStream_t
 // two rows of online-softmax state per lane cost more than it gains); both in the development build (joint_mfma,
 // joint_bwd_mfma). H = 640 keeps the 32x32 tile everywhere (the 16x16 one spills there: two rows' state per lane
 // beside 160 B-operand registers).
+static int cu_count() {
+    static int n[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    if (n[dev] == 0) {
+        int c = 0;
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+        n[dev] = c;
+    }
+    return n[dev];
+}
+
+// the pipelined forward: one persistent 4-wave workgroup per CU (its 512-register waves fill the CU's register file)
+template <int KS>
+static hipError_t launch_pipe(const DevProblem &p, const JointArgs &j, hipStream_t stream) {
+    const size_t lds = 2 * sizeof(unsigned short) * WTile<KS>::ELEMS + sizeof(float) * ((p.V + 31) / 32 * 32);
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    const int64_t tiles = (j.n + 127) / 128;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(tiles, cu_count()));
+    auto kern = joint_fwd_pipe_kernel<KS, 2, true>;
+    if constexpr (kVariants)
+        if (tuning().joint_pipe == 2) kern = joint_fwd_pipe_kernel<KS, 2, false>;
+    if (lds > 65536) {
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    kern<<<grid, 256, lds, stream>>>(p, j);
+    return hipGetLastError();
+}
+
 template <int KS, bool BWD>
 static hipError_t launch_kb(const DevProblem &p, const JointArgs &j, hipStream_t stream) {
     constexpr int kDefault = KS > 32 ? 32 : BWD ? Tuning{}.joint_bwd_mfma : Tuning{}.joint_mfma;
+    if constexpr (!BWD && KS <= 32 && (kVariants || Tuning{}.joint_pipe)) {
+        if (tuning().joint_pipe) return launch_pipe<KS>(p, j, stream);
+    }
     if constexpr (kVariants && KS <= 32) {
         const int mf = BWD ? tuning().joint_bwd_mfma : tuning().joint_mfma;
         return mf == 16 ? launch_kt<KS, 16, BWD>(p, j, stream) : launch_kt<KS, 32, BWD>(p, j, stream);
