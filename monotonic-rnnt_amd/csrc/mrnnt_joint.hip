@@ -240,6 +240,18 @@ struct WTile {
         }
     }
 
+    // piece ii (of NI / NW) of this wave's share of stage<NW>
+    template <int NW>
+    __device__ static __forceinline__ void stage_piece(const JointArgs &j, int V, int c, unsigned short *wbuf, int ii) {
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        const int i = NW * ii + wave;
+        const int L = 64 * i + lane;
+        const int r = L / CPR, pc = L % CPR;
+        const int v = min(32 * c + r, V - 1);
+        const unsigned short *g = j.W + (int64_t)v * H + 8 * (pc ^ (r & 15));
+        __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void *)(wbuf + 512 * i), 16, 0, 0);
+    }
+
     // one 32x32 output tile: D[vocab][row] = sum_k W[vocab][k] h[row][k]; A fragments stream from LDS
     // through a 4-deep register ring so no MFMA waits on a ds_read it has just issued. The swizzled piece of
     // k-step ks = 8m + k' is 16m + ((2k' + half) ^ (r & 15)): 8 base addresses, m in the immediate offset.
@@ -873,10 +885,11 @@ __device__ __forceinline__ void static_for(F &&f) {
 // fragment from its loaded enc / pred slices with its two blank / label dot products (18 work units), spread evenly;
 // a sched_barrier after each gap keeps this order (the compiler otherwise issues the MFMAs back to back and the VALU
 // after them, MI355X_MICROARCH.md 'MFMA gap' rows: <= 5 issues per 32x32x16 gap hide).
-template <int KS, bool EPI>
+template <int KS, bool EPI, int NMEM = 0, class Mem = std::nullptr_t>
 __device__ __forceinline__ f32x16 pipe_chunk(const unsigned short *wbuf, const bf16x8 (&bfr)[KS], int lane,
                                              const f32x16 &accp, const float *bias_c, float &m, float &sum,
-                                             const FragIn &cur, bf16x8 &hout, float &zbd, float &zed) {
+                                             const FragIn &cur, bf16x8 &hout, float &zbd, float &zed,
+                                             Mem &&mem = nullptr) {
     constexpr int H = 16 * KS, D = 3, NS = 35, NBU = 18;
     const int r = lane & 31, hf = lane >> 5;
     const unsigned short *row = wbuf + r * H;
@@ -953,12 +966,16 @@ __device__ __forceinline__ f32x16 pipe_chunk(const unsigned short *wbuf, const b
         }
         constexpr int blo = ks * NBU / KS, bhi = (ks + 1) * NBU / KS;
         static_for<bhi - blo>([&](auto ic) { b_unit(std::integral_constant<int, blo + decltype(ic)::value>{}); });
+        if constexpr (NMEM > 0 && ks < KS / 2) {  // the next chunk's DMA and the next fragment's loads: first half
+            constexpr int mlo = ks * NMEM / (KS / 2), mhi = (ks + 1) * NMEM / (KS / 2);
+            static_for<mhi - mlo>([&](auto ic) { mem(std::integral_constant<int, mlo + decltype(ic)::value>{}); });
+        }
         __builtin_amdgcn_sched_barrier(0);
     });
     return acc;
 }
 
-template <int KS, int NB, bool PIPE>
+template <int KS, int NB, bool PIPE, bool MEMGAP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void joint_fwd_pipe_kernel(DevProblem p,
                                                                                                    JointArgs j) {
     static_assert(KS <= 32, "put_frag covers 32 fragments");
@@ -1012,13 +1029,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         auto body = [&](int c, auto epi_tag) {
             wait_dma();  // chunk c's DMA and fragment c's inputs (issued one chunk ago)
             __builtin_amdgcn_s_barrier();
-            stage_next();
             const FragIn cur = in;
-            in = frag_load(rn, min(c + 1, KS - 1));
+            if constexpr (!MEMGAP) {
+                stage_next();
+                in = frag_load(rn, min(c + 1, KS - 1));
+            }
             bf16x8 h;
             float zbd, zed;
             f32x16 acc;
-            if constexpr (PIPE) {
+            if constexpr (MEMGAP) {  // the DMA pieces and the fragment loads in the MFMA gaps too
+                constexpr int NPW = WT::NI / NW;
+                unsigned short *wb_is = wsh + b_issue * WT::ELEMS;
+                const int c_is = c_issue;
+                acc = pipe_chunk<KS, decltype(epi_tag)::value, NPW + 1>(
+                    wsh + b_use * WT::ELEMS, bcur, lane, accp, bias + 32 * (c - 1) + 4 * half, m, sum, cur, h, zbd,
+                    zed, [&](auto uc) {
+                        constexpr int u = decltype(uc)::value;
+                        if constexpr (u < NPW) WT::template stage_piece<NW>(j, V, c_is, wb_is, u);
+                        else in = frag_load(rn, min(c + 1, KS - 1));
+                    });
+                c_issue = c_issue + 1 == nch ? 0 : c_issue + 1;
+                b_issue = b_issue + 1 == NB ? 0 : b_issue + 1;
+            } else if constexpr (PIPE) {
                 acc = pipe_chunk<KS, decltype(epi_tag)::value>(wsh + b_use * WT::ELEMS, bcur, lane, accp,
                                                                bias + 32 * (c - 1) + 4 * half, m, sum, cur, h, zbd, zed);
             } else {  // development check: the same stream and build, compiler-scheduled
@@ -1334,9 +1366,11 @@ static hipError_t launch_pipe(const DevProblem &p, const JointArgs &j, hipStream
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     const int64_t tiles = (j.n + 127) / 128;
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(tiles, cu_count()));
-    auto kern = joint_fwd_pipe_kernel<KS, 2, true>;
-    if constexpr (kVariants)
-        if (tuning().joint_pipe == 2) kern = joint_fwd_pipe_kernel<KS, 2, false>;
+    auto kern = joint_fwd_pipe_kernel<KS, 2, true, true>;
+    if constexpr (kVariants) {
+        if (tuning().joint_pipe == 2) kern = joint_fwd_pipe_kernel<KS, 2, false, false>;
+        if (tuning().joint_pipe == 3) kern = joint_fwd_pipe_kernel<KS, 2, true, false>;
+    }
     if (lds > 65536) {
         const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

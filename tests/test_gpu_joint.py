@@ -251,7 +251,7 @@ def test_joint_four_wave_workgroups_bit_identical(dev, H, V):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("tile", ["joint_mfma=16", "joint_bwd_mfma=32", "joint_ring=4", "joint_ring=8", "joint_pipe=1", "joint_pipe=2"])
+@pytest.mark.parametrize("tile", ["joint_mfma=16", "joint_bwd_mfma=32", "joint_ring=4", "joint_ring=8", "joint_pipe=1", "joint_pipe=2", "joint_pipe=3"])
 @pytest.mark.parametrize("H,V,blank", [(512, 1024, 517), (512, 1000, 0), (256, 17, 16), (128, 64, 37), (384, 130, 129),
                                        (256, 2, 1)])
 def test_joint_tile_variants_vs_host(dev, H, V, blank, tile):
@@ -284,13 +284,14 @@ def test_joint_pipe_many_tiles_per_workgroup(dev, H, V):
     tile's activations during the current one's MFMAs): costs and all gradients against the 8-wave forward within this
     file's tolerances (blank / label logits come from dot products there, from the accumulators here)."""
     import monotonic_rnnt_joint as jm
-    enc, pred, w, bias, labels, T, S = make_case(91 + H, 8, (150, 200), 40, H, V)
+    enc, pred, w, bias, labels, T, S = make_case(91 + H, 32, (150, 200), 60, H, V)
     blank = V // 2
     labels = np.where(labels == blank, (blank + 1) % V, labels).astype(np.int32)
     ref = run_joint(jm, dev, enc, pred, w, bias, labels, T, S, blank=blank)
     with knobs(joint_pipe=1):
         got = run_joint(jm, dev, enc, pred, w, bias, labels, T, S, blank=blank)
-    assert int(np.sum(T * (S + 1))) > 300 * 128  # more tiles than the 256 workgroups
+    inband = sum(min(t, s) - max(0, t - (tt - s)) + 1 for tt, s in zip(T.tolist(), S.tolist()) for t in range(tt))
+    assert inband > 300 * 128, inband  # more 128-row tiles than the 256 workgroups
     assert np.all(np.abs(got[0] - ref[0]) <= 1e-5 * np.maximum(1.0, np.abs(ref[0]))), (got[0], ref[0])
     for a, b, name in zip(got[1:], ref[1:], ["d_enc", "d_pred", "d_weight", "d_bias"]):
-        close(a, b, name=name)
+        close(a.cpu(), b.cpu().double(), name=name)
