@@ -127,6 +127,8 @@ struct Tuning {
     int joint_mfma = 32;          // fused joint forward: MFMA tile, 32 (v_mfma_f32_32x32x16_bf16) or 16 (16x16x32)
     int joint_bwd_mfma = 16;      // fused joint backward: the same
     int joint_pipe = 0;           // fused joint forward: 1 -> the pipelined one-wave-per-SIMD kernel (H <= 512)
+    int joint_fwd_opt = 0;        // fused joint 8-wave forward: bit 0 bias as the initial accumulator, bit 1 label logit
+                                  // as a dot product (development A/B)
     int joint_ring = 2;           // fused joint 32x32 tile: A fragments in flight (development build: 2, 4, 8)
     int joint_reduce_sparse = 0;  // joint d_enc/d_pred reduce: 0 row-parallel kernel below 4 live rows per column,
                                   // 1 always frame by frame, 2 always row-parallel

@@ -53,6 +53,20 @@ __device__ __forceinline__ f2 fast_tanh2(f2 x) {
     return (f2){copysignf(y.x, x.x), copysignf(y.y, x.y)};
 }
 
+// acc + h . w over 8 bf16: 4 v_dot2_f32_bf16 (the VOP3P form, explicit accumulator operand: through
+// __builtin_amdgcn_fdot2_f32_bf16 hipcc emits the tied-accumulator v_dot2c form, and inside this kernel that gave
+// wrong dot products -- the tests with the builtin failed, the same kernel with this form or with FMAs passes)
+__device__ __forceinline__ float dot8(const bf16x8 &h, const u4 &w, float acc) {
+    const u4 hu = __builtin_bit_cast(u4, h);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        float r;
+        asm("v_dot2_f32_bf16 %0, %1, %2, %3" : "=v"(r) : "v"(hu[q]), "v"(w[q]), "v"(acc));
+        acc = r;
+    }
+    return acc;
+}
+
 // ---------------------------------------------------------------------------------------------------------
 // row lists: entries (column, s) in column order, s ascending; mode 0 = in-band rows, 1 = live rows
 
@@ -257,6 +271,16 @@ struct WTile {
     // k-step ks = 8m + k' is 16m + ((2k' + half) ^ (r & 15)): 8 base addresses, m in the immediate offset.
     template <int RING = 4>
     __device__ static __forceinline__ f32x16 mma(const unsigned short *wbuf, const bf16x8 (&bfr)[KS], int lane) {
+        f32x16 zero;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) zero[i] = 0.0f;
+        return mma_from<RING>(wbuf, bfr, lane, zero);
+    }
+
+    // the same accumulating onto acc0 (the forward passes the bias there: z comes out of the MFMA chain)
+    template <int RING = 4>
+    __device__ static __forceinline__ f32x16 mma_from(const unsigned short *wbuf, const bf16x8 (&bfr)[KS], int lane,
+                                                      const f32x16 &acc0) {
         const int r = lane & 31, half = lane >> 5;
         const unsigned short *row = wbuf + r * H;
         const unsigned short *base[8];
@@ -267,9 +291,7 @@ struct WTile {
         bf16x8 a[D];
 #pragma unroll
         for (int d = 0; d < D; ++d) a[d] = rd(d);
-        f32x16 acc;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+        f32x16 acc = acc0;
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks % D], bfr[ks], acc, 0, 0, 0);
@@ -427,7 +449,10 @@ __device__ __forceinline__ float *load_bias(const JointArgs &j, int V, unsigned 
 }
 
 // two waves per SIMD: the compiler keeps each kernel within 256 registers per lane
-template <int KS, int NB, int NW, int RG>
+// OPT (development A/B, joint_fwd_opt): bit 0 -- the bias is the MFMA chain's initial accumulator (no bias adds in
+// the epilogue); bit 1 -- the label logit as a dot product W[label] . h beside the activation build (no per-chunk
+// label select tree)
+template <int KS, int NB, int NW, int RG, int OPT = 0>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2))) void joint_fwd_kernel(DevProblem p,
                                                                                              JointArgs j) {
     extern __shared__ __attribute__((aligned(16))) unsigned short wsh[];
@@ -444,9 +469,38 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const f2 l2e = {kLog2e, kLog2e};
     float m = NEG_INF_F, sum = 0.0f, zb = 0.0f, ze = 0.0f;
     bool fb = false, fe = false;
-    chunk_loop<KS, NB, NW, RG>(j, V, wsh, bfr, lane, 0, [&](const f32x16 &acc, int c) {
+    if constexpr (OPT & 2) {  // W[label] . h over this lane's k half (rows without a label: row 0, unused)
+        const unsigned short *wl = j.W + (int64_t)(q.lab >= 0 ? q.lab : 0) * (16 * KS) + 8 * half;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) ze = dot8(bfr[ks], *reinterpret_cast<const u4 *>(wl + 16 * ks), ze);
+        fe = q.lab >= 0;
+    }
+    auto mma = [&](const unsigned short *wb, int c) {
+        if constexpr (OPT & 1) {
+            f32x16 b0;
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+                const f4 bv = *reinterpret_cast<const f4 *>(bias + 32 * c + 8 * q4 + 4 * half);
+                b0[4 * q4] = bv.x;
+                b0[4 * q4 + 1] = bv.y;
+                b0[4 * q4 + 2] = bv.z;
+                b0[4 * q4 + 3] = bv.w;
+            }
+            return WTile<KS>::template mma_from<RG>(wb, bfr, lane, b0);
+        } else {
+            return WTile<KS>::template mma<RG>(wb, bfr, lane);
+        }
+    };
+    int c_mma = 0;
+    chunk_loop_with<KS, NB, NW>(j, V, wsh, 0, [&](const unsigned short *wb) { return mma(wb, c_mma++); },
+                                [&](const f32x16 &acc, int c) {
         f2 z[8];
-        logits2(acc, bias, c, half, z);
+        if constexpr (OPT & 1) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) z[k] = (f2){acc[2 * k], acc[2 * k + 1]};
+        } else {
+            logits2(acc, bias, c, half, z);
+        }
         float cm = fmaxf(z[0].x, z[0].y);
 #pragma unroll
         for (int k = 1; k < 8; ++k) cm = max3(cm, z[k].x, z[k].y);
@@ -469,14 +523,16 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
                 fb = true;
             }
         }
-        const int jl = q.lab - 32 * c;
-        const int rl = acc_reg_of(jl & 31, half);
-        const bool mine = q.lab >= 0 && jl >= 0 && jl < 32 && rl >= 0;
-        if (__ballot(mine)) {  // most chunks hold some lane's label; skip the select when none does
-            const float x = tree_pick(z, rl);
-            if (mine) {
-                ze = x;
-                fe = true;
+        if constexpr (!(OPT & 2)) {
+            const int jl = q.lab - 32 * c;
+            const int rl = acc_reg_of(jl & 31, half);
+            const bool mine = q.lab >= 0 && jl >= 0 && jl < 32 && rl >= 0;
+            if (__ballot(mine)) {  // most chunks hold some lane's label; skip the select when none does
+                const float x = tree_pick(z, rl);
+                if (mine) {
+                    ze = x;
+                    fe = true;
+                }
             }
         }
     });
@@ -488,7 +544,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const float mr = (mn == NEG_INF_F) ? 0.0f : mn;
     sum = sum * fast_exp2((m - mr) * kLog2e) + s2 * fast_exp2((m2 - mr) * kLog2e);
     if (!fb && fb2) zb = zb2;
-    if (!fe && fe2) ze = ze2;
+    if constexpr (OPT & 2) {
+        ze = ze + ze2 + ((j.bias && q.lab >= 0) ? j.bias[q.lab] : 0.0f);  // the two k halves, then the bias
+    } else {
+        if (!fe && fe2) ze = ze2;
+    }
     if (q.valid && half == 0) {
         const double den = -(double)mn - log_row_sum(sum);
         p.den[q.row] = (float)den;
@@ -779,20 +839,6 @@ __device__ __forceinline__ bf16x8 act8(const u4 &ev, const u4 &pv) {
         h[2 * w + 1] = (__bf16)tanh1(bf16_hi(ev[w]) + bf16_hi(pv[w]));
     }
     return h;
-}
-
-// acc + h . w over 8 bf16: 4 v_dot2_f32_bf16 (the VOP3P form, explicit accumulator operand: through
-// __builtin_amdgcn_fdot2_f32_bf16 hipcc emits the tied-accumulator v_dot2c form, and inside this kernel that gave
-// wrong dot products -- the tests with the builtin failed, the same kernel with this form or with FMAs passes)
-__device__ __forceinline__ float dot8(const bf16x8 &h, const u4 &w, float acc) {
-    const u4 hu = __builtin_bit_cast(u4, h);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        float r;
-        asm("v_dot2_f32_bf16 %0, %1, %2, %3" : "=v"(r) : "v"(hu[q]), "v"(w[q]), "v"(acc));
-        acc = r;
-    }
-    return acc;
 }
 
 // the same with fp32 FMAs on unpacked bf16 (development check)
@@ -1298,7 +1344,7 @@ hipError_t launch_joint_reduce(const DevProblem &p, const JointArgs &j, const in
 }
 
 // kernel of a launch shape: MF = MFMA tile (32: 32x32x16, 16: 16x16x32), RG = A-fragment ring of the 32x32 tile
-template <int KS, int NB, int NW, int MF, bool BWD, int RG>
+template <int KS, int NB, int NW, int MF, bool BWD, int RG, int OPT = 0>
 static hipError_t launch_knw(const DevProblem &p, const JointArgs &j, size_t lds, hipStream_t stream) {
     const int64_t blocks = (j.n + 32 * NW - 1) / (32 * NW);
     if (blocks * 64 * NW > 0xffffffffll) return hipErrorInvalidValue;  // 32-bit dispatch size in work-items
@@ -1306,7 +1352,7 @@ static hipError_t launch_knw(const DevProblem &p, const JointArgs &j, size_t lds
     if constexpr (MF == 16 && BWD) kern = joint_bwd16_kernel<KS, NB, NW>;
     else if constexpr (MF == 16) kern = joint_fwd16_kernel<KS, NB, NW>;
     else if constexpr (BWD) kern = joint_bwd_kernel<KS, NB, NW, RG>;
-    else kern = joint_fwd_kernel<KS, NB, NW, RG>;
+    else kern = joint_fwd_kernel<KS, NB, NW, RG, OPT>;
     if (lds > 65536) {
         const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1331,6 +1377,12 @@ static hipError_t launch_kt(const DevProblem &p, const JointArgs &j, hipStream_t
         // MFMAs; 128 rows share each W chunk
         if (tuning().joint_nw == 4 && WTile<KS>::NI % 4 == 0 && 2 * (2 * tile + bias) <= 160 * 1024)
             return launch_knw<KS, 2, 4, MF, BWD, 2>(p, j, 2 * tile + bias, stream);
+        if constexpr (MF == 32 && !BWD) {
+            const int o = tuning().joint_fwd_opt;
+            if (2 * tile + bias <= 160 * 1024 && o == 1) return launch_knw<KS, 2, 8, MF, BWD, 2, 1>(p, j, 2 * tile + bias, stream);
+            if (2 * tile + bias <= 160 * 1024 && o == 2) return launch_knw<KS, 2, 8, MF, BWD, 2, 2>(p, j, 2 * tile + bias, stream);
+            if (2 * tile + bias <= 160 * 1024 && o == 3) return launch_knw<KS, 2, 8, MF, BWD, 2, 3>(p, j, 2 * tile + bias, stream);
+        }
         if constexpr (MF == 32 && (KS == 16 || KS == 32)) {
             if (2 * tile + bias <= 160 * 1024 && tuning().joint_ring == 4)
                 return launch_knw<KS, 2, 8, MF, BWD, 4>(p, j, 2 * tile + bias, stream);

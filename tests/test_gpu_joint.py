@@ -251,7 +251,8 @@ def test_joint_four_wave_workgroups_bit_identical(dev, H, V):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("tile", ["joint_mfma=16", "joint_bwd_mfma=32", "joint_ring=4", "joint_ring=8", "joint_pipe=1", "joint_pipe=2", "joint_pipe=3"])
+@pytest.mark.parametrize("tile", ["joint_mfma=16", "joint_bwd_mfma=32", "joint_ring=4", "joint_ring=8", "joint_pipe=1", "joint_pipe=2", "joint_pipe=3",
+                                  "joint_fwd_opt=1", "joint_fwd_opt=2", "joint_fwd_opt=3"])
 @pytest.mark.parametrize("H,V,blank", [(512, 1024, 517), (512, 1000, 0), (256, 17, 16), (128, 64, 37), (384, 130, 129),
                                        (256, 2, 1)])
 def test_joint_tile_variants_vs_host(dev, H, V, blank, tile):
