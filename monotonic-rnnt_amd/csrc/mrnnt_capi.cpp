@@ -995,6 +995,7 @@ __attribute__((visibility("default"))) int mrnnt_tune(const char *key, int value
     else if (!std::strcmp(key, "joint_ring")) slot = &t.joint_ring;
     else if (!std::strcmp(key, "joint_pipe")) slot = &t.joint_pipe;
     else if (!std::strcmp(key, "joint_fwd_opt")) slot = &t.joint_fwd_opt;
+    else if (!std::strcmp(key, "joint_fwd_persist")) slot = &t.joint_fwd_persist;
     if (!slot) return -1;
     const int prev = *slot;
     if (value >= 0) *slot = value;

@@ -129,6 +129,8 @@ struct Tuning {
     int joint_pipe = 0;           // fused joint forward: 1 -> the pipelined one-wave-per-SIMD kernel (H <= 512)
     int joint_fwd_opt = 0;        // fused joint 8-wave forward: bit 0 bias as the initial accumulator, bit 1 label logit
                                   // as a dot product (development A/B)
+    int joint_fwd_persist = 0;    // fused joint forward: 1 -> persistent 8-wave kernel (W stream across tiles, next tile's
+                                  // row positions prefetched)
     int joint_ring = 2;           // fused joint 32x32 tile: A fragments in flight (development build: 2, 4, 8)
     int joint_reduce_sparse = 0;  // joint d_enc/d_pred reduce: 0 row-parallel kernel below 4 live rows per column,
                                   // 1 always frame by frame, 2 always row-parallel

@@ -556,6 +556,126 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     }
 }
 
+// Persistent form of the forward (development A/B, joint_fwd_persist): one 8-wave workgroup per CU walks its tiles;
+// the W-chunk stream runs on across tiles (the next tile's first chunk lands during the current tile's last), the
+// bias is staged once, and the next tile's row positions -- a chain of dependent loads (list entry -> utterance ->
+// lattice offsets, lengths, label) -- are fetched one link per third of the current tile's chunks, so no tile starts
+// with that chain or with a cold W chunk.
+template <int KS, int NB, int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2))) void joint_fwd_persist_kernel(
+    DevProblem p, JointArgs j) {
+    using WT = WTile<KS>;
+    extern __shared__ __attribute__((aligned(16))) unsigned short wsh[];
+    constexpr int ROWS = 32 * NW;
+    const int64_t n = list_len(j);
+    const int64_t ntiles = (n + ROWS - 1) / ROWS;
+    int64_t tile = blockIdx.x;
+    if (tile >= ntiles) return;
+    const int lane = threadIdx.x & 63, half = lane >> 5;
+    const int V = p.V, blank = p.blank;
+    const int nch = (V + 31) / 32;
+    const float *bias = load_bias<KS, NB>(j, V, wsh);
+    auto row_of = [&](int64_t t) { return t * ROWS + (threadIdx.x >> 6) * 32 + (lane & 31); };
+    int c_issue = 0, b_issue = 0, b_use = 0;
+    auto stage_next = [&]() {
+        WT::template stage<NW>(j, V, c_issue, wsh + b_issue * WT::ELEMS);
+        c_issue = c_issue + 1 == nch ? 0 : c_issue + 1;
+        b_issue = b_issue + 1 == NB ? 0 : b_issue + 1;
+    };
+#pragma unroll
+    for (int k = 0; k < NB - 1; ++k) stage_next();
+    RowPos q = row_pos(p, j, row_of(tile));
+    __syncthreads();  // bias in LDS
+    const int sA = 0, sB = nch / 3, sC = (2 * nch) / 3;
+    const f2 l2e = {kLog2e, kLog2e};
+    for (;;) {
+        bf16x8 bfr[KS];
+        build_act<KS, false>(j, q, half, row_of(tile), bfr);
+        const int64_t inext = row_of(tile + gridDim.x);
+        const bool vnext = inext < n;
+        int ncol = 0, ns = 0, nb = 0;
+        RowPos qn{false, 0, 0, 0, 1, 0, -1, 0};
+        float m = NEG_INF_F, sum = 0.0f, zb = 0.0f, ze = 0.0f;
+        bool fb = false, fe = false;
+        for (int c = 0; c < nch; ++c) {
+            wait_dma();
+            __builtin_amdgcn_s_barrier();
+            stage_next();
+            const f32x16 acc = WT::template mma<2>(wsh + b_use * WT::ELEMS, bfr, lane);
+            b_use = b_use + 1 == NB ? 0 : b_use + 1;
+            f2 z[8];
+            logits2(acc, bias, c, half, z);
+            float cm = fmaxf(z[0].x, z[0].y);
+#pragma unroll
+            for (int k = 1; k < 8; ++k) cm = max3(cm, z[k].x, z[k].y);
+            const float mn = fmaxf(m, cm);
+            const float mr = (mn == NEG_INF_F) ? 0.0f : mn;
+            const f2 nb2 = {-mr * kLog2e, -mr * kLog2e};
+            f2 s2 = {0.0f, 0.0f};
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const f2 t = fma2(z[k], l2e, nb2);
+                s2 = add2(s2, (f2){fast_exp2(t.x), fast_exp2(t.y)});
+            }
+            sum = sum * fast_exp2((m - mr) * kLog2e) + (s2.x + s2.y);
+            m = mn;
+            const int jb = blank - 32 * c;  // wave-uniform: one chunk holds the blank
+            if (jb >= 0 && jb < 32) {
+                const int rb = acc_reg_of(jb, half);
+                if (rb >= 0) {
+                    zb = tree_pick(z, rb);
+                    fb = true;
+                }
+            }
+            const int jl = q.lab - 32 * c;
+            const int rl = acc_reg_of(jl & 31, half);
+            const bool mine = q.lab >= 0 && jl >= 0 && jl < 32 && rl >= 0;
+            if (__ballot(mine)) {
+                const float x = tree_pick(z, rl);
+                if (mine) {
+                    ze = x;
+                    fe = true;
+                }
+            }
+            // the next tile's row positions, one dependent link at a time
+            if (c == sA && vnext) {
+                ncol = j.lcol[inext];
+                ns = j.ls[inext];
+            }
+            if (c == sB && vnext) nb = p.col_b[ncol];
+            if (c == sC && vnext) {
+                qn.valid = true;
+                qn.s = ns;
+                qn.b = nb;
+                qn.t = (int)(ncol - p.col_off[nb]);
+                qn.T = p.T[nb];
+                qn.S = p.S[nb];
+                qn.row = p.row_off[nb] + (int64_t)qn.t * (qn.S + 1) + ns;
+                const int l = ns < qn.S ? p.labels[(int64_t)nb * p.label_stride + ns] : -1;
+                qn.lab = (ns < qn.S && (unsigned)l >= (unsigned)p.V) ? -2 : l;
+            }
+        }
+        const float m2 = __shfl_xor(m, 32), s2 = __shfl_xor(sum, 32);
+        const float zb2 = __shfl_xor(zb, 32), ze2 = __shfl_xor(ze, 32);
+        const int fb2 = __shfl_xor((int)fb, 32), fe2 = __shfl_xor((int)fe, 32);
+        const float mn = fmaxf(m, m2);
+        const float mr = (mn == NEG_INF_F) ? 0.0f : mn;
+        sum = sum * fast_exp2((m - mr) * kLog2e) + s2 * fast_exp2((m2 - mr) * kLog2e);
+        if (!fb && fb2) zb = zb2;
+        if (!fe && fe2) ze = ze2;
+        if (q.valid && half == 0) {
+            const double den = -(double)mn - log_row_sum(sum);
+            p.den[q.row] = (float)den;
+            p.lp[q.row] =
+                Lp{(double)zb + den, (q.lab >= 0 ? (double)ze : (q.lab == -2 ? __builtin_nan("") : 0.0)) + den};
+        }
+        tile += gridDim.x;
+        if (tile >= ntiles) break;
+        q = qn;
+    }
+    wait_dma();  // the stream's last DMA lands before the workgroup's LDS is released
+}
+
 template <int KS, int NB, int NW, int RG>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2))) void joint_bwd_kernel(DevProblem p,
                                                                                              JointArgs j) {
@@ -1432,9 +1552,29 @@ static hipError_t launch_pipe(const DevProblem &p, const JointArgs &j, hipStream
     return hipGetLastError();
 }
 
+// the persistent 8-wave forward: one workgroup per CU
+template <int KS>
+static hipError_t launch_persist(const DevProblem &p, const JointArgs &j, hipStream_t stream) {
+    const size_t lds = 2 * sizeof(unsigned short) * WTile<KS>::ELEMS + sizeof(float) * ((p.V + 31) / 32 * 32);
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    const int64_t tiles = (j.n + 255) / 256;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(tiles, cu_count()));
+    auto kern = joint_fwd_persist_kernel<KS, 2, 8>;
+    if (lds > 65536) {
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    kern<<<grid, 512, lds, stream>>>(p, j);
+    return hipGetLastError();
+}
+
 template <int KS, bool BWD>
 static hipError_t launch_kb(const DevProblem &p, const JointArgs &j, hipStream_t stream) {
     constexpr int kDefault = KS > 32 ? 32 : BWD ? Tuning{}.joint_bwd_mfma : Tuning{}.joint_mfma;
+    if constexpr (!BWD && (kVariants || Tuning{}.joint_fwd_persist)) {
+        if (tuning().joint_fwd_persist) return launch_persist<KS>(p, j, stream);
+    }
     if constexpr (!BWD && KS <= 32 && (kVariants || Tuning{}.joint_pipe)) {
         if (tuning().joint_pipe) return launch_pipe<KS>(p, j, stream);
     }

@@ -252,7 +252,7 @@ def test_joint_four_wave_workgroups_bit_identical(dev, H, V):
 
 
 @pytest.mark.parametrize("tile", ["joint_mfma=16", "joint_bwd_mfma=32", "joint_ring=4", "joint_ring=8", "joint_pipe=1", "joint_pipe=2", "joint_pipe=3",
-                                  "joint_fwd_opt=1", "joint_fwd_opt=2", "joint_fwd_opt=3"])
+                                  "joint_fwd_opt=1", "joint_fwd_opt=2", "joint_fwd_opt=3", "joint_fwd_persist=1"])
 @pytest.mark.parametrize("H,V,blank", [(512, 1024, 517), (512, 1000, 0), (256, 17, 16), (128, 64, 37), (384, 130, 129),
                                        (256, 2, 1)])
 def test_joint_tile_variants_vs_host(dev, H, V, blank, tile):
@@ -279,8 +279,9 @@ def test_joint_tile_variants_vs_host(dev, H, V, blank, tile):
         assert torch.all(de[b, T[b]:] == 0) and torch.all(dp[b, S[b] + 1:] == 0)
 
 
+@pytest.mark.parametrize("knob", ["joint_pipe=1", "joint_fwd_persist=1"])
 @pytest.mark.parametrize("H,V", [(512, 1024), (256, 100), (384, 32)])
-def test_joint_pipe_many_tiles_per_workgroup(dev, H, V):
+def test_joint_pipe_many_tiles_per_workgroup(dev, H, V, knob):
     """joint_pipe = 1 with more 128-row tiles than CUs (each persistent workgroup walks several, building every next
     tile's activations during the current one's MFMAs): costs and all gradients against the 8-wave forward within this
     file's tolerances (blank / label logits come from dot products there, from the accumulators here)."""
@@ -289,7 +290,8 @@ def test_joint_pipe_many_tiles_per_workgroup(dev, H, V):
     blank = V // 2
     labels = np.where(labels == blank, (blank + 1) % V, labels).astype(np.int32)
     ref = run_joint(jm, dev, enc, pred, w, bias, labels, T, S, blank=blank)
-    with knobs(joint_pipe=1):
+    k, v = knob.split("=")
+    with knobs(**{k: int(v)}):
         got = run_joint(jm, dev, enc, pred, w, bias, labels, T, S, blank=blank)
     inband = sum(min(t, s) - max(0, t - (tt - s)) + 1 for tt, s in zip(T.tolist(), S.tolist()) for t in range(tt))
     assert inband > 300 * 128, inband  # more 128-row tiles than the 256 workgroups
