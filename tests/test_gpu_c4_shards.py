@@ -81,7 +81,7 @@ def test_config_c4_shard_rows_and_oracle(c4_shard):
 
 @pytest.mark.skipif(os.environ.get("MRNNT_FULL_BATCH", "0") != "1",
                     reason="opt-in (MRNNT_FULL_BATCH=1): every configs[3] cost against the oracle, minutes on the "
-                           "box's 16 cores; its last run is recorded under profiles/r02/tests/")
+                           "box's 16 cores; its last run is recorded under profiles/r03/tests/")
 def test_config_c4_all_costs_match_oracle(c4_shard):
     """Every cost of the shard against the fp64 oracle (costs only), in groups of 16 utterances."""
     c, V = c4_shard["costs"], c4_shard["V"]

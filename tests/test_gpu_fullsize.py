@@ -99,7 +99,7 @@ def test_subset_matches_oracle(headline):
 
 @pytest.mark.skipif(os.environ.get("MRNNT_FULL_BATCH", "0") != "1",
                     reason="opt-in (MRNNT_FULL_BATCH=1): all 64 headline utterances against the oracle, ~2 min on "
-                           "the box's 16 cores; its last run is recorded under profiles/r02/tests/")
+                           "the box's 16 cores; its last run is recorded under profiles/r03/tests/")
 def test_full_batch_matches_oracle(headline):
     """Every utterance of the headline batch (64 x 201,000 rows x 1024) against the fp64 oracle, in groups of 16
     utterances (OpenMP over utterances on the box's CPU share): costs 1e-4 relative, grads 1e-4 absolute."""
