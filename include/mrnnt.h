@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MRNNT_VERSION 7
+#define MRNNT_VERSION 8
 
 /* acts / grads element types */
 #define MRNNT_F32 0
@@ -201,6 +201,8 @@ typedef struct mrnnt_joint_problem {
     int64_t hact_ld;         /* (version 3) Hact row stride in elements, 0 = H; a multiple of 8 > H makes
                                 mrnnt_joint_backward write columns H .. hact_ld-1 of every row as [1, 0, ...],
                                 so that the dweight GEMM G^T Hact also yields dbias = sum_i G[i] in column H */
+    float *dbias;            /* (version 8) device fp32 [V] or NULL: mrnnt_joint_backward ADDS sum_i G[i] (the fp32
+                                values before their bf16 rounding) into it -- zero it first; H <= 512 only */
 } mrnnt_joint_problem;
 
 RNNTStatus mrnnt_joint_workspace_size(const mrnnt_joint_problem *p, size_t *bytes);

@@ -883,6 +883,8 @@ RNNTStatus mrnnt_joint_backward(const mrnnt_joint_problem *jp, void *ws, int64_t
     j.bt_idx = bt_idx;
     j.bs_idx = bs_idx;
     j.scale = grad_scale;
+    j.dbias = jp->dbias;
+    if (jp->dbias && jp->H > 512) return fail(RNNT_STATUS_INVALID_VALUE, "dbias in the gradient pass needs H <= 512");
     const hipError_t e = timed(K_JOINT_BWD, stream, [&] { return launch_joint_backward(d, j, stream); });
     if (e != hipSuccess) return fail_hip(e, "joint gradient kernel");
     return RNNT_STATUS_SUCCESS;

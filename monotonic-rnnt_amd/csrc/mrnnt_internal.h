@@ -93,6 +93,7 @@ struct JointArgs {
     int64_t *bt_idx;             // [n] b * enc_sb / H + t   (row of enc viewed as [B * T_slots, H])
     int64_t *bs_idx;             // [n] b * pred_sb / H + s  (row of pred viewed as [B * S_slots, H])
     const float *scale;          // [B] upstream dL/dcost or nullptr
+    float *dbias;                // [V] fp32: the backward adds sum_i G[i] into it (16x16x32 backward only), or nullptr
 };
 
 // Row lists over the lattice: mode 0 = every in-band row, mode 1 = live rows (needs alpha/beta/ll).

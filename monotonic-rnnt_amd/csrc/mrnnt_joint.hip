@@ -881,6 +881,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     }
     const int V = p.V, blank = p.blank;
     const float *bias = load_bias<KS, NB>(j, V, wsh);
+    // dbias: column sums of this workgroup's G in LDS behind the bias (launch_kt sizes the LDS for it)
+    const int vpad = (V + 31) / 32 * 32;
+    float *dbl = const_cast<float *>(bias) + vpad;
+    if (j.dbias)
+        for (int v = threadIdx.x; v < vpad; v += blockDim.x) dbl[v] = 0.0f;
     __syncthreads();
     bf16x8 bfr[2][K32];
     build_row<K32, 32, true>(j, q[0], 8 * g, i0, bfr[0]);
@@ -898,6 +903,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
                               *reinterpret_cast<const f4 *>(bias + 32 * c + 16 + 4 * g)};
             const int jb = blank - 32 * c;
             const bool hb = jb >= 0 && jb < 32 && ((jb >> 2) & 3) == g;
+            float cs[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};  // dbias: this lane's two rows
 #pragma unroll
             for (int rt = 0; rt < 2; ++rt) {
                 float x[8];
@@ -916,6 +922,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
                     for (int vt = 0; vt < 2; ++vt) {
                         const int v0 = 32 * c + 16 * vt + 4 * g;
                         const float e4[4] = {x[4 * vt] * s, x[4 * vt + 1] * s, x[4 * vt + 2] * s, x[4 * vt + 3] * s};
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) cs[4 * vt + e] += e4[e];
                         if (vec_out && v0 + 3 < V) {
                             *reinterpret_cast<uint2 *>(grow[rt] + v0) =
                                 make_uint2(IoBF16::pack2(e4[0], e4[1]), IoBF16::pack2(e4[2], e4[3]));
@@ -927,9 +935,35 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
                     }
                     if (hb) grow[rt][blank] = IoBF16::from_f((gb - rc[rt].cb) * s);
                     if (mine) grow[rt][rc[rt].lab] = IoBF16::from_f((gl - rc[rt].ce) * s);
+                    if (j.dbias) {  // the two corrected entries: the column sums above hold them uncorrected
+                        if (hb) atomicAdd(&dbl[blank], -rc[rt].cb * s);
+                        if (mine) atomicAdd(&dbl[rc[rt].lab], -rc[rt].ce * s);
+                    }
+                }
+            }
+            if (j.dbias) {  // sum the 16 lanes of each lane group (one DPP row: rows of the tile), lane 15 adds to LDS
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    float v = cs[k];
+                    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x111, 0xf, 0xf, true));
+                    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x112, 0xf, 0xf, true));
+                    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x114, 0xf, 0xf, true));
+                    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x118, 0xf, 0xf, true));
+                    cs[k] = v;
+                }
+                if (c16 == 15) {
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) atomicAdd(&dbl[32 * c + 16 * (k >> 2) + 4 * g + (k & 3)], cs[k]);
                 }
             }
         });
+    if (j.dbias) {
+        __syncthreads();
+        for (int v = threadIdx.x; v < V; v += blockDim.x) {
+            const float t = dbl[v];
+            if (t != 0.0f) atomicAdd(&j.dbias[v], t);
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -1487,7 +1521,9 @@ static hipError_t launch_knw(const DevProblem &p, const JointArgs &j, size_t lds
 // (joint_ring = 4 / 8) of the 32x32 tile.
 template <int KS, int MF, bool BWD>
 static hipError_t launch_kt(const DevProblem &p, const JointArgs &j, hipStream_t stream) {
-    const size_t bias = sizeof(float) * ((p.V + 31) / 32 * 32);
+    // the 16x16x32 backward keeps its dbias column sums behind the bias
+    const size_t bias = sizeof(float) * ((p.V + 31) / 32 * 32) * (MF == 16 && BWD ? 2 : 1);
+    if (j.dbias && !(MF == 16 && BWD)) return hipErrorInvalidValue;
     const size_t tile = sizeof(unsigned short) * WTile<KS>::ELEMS;
     if constexpr (kVariants) {
         if (tuning().joint_nbuf >= 3 && 3 * tile + bias <= 160 * 1024)
@@ -1590,8 +1626,8 @@ static hipError_t launch_kh(const DevProblem &p, const JointArgs &j, bool bwd, h
     return bwd ? launch_kb<KS, true>(p, j, stream) : launch_kb<KS, false>(p, j, stream);
 }
 
-size_t joint_min_lds_bytes(int H, int V) {
-    return 2 * sizeof(unsigned short) * 32 * (size_t)H + sizeof(float) * (((size_t)V + 31) / 32 * 32);
+size_t joint_min_lds_bytes(int H, int V) {  // the 16x16x32 backward (H <= 512) adds its dbias column sums
+    return 2 * sizeof(unsigned short) * 32 * (size_t)H + (H <= 512 ? 2 : 1) * sizeof(float) * (((size_t)V + 31) / 32 * 32);
 }
 
 static hipError_t launch_joint(const DevProblem &p, const JointArgs &j, bool bwd, hipStream_t stream) {

@@ -97,6 +97,7 @@ class MrnntJointProblem(ctypes.Structure):
         ("align_blank", ctypes.c_int),
         ("max_shift", ctypes.c_int),
         ("hact_ld", ctypes.c_int64),
+        ("dbias", ctypes.c_void_p),
     ]
 
 
@@ -155,8 +156,8 @@ def _bind(path: str, dev: bool = False) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.mrnnt_version() < 7:
-        raise ImportError(f"{path} is a stale build (ABI version {lib.mrnnt_version()} < 7); "
+    if lib.mrnnt_version() < 8:
+        raise ImportError(f"{path} is a stale build (ABI version {lib.mrnnt_version()} < 8); "
                           "rebuild with `make -C monotonic-rnnt_amd`")
     return lib
 

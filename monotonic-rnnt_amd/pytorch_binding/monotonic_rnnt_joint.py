@@ -112,7 +112,7 @@ class _JointPrepared:
                                              1 if with_beta else 0, self.stream()), "mrnnt_joint_forward")
         return costs, ws
 
-    def backward_rows(self, ws, grad_scale, with_index=False, bias_column=False):
+    def backward_rows(self, ws, grad_scale, with_index=False, bias_column=False, dbias=None):
         """The fused gradient pass over the live rows: (G [n, V], Hact [n, H]) and, with_index, the enc / pred
         row of each live row (bt_idx, bs_idx). bias_column: Hact is [n, _HACT_LD[H]] with column H = 1 (and zeros
         after it), so G^T Hact carries dbias = sum_i G[i] in column H (no separate pass over G)."""
@@ -132,6 +132,7 @@ class _JointPrepared:
                 bs = torch.empty(max(1, n), dtype=torch.int64, device=self.device)
             if grad_scale is not None:
                 grad_scale = grad_scale.detach().to(self.device, torch.float32).contiguous()
+            self.problem.dbias = _vp(dbias)  # the gradient pass adds sum_i G[i] into it (zeroed by the caller)
             _L.check(lib.mrnnt_joint_backward(ctypes.byref(self.problem), _vp(ws), n, _vp(grad_scale), _vp(G),
                                               _vp(Hact), _vp(bt), _vp(bs), self.stream()), "mrnnt_joint_backward")
         if with_index:
@@ -150,6 +151,17 @@ class _JointPrepared:
 
 
 _BIAS_SUM = os.environ.get("MRNNT_JOINT_BIAS_SUM") == "1"
+
+
+def _bwd_sums_columns(H):
+    """Whether the gradient pass runs on the 16x16x32 tile, which can add sum_i G[i] into dbias: H <= 512 (the
+    product library always; the development build unless its joint_bwd_mfma knob selects the 32x32x16 tile)."""
+    if H > 512:
+        return False
+    lib = _L.load()
+    if hasattr(lib, "mrnnt_tune") and lib.mrnnt_tune.restype is ctypes.c_int:
+        return _L.tune("joint_bwd_mfma") == 16
+    return True
 # Hact row stride when it carries the dbias ones column: the widths at which hipBLASLt's split-K dW GEMM (n = 3.9 M
 # live rows, V = 1024) costs least over the plain H-wide one -- some widths pick much slower kernels
 # (profiles/r01/joint_bias_column_gemm.json). H = 512 keeps the separate G.sum: its cheapest wider GEMM (640) costs
@@ -193,7 +205,10 @@ class MonotonicRNNTJointFunction(torch.autograd.Function):
         need_b = ctx.bias_dtype is not None and ctx.needs_input_grad[3]
         # dbias rides on the dweight GEMM (a ones column in Hact); MRNNT_JOINT_BIAS_SUM=1: a separate G.sum (A/B)
         bias_col = need_b and ctx.needs_input_grad[2] and not _BIAS_SUM and prep.H in _HACT_LD
-        G, Hact = prep.backward_rows(ws, grad_costs, bias_column=bias_col)
+        # otherwise the 16x16x32 gradient pass (H <= 512) sums G's columns itself (no separate pass over G)
+        fused_b = need_b and not bias_col and not _BIAS_SUM and _bwd_sums_columns(prep.H)
+        db = torch.zeros(prep.V, dtype=torch.float32, device=prep.device) if fused_b else None
+        G, Hact = prep.backward_rows(ws, grad_costs, bias_column=bias_col, dbias=db)
         d_enc = d_pred = d_w = d_b = None
         H = prep.H
         if ctx.needs_input_grad[2]:
@@ -201,7 +216,9 @@ class MonotonicRNNTJointFunction(torch.autograd.Function):
             d_w = dw[:, :H].to(prep.weight.dtype)
             if bias_col:
                 d_b = dw[:, H].to(ctx.bias_dtype)
-        if need_b and not bias_col:
+        if fused_b:
+            d_b = db.to(ctx.bias_dtype)
+        elif need_b and not bias_col:
             d_b = G.sum(0, dtype=torch.float32).to(ctx.bias_dtype)
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
             dH = G @ prep.weight  # [n, H] bf16 (hipBLASLt)

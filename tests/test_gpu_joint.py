@@ -240,15 +240,18 @@ def test_joint_alignment_restricted(jop, dev, k):
 @pytest.mark.parametrize("H,V", [(512, 256), (256, 1000), (128, 64)])
 def test_joint_four_wave_workgroups_bit_identical(dev, H, V):
     """joint_nw = 4 (development build): two 4-wave workgroups per CU instead of one of 8 -- the same tiles, chunk
-    order and epilogues per wave, so the same bits."""
+    order and epilogues per wave, so the same bits (d_bias aside: at H = 512 the gradient pass adds its column sums
+    with fp32 atomics, whose order is not fixed -- equal to ~1e-6 relative)."""
     import monotonic_rnnt_joint as jm
     enc, pred, w, bias, labels, T, S = make_case(7 + H, 5, (10, 60), 20, H, V)
     ref = run_joint(jm, dev, enc, pred, w, bias, labels, T, S)
     with knobs(joint_nw=4):
         got = run_joint(jm, dev, enc, pred, w, bias, labels, T, S)
     assert np.array_equal(ref[0], got[0])
-    for a, b in zip(ref[1:], got[1:]):
+    for a, b in zip(ref[1:4], got[1:4]):
         assert torch.equal(a, b)
+    db_ref, db = ref[4].double().cpu(), got[4].double().cpu()
+    assert (db - db_ref).abs().max().item() <= 1e-6 * db_ref.abs().max().item() + 1e-7
 
 
 @pytest.mark.parametrize("tile", ["joint_mfma=16", "joint_bwd_mfma=32", "joint_ring=4", "joint_ring=8", "joint_pipe=1", "joint_pipe=2", "joint_pipe=3",
