@@ -151,6 +151,18 @@ class _JointPrepared:
 
 
 _BIAS_SUM = os.environ.get("MRNNT_JOINT_BIAS_SUM") == "1"
+# dbias source per H: the 16x16x32 gradient pass sums G's columns at H = 256, 384, 512 (measured faster than the
+# ones column at 256 / 384, profiles/r03/joint/dbias/); the ones column stays at H = 128 (the pass's column sums cost
+# more there) and H = 640 (32x32x16 gradient pass). MRNNT_JOINT_DBIAS=pass / column forces one (A/B).
+_DBIAS_MODE = os.environ.get("MRNNT_JOINT_DBIAS", "")
+
+
+def _dbias_in_pass(H):
+    if _DBIAS_MODE == "column" and H in _HACT_LD:
+        return False
+    if not _bwd_sums_columns(H):
+        return False
+    return _DBIAS_MODE == "pass" or H >= 256
 
 
 def _bwd_sums_columns(H):
@@ -204,8 +216,9 @@ class MonotonicRNNTJointFunction(torch.autograd.Function):
         prep, ws = ctx.prep, ctx.saved_tensors[3]
         need_b = ctx.bias_dtype is not None and ctx.needs_input_grad[3]
         # dbias rides on the dweight GEMM (a ones column in Hact); MRNNT_JOINT_BIAS_SUM=1: a separate G.sum (A/B)
-        bias_col = need_b and ctx.needs_input_grad[2] and not _BIAS_SUM and prep.H in _HACT_LD
-        # otherwise the 16x16x32 gradient pass (H <= 512) sums G's columns itself (no separate pass over G)
+        in_pass = need_b and not _BIAS_SUM and _dbias_in_pass(prep.H)
+        bias_col = need_b and ctx.needs_input_grad[2] and not _BIAS_SUM and prep.H in _HACT_LD and not in_pass
+        # the 16x16x32 gradient pass (H <= 512) sums G's columns itself: no separate pass over G
         fused_b = need_b and not bias_col and not _BIAS_SUM and _bwd_sums_columns(prep.H)
         db = torch.zeros(prep.V, dtype=torch.float32, device=prep.device) if fused_b else None
         G, Hact = prep.backward_rows(ws, grad_costs, bias_column=bias_col, dbias=db)
