@@ -122,9 +122,13 @@ def parse():
     ap.add_argument("--graph", action="store_true",
                     help="capture forward + backward once in a HIP graph and time its replays (host-launch-bound "
                          "sizes such as configs[1]); per-kernel times then come from eager steps after the timing")
-    ap.add_argument("--device-lengths", action="store_true",
-                    help="pass input / label lengths as GPU tensors (the reference's calling convention, "
-                         "monotonic_rnnt.cu:85-88): planned without reading them back, lattice built on the device")
+    ap.add_argument("--host-lengths", action="store_true",
+                    help="time the steps with input / label lengths as host tensors (planned exactly on the host); "
+                         "the default passes them as GPU tensors, the reference's calling convention "
+                         "(monotonic_rnnt.cu:85-88: planned without reading them back, lattice built on the device). "
+                         "The other form is timed after the measured steps in the same process (lengths_ab)")
+    ap.add_argument("--device-lengths", action="store_true", help=argparse.SUPPRESS)  # (the default; kept for old scripts)
+    ap.add_argument("--no-lengths-ab", action="store_true", help="skip timing the other lengths form")
     ap.add_argument("--shard", default=None, metavar="R/N",
                     help="time only shard R of the N-way sharded config in this one process (strong-scaling "
                          "emulation on one GPU: the sharded path has no data-path collective; tools/shard_scaling.py)")
@@ -283,11 +287,12 @@ def run(args, world):
         align = torch.from_numpy(al_np).to(dev)
         workload += f", alignment-restricted (k={args.align_k}, labels evenly spaced)"
 
-    T_t, S_t = torch.from_numpy(T), torch.from_numpy(S)
-    if args.device_lengths:
-        T_t, S_t = T_t.to(dev), S_t.to(dev)
-        workload += ", device-resident lengths"
+    T_h, S_h = torch.from_numpy(T), torch.from_numpy(S)
+    T_g, S_g = T_h.to(dev), S_h.to(dev)
+    device_lengths = not args.host_lengths
+    T_t, S_t = (T_g, S_g) if device_lengths else (T_h, S_h)
     prof_steps = min(args.steps, 100) if args.graph else args.steps  # steps the per-kernel times cover
+    lengths_ab = None
     if args.graph and mode != "resident":
         raise SystemExit("--graph needs a resident config")
     if mode == "resident":
@@ -299,8 +304,8 @@ def run(args, world):
         acts.requires_grad_(True)
         torch.cuda.synchronize()
 
-        def loss_and_grad():
-            costs = op.monotonic_rnnt_loss(acts, labels_dev, T_t, S_t, align, args.align_k or 0, blank_label=0)
+        def loss_and_grad(Tl, Sl):
+            costs = op.monotonic_rnnt_loss(acts, labels_dev, Tl, Sl, align, args.align_k or 0, blank_label=0)
             loss = costs.sum()
             loss.backward()
             return loss
@@ -310,14 +315,15 @@ def run(args, world):
                 tot = coll(loss.detach().clone())
                 dist.all_reduce(tot)  # the one RCCL exchange of the path: 4 bytes over xGMI
 
-        def eager_step():
-            acts.grad = None
-            loss = loss_and_grad()
-            reduce(loss)
-            return loss
+        def make_steps(Tl, Sl):
+            def eager_step():
+                acts.grad = None
+                loss = loss_and_grad(Tl, Sl)
+                reduce(loss)
+                return loss
 
-        step = eager_step
-        if args.graph:
+            if not args.graph:
+                return eager_step, eager_step
             # forward + backward captured once in a HIP graph (torch.cuda.graph) and replayed: no host work per
             # step beyond one graph launch; acts.grad lives in the graph's pool and is rewritten by every replay
             side = torch.cuda.Stream(dev)
@@ -329,35 +335,55 @@ def run(args, world):
             acts.grad = None
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
-                g_loss = loss_and_grad()
+                g_loss = loss_and_grad(Tl, Sl)
 
-            def step():
+            def replay_step():
                 graph.replay()
                 reduce(g_loss)
                 return g_loss
 
+            return replay_step, eager_step
+
+        def timed_steps(step, n):
+            torch.cuda.synchronize()
+            barrier()
+            t0 = time.perf_counter()
+            for _ in range(n):
+                loss = step()
+            torch.cuda.synchronize()
+            barrier()
+            return time.perf_counter() - t0, loss
+
+        step, eager_step = make_steps(T_t, S_t)
         for _ in range(args.warmup):
             step()
         torch.cuda.synchronize()
         barrier()
         L.profile_enable(not args.graph)
-        torch.cuda.synchronize()
-        barrier()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            loss = step()
-        torch.cuda.synchronize()
-        barrier()
-        elapsed = time.perf_counter() - t0
+        elapsed, loss = timed_steps(step, args.steps)
         loss_val = loss.detach().reshape(1).double()
         if args.graph:  # replays launch no kernels from the host: per-kernel times from eager steps after timing
             L.profile_enable(True)
             for _ in range(prof_steps):
                 eager_step()
             torch.cuda.synchronize()
+        prof_main = L.profile_read()
+        L.profile_enable(False)
+        if not args.no_lengths_ab:
+            # the other lengths form, same process, buffers and step count, after the measured steps (not in `value`)
+            other = (T_h, S_h) if device_lengths else (T_g, S_g)
+            step_o, _ = make_steps(*other)
+            for _ in range(args.warmup):
+                step_o()
+            el_o, _ = timed_steps(step_o, args.steps)
+            el_m, _ = timed_steps(step, args.steps)  # this form again, right after it (drift check)
+            ms = {("device" if device_lengths else "host"): round(elapsed * 1e3 / args.steps, 4),
+                  ("host" if device_lengths else "device"): round(el_o * 1e3 / args.steps, 4)}
+            lengths_ab = {"ms_per_step": ms, "measured_form_again_ms": round(el_m * 1e3 / args.steps, 4),
+                          "device_over_host": round(ms["device"] / ms["host"], 4)}
     else:
         costs_c = torch.zeros(B, dtype=torch.float32, device=dev)
-        T_d, S_d = T_t.to(dev), S_t.to(dev)
+        T_d, S_d = T_g, S_g
 
         def chunk_step(lo, hi):
             """Regenerate the chunk's logits (not timed), then one timed forward + in-place backward."""
@@ -384,13 +410,14 @@ def run(args, world):
                 elapsed += chunk_step(lo, hi)
         loss_val = costs_c.double().sum().reshape(1)
         acts = None
+        prof_main = L.profile_read()
+        L.profile_enable(False)
     # the whole batch's summed loss (every rank's share, the same all-reduce the step performs), for checks
     loss_val = coll(loss_val)
     if world > 1:
         dist.all_reduce(loss_val)
     loss_val = float(loss_val.item())
-    prof = L.profile_read()
-    L.profile_enable(False)
+    prof = prof_main
     el = coll(torch.tensor([elapsed], dtype=torch.float64, device=dev))
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -405,7 +432,7 @@ def run(args, world):
     live = 0
     for lo, hi in chunks:
         a = acts.detach() if mode == "resident" else synth(lo, hi)
-        live += live_rows(op, L, a, labels_dev[lo:hi], T_t[lo:hi], S_t[lo:hi], dev, align, args.align_k or 0)
+        live += live_rows(op, L, a, labels_dev[lo:hi], T_h[lo:hi], S_h[lo:hi], dev, align, args.align_k or 0)
     grad_bytes = (live + rows) * V * elem  # algorithmic: read live acts rows once, write every grads row once
     formula_grad_bytes = (n_band + rows) * V * elem  # SURVEY.md §8d formula: every in-band row read
     n_read = n_band if n_window is None else n_window  # rows the log-softmax pass reads
@@ -432,12 +459,14 @@ def run(args, world):
             ek = {"f32": "IoF32", "bf16": "IoBF16", "f16": "IoF16"}[args.acts_dtype]
             # the counter record belongs to this exact workload only: same config and acts dtype, and the same
             # live-row bytes per launch (an alignment band, a shard or chunking all change those)
+            # workload, measured with this very library build (its sha256)
             if (pm.get("config") == args.config and pm.get("dtype") == args.acts_dtype
                     and pm.get("kernel", "").startswith(f"grad_staged_kernel<{ek}")
-                    and pm.get("algorithmic_bytes_per_launch") == grad_bytes // n_chunks):
+                    and pm.get("algorithmic_bytes_per_launch") == grad_bytes // n_chunks
+                    and pm.get("lib_sha256") == lib_sha256(L.LIB_PATH)):
                 traffic = pm.get("hbm_bytes_per_launch")
                 traffic_source = {"file": os.path.relpath(pmc_path, ROOT), "run": pm.get("source"),
-                                  "measured_in_this_run": False}
+                                  "lib_sha256": pm.get("lib_sha256"), "measured_in_this_run": False}
         except Exception:
             traffic = None
 
@@ -468,7 +497,7 @@ def run(args, world):
                        "rows_per_gpu": rows, "inband_rows_per_gpu": n_band, "V": V,
                        "memory_mode": mode, "chunks_per_step": n_chunks,
                        "execution": "hip_graph_replay" if args.graph else "eager",
-                       "lengths": "device" if (args.device_lengths or mode != "resident") else "host",
+                       "lengths": "device" if (device_lengths or mode != "resident") else "host",
                        "rank_devices": rank_devices,
                        **({"window_rows_per_gpu": n_window} if n_window is not None else {}),
                        "parallelism": f"dp{world} (batch-sharded, one 4-byte "
@@ -496,6 +525,7 @@ def run(args, world):
                 "grad": {"avg_ms": round(g_avg, 4) if g_avg else None, "gbps": round(achieved, 1) if achieved else None},
             },
             "cpu_baseline": cpu,
+            "lengths_ab": lengths_ab,
             "grads_placement": placement_log(),
             "tune": args.tune or None,
             "loss_check": loss_val,
@@ -503,6 +533,16 @@ def run(args, world):
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def lib_sha256(path):
+    """sha256 of the product library file: a PMC record counts only for the build it was measured on."""
+    import hashlib
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
 
 
 def placement_log():

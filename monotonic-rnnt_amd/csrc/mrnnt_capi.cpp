@@ -65,10 +65,52 @@ struct Plan {
     int64_t pad_T = 0, pad_S1 = 0;
     bool align = false;
     bool dyn = false;
-    size_t off_flags = 0, flags_bytes = 0;  // the chase launch's ready flags (host lengths: 2 x 8 bytes per column)
+    size_t off_flags = 0, flags_bytes = 0;  // the chase launch's ready flags (8 bytes per column), where it can run
     size_t off_row, off_col, off_colb, off_mtmp, off_min, off_max, off_den, off_lp, off_alpha, off_beta, off_ll,
         off_llb, off_dyn, total;
 };
+
+int cu_count_of_device() {
+    static int cu_count[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    if (cu_count[dev] == 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cu_count[dev] = n;
+    }
+    return cu_count[dev];
+}
+
+// Mean frames per utterance: exact with host lengths; with device lengths the plan's lower bound on the column count
+// over B (exact when every S_b equals the label row stride), or pad_T for the padded layout.
+double mean_frames(const Plan &pl) {
+    if (!pl.dyn) return (double)pl.cols / pl.B;
+    if (pl.pad_S1) return (double)pl.pad_T;
+    return (double)((pl.N + pl.S_max) / (pl.S_max + 1)) / pl.B;
+}
+
+// The chase launch (mrnnt_chase.hip) where its shape allows it and it pays:
+// * f32 rows it has a body for, no alignment band, the halo recursion in one 4-wave workgroup (S + 1 <= 4 * 56), the
+//   lp array one buffer descriptor (N * 16 bytes < 2^31), device lengths for B <= 64 (one utterance per lane);
+// * its recursion workgroups spin while they wait, so together they should leave the chip to the producers: at most
+//   one per CU (B or 2B <= CUs). (Progress does not rely on it -- a starved recursion wave computes its columns
+//   itself -- but a launch that has to is slow.)
+// * it saves the recursion's time (~T steps of ~0.1 us) at the price of a slightly slower log-softmax pass (+5-10 %,
+//   the hand-off and the production order): taken when the recursion is at least a quarter of the pass's streaming
+//   time (configs[1]: 20 vs 22 us; the headline: 0.16 vs 6.5 ms, not taken).
+bool chase_shape_ok(const Plan &pl) {
+    if (pl.align || pl.elem != ELEM_F32 || chase_body_shape(pl.V) < 0) return false;
+    if (pl.S_max + 1 > 4 * 56 || pl.N * (int64_t)sizeof(Lp) >= ((int64_t)1 << 31)) return false;
+    if (pl.dyn && pl.B > 64) return false;
+    if (2 * pl.B > cu_count_of_device()) return false;
+    const double pass_s = (double)pl.N * pl.V * 4.0 / 6.0e12, recursion_s = mean_frames(pl) * 1.0e-7;
+    return recursion_s >= 0.25 * pass_s;
+}
+
+bool chase_pays(const Plan &pl, bool with_beta) {
+    return pl.flags_bytes && (with_beta ? 2 * pl.B : pl.B) <= cu_count_of_device();
+}
 
 RNNTStatus plan_device_lengths(const mrnnt_problem *p, Plan &q) {
     if (!p->T_dev || !p->S_dev) return fail(RNNT_STATUS_INVALID_VALUE, "device lengths are required");
@@ -165,11 +207,6 @@ RNNTStatus make_plan(const mrnnt_problem *p, Plan *pl) {
         o = align_up(o + bytes);
         return at;
     };
-    // the chase launch's ready flags (mrnnt_chase.hip; host lengths only)
-    if (!q.dyn) {
-        q.flags_bytes = sizeof(unsigned long long) * 2 * (size_t)q.cols;
-        q.off_flags = take(q.flags_bytes);
-    }
     q.off_row = take(sizeof(int64_t) * (q.B + 1));
     q.off_col = take(sizeof(int64_t) * (q.B + 1));
     q.off_colb = take(sizeof(int) * q.cols);
@@ -185,6 +222,12 @@ RNNTStatus make_plan(const mrnnt_problem *p, Plan *pl) {
     q.off_min = q.align ? take(sizeof(int) * q.cols) : 0;
     q.off_max = q.align ? take(sizeof(int) * q.cols) : 0;
     q.off_dyn = q.dyn ? take(sizeof(DynWords)) : 0;
+    // the chase launch's ready flags (mrnnt_chase.hip), one word per column (device lengths: per column of the bound),
+    // for problems whose shape can take it -- last, so no other offset depends on it
+    if (chase_shape_ok(q)) {
+        q.flags_bytes = sizeof(unsigned long long) * (size_t)q.cols;
+        q.off_flags = take(q.flags_bytes);
+    }
     q.total = o;
     *pl = q;
     return RNNT_STATUS_SUCCESS;
@@ -319,22 +362,6 @@ int streaming_grid(int64_t cols, int per_cu) {
     // every streaming kernel walks its columns grid-stride, so larger problems just take more than one turn)
     const int64_t g = per_cu <= 0 ? std::min<int64_t>(cols, 1 << 22) : (int64_t)cu_count[dev] * per_cu;
     return (int)std::max<int64_t>(1, std::min<int64_t>(g, cols));
-}
-
-// The chase launch (mrnnt_chase.hip) where it pays and is safe:
-// * its recursion workgroups spin while they wait, so together they must leave the chip room for the log-softmax
-//   workgroups they wait for: at most one per CU (B or 2B <= CUs, whatever the dispatch order);
-// * one 4-wave workgroup runs the halo recursion (S + 1 <= 4 * 56), and the lp array is one buffer descriptor
-//   (N * 16 bytes < 2^31);
-// * it saves the recursion's time (~T_max steps of ~0.1 us) at the price of a slightly slower log-softmax pass
-//   (+5-10 %, the hand-off and the production order): taken when the recursion is at least a quarter of the pass's
-//   streaming time (configs[1]: 20 vs 22 us; the headline: 0.16 vs 6.5 ms, not taken).
-bool chase_pays(const Plan &pl, bool with_beta) {
-    if ((with_beta ? 2 * pl.B : pl.B) > streaming_grid((int64_t)1 << 40, 1)) return false;
-    if (pl.S_max + 1 > 4 * 56 || pl.N * (int64_t)sizeof(Lp) >= ((int64_t)1 << 31)) return false;
-    const double elem = pl.elem == ELEM_F32 ? 4.0 : 2.0;
-    const double pass_s = (double)pl.N * pl.V * elem / 6.0e12, recursion_s = (double)pl.T_max * 1.0e-7;
-    return recursion_s >= 0.25 * pass_s;
 }
 
 // ---- profiling ---------------------------------------------------------------------------------
@@ -496,20 +523,33 @@ RNNTStatus mrnnt_forward(const mrnnt_problem *p, void *ws, size_t ws_bytes, floa
         });
         if (e != hipSuccess) return fail_hip(e, "alignment band kernels");
     }
-    // host lengths, no alignment: the forward as one launch, the recursion chasing the log-softmax (mrnnt_chase.hip),
-    // where it has a body for these rows and pays (chase_pays)
-    if (!pl.dyn && !pl.align && tuning().chase && chase_body(d, pl.elem) >= 0 && chase_pays(pl, with_beta)) {
+    // no alignment: the forward as one launch, the recursion chasing the log-softmax (mrnnt_chase.hip), where it has a
+    // body for these rows and pays (chase_pays); with device lengths the launch also plans and validates them
+    if (tuning().chase && chase_body(d, pl.elem) >= 0 && chase_pays(pl, with_beta) && (!pl.dyn || fused)) {
         ChaseArgs ca;
         ca.flags = reinterpret_cast<unsigned long long *>(w + pl.off_flags);
-        ca.cols = pl.cols;
-        ca.slots = chase_slots(d, pl.T_max, with_beta ? 1 : 0);
+        // device lengths: the slots come from the lengths on the device; the grid from the plan's column bound
+        // (rows / (label stride + 1), exact when every S_b equals the stride; + B for the middle frames of odd T)
+        const int64_t slot_bound = pl.dyn ? (pl.pad_S1 ? pl.cols : (pl.N + pl.S_max) / (pl.S_max + 1)) + pl.B
+                                          : chase_slots(pl.B, pl.T_max, with_beta ? 1 : 0);
+        ca.slots = pl.dyn ? 0 : slot_bound;
         ca.epoch = chase_epoch();
-        ca.probe = kVariants ? tuning().chase_probe : 0;
+        ca.budget = (uint32_t)std::min<int64_t>((int64_t)std::max(0, tuning().chase_wait_us) * 100, UINT32_MAX / 2);
+        ca.delay = kVariants ? (uint32_t)std::max(0, tuning().chase_delay_us) * 100u : 0u;
+        ca.stage = kVariants ? tuning().chase_stage : 1;
         const int nrec = with_beta ? 2 * pl.B : pl.B;
-        const int producers = (int)std::min<int64_t>(streaming_grid(ca.slots, tuning().chase_grid_per_cu),
+        const int producers = (int)std::min<int64_t>(streaming_grid(slot_bound, tuning().chase_grid_per_cu),
                                                      ((int64_t)1 << 22) - nrec);
+        DevProblem dc = d;
+        if (pl.dyn) {  // validation limits and the status report, as the fused log-softmax launch (walk_columns)
+            dc.s_cap = pl.S_max;
+            dc.t_cap = pl.pad_S1 ? pl.pad_T : 0;
+            dc.s1_cap = pl.pad_S1;
+            dc.scatter_above = scatter_above;
+            if ((st = status_device_ptr(p, &dc.status_host)) != RNNT_STATUS_SUCCESS) return st;
+        }
         e = timed(K_CHASE, stream, [&] {
-            return launch_chase(d, ca, pl.elem, pl.S_max, with_beta ? 1 : 0, producers, costs_dev, stream);
+            return launch_chase(dc, ca, pl.elem, pl.S_max, with_beta ? 1 : 0, producers, costs_dev, stream);
         });
         if (e != hipSuccess) return fail_hip(e, "chase kernel");
         return RNNT_STATUS_SUCCESS;
@@ -963,6 +1003,9 @@ int mrnnt_profile_read(double *total_ms, int64_t *launches, int n) {
 }
 
 #ifdef MRNNT_DEVTOOLS
+// development build: columns chase recursion waves computed themselves since the last reset (mrnnt_chase.hip)
+__attribute__((visibility("default"))) unsigned long long mrnnt_chase_helped(int reset) { return chase_helped(reset != 0); }
+
 // launch knobs: exported by the development build only (libmonotonic_rnnt_amd_dev.so, `make dev`)
 __attribute__((visibility("default"))) int mrnnt_tune(const char *key, int value) {
     if (!key) return -1;
@@ -985,19 +1028,13 @@ __attribute__((visibility("default"))) int mrnnt_tune(const char *key, int value
     else if (!std::strcmp(key, "nt_store")) slot = &t.nt_store;
     else if (!std::strcmp(key, "dyn_fused")) slot = &t.dyn_fused;
     else if (!std::strcmp(key, "chase")) slot = &t.chase;
-    else if (!std::strcmp(key, "chase_depth")) slot = &t.chase_depth;
-    else if (!std::strcmp(key, "chase_probe")) slot = &t.chase_probe;
+    else if (!std::strcmp(key, "chase_wait_us")) slot = &t.chase_wait_us;
+    else if (!std::strcmp(key, "chase_stage")) slot = &t.chase_stage;
+    else if (!std::strcmp(key, "chase_delay_us")) slot = &t.chase_delay_us;
     else if (!std::strcmp(key, "chase_grid_per_cu")) slot = &t.chase_grid_per_cu;
     else if (!std::strcmp(key, "nt_load")) slot = &t.nt_load;
     else if (!std::strcmp(key, "occ_skip")) slot = &t.occ_skip;
-    else if (!std::strcmp(key, "joint_nbuf")) slot = &t.joint_nbuf;
-    else if (!std::strcmp(key, "joint_nw")) slot = &t.joint_nw;
-    else if (!std::strcmp(key, "joint_mfma")) slot = &t.joint_mfma;
     else if (!std::strcmp(key, "joint_bwd_mfma")) slot = &t.joint_bwd_mfma;
-    else if (!std::strcmp(key, "joint_ring")) slot = &t.joint_ring;
-    else if (!std::strcmp(key, "joint_pipe")) slot = &t.joint_pipe;
-    else if (!std::strcmp(key, "joint_fwd_opt")) slot = &t.joint_fwd_opt;
-    else if (!std::strcmp(key, "joint_fwd_persist")) slot = &t.joint_fwd_persist;
     if (!slot) return -1;
     const int prev = *slot;
     if (value >= 0) *slot = value;

@@ -4,115 +4,424 @@
 // frame, ~0.1 us) while the log-softmax is HBM-bound, so the recursion workgroups run beside the log-softmax
 // workgroups and consume each lattice column as soon as it is published.
 //
-// Grid: first the recursion workgroups (one per utterance and direction, B or 2B), then G log-softmax workgroups
-// that take the slots of the production order round-robin (slot si, si + G, ...). The order feeds both walks from
-// their ends: round k publishes frames k and T_b - 1 - k of every utterance (alpha walks up from frame 0, beta down
-// from T - 1), so neither walk waits for the whole pass; alpha alone (no beta): round k publishes frame k. G is a
-// few workgroups per CU, not one per slot: with every slot's workgroup resident at once the columns would share the
-// bandwidth and all land near the end; G at a time, they land in order, batch after batch.
+// Grid: first the recursion workgroups (one per utterance and direction, B or 2B), then the log-softmax (producer)
+// workgroups, which take the slots of the production order grid-stride. The order feeds both walks from their ends:
+// round k publishes frames k and T_b - 1 - k of every utterance (alpha walks up from frame 0, beta down from T - 1),
+// so neither walk waits for the whole pass; alpha alone (no beta): round k publishes frame k.
 //
-// Hand-off (cdna_hip_programming.md Guideline 16, R1): a log-softmax workgroup stores its den / lpb / lpe rows
-// write-through (sc1), every wave drains its stores, a barrier, then one lane stores the column's ready flag (one per
-// direction). A recursion wave reads a column's lp rows only after seeing its flag and only with sc1 loads
-// (mrnnt_dp.h, Chase), never from a stale L1 / L2 line. Nothing else crosses workgroups inside the launch.
+// Hand-off (cdna_hip_programming.md Guideline 16, R1): a producer workgroup stores its lp rows write-through (sc1),
+// every wave drains its stores, a barrier, then one lane stores the column's ready flag. A recursion workgroup reads
+// a column's lp rows only after seeing its flag and only with sc1 loads (L1 bypassed), never from a stale line.
 //
-// Flag words: 64-bit, in the workspace, tagged with the launch's epoch (a fresh host value per call: a producer stores
-// it, a consumer waits for exactly it), and cleared by each recursion workgroup when its walk is done -- so a graph
-// replay, whose epoch is frozen at capture, starts from cleared flags, and an eager call never needs a memset node
-// (4 us of a 90 us configs[1] step). A workspace's words that were never cleared are older epochs (distinct) or
-// unrelated bytes, which equal a fresh 64-bit epoch with probability 2^-64 per word. A wait is bounded: a recursion
-// workgroup that gives up returns NaN for its utterance.
+// Ready tags: one 64-bit flag word per lattice column in the workspace, holding the tag of the launch that published
+// it. The tag is a bijective mix of the host's per-call epoch with the launch's dispatch id (the AQL packet index of
+// its queue) and queue address, so every launch -- a HIP-graph replay included, whose kernel arguments are frozen at
+// capture -- waits for a tag no earlier launch stored: flags are never cleared, and a producer that publishes late
+// cannot mislead a later launch. (Workspace bytes that were never a flag match with probability 2^-64.)
+//
+// Progress does not depend on scheduling. A recursion wave that has waited `budget` ticks of the 100 MHz constant
+// clock for a column computes the rows it needs itself, with the producers' own column body (one wave, its rows):
+// the same bits, so the result is unchanged whoever computes them. A kernel that holds the CUs on another stream, or
+// recursion workgroups that fill the chip, make the launch slower, never wrong.
+//
+// One-wave recursion (S + 1 <= 64; configs[1]): wave 1 of the recursion workgroup is a loader. It polls the flags,
+// copies each ready frame's lp rows into an LDS ring with one LDS-DMA instruction per frame (sc1, no registers), and
+// counts them in LDS; wave 0 runs the dependent LSE chain from LDS, so no lp load on the chain waits for L2.
+//
+// Device-resident lengths (the reference's calling convention, monotonic_rnnt.cu:85-88; B <= 64): every wave holds
+// the lengths in registers (wave_lengths) and locates its utterance or its slot's column from them, the first
+// producer workgroup publishes the lattice offsets and the validation status (publish_lengths) for the gradient pass,
+// each producer writes its column's entry of the column map, and lengths that fail validation make every workgroup
+// stop: NaN costs, the status word set -- as the two-kernel path.
 //
 // Every lp value, every LSE and every store is the one the two-kernel path computes (the log-softmax bodies are
-// mrnnt_lsm.h's, the recursion passes mrnnt_dp.h's), so results are bit-identical to it.
+// mrnnt_lsm.h's, the recursion steps mrnnt_dp.h's), so results are bit-identical to it.
+#include <type_traits>
+
 #include "mrnnt_dp.h"
 #include "mrnnt_lsm.h"
 
 namespace mrnnt {
 
-template <int SM, class IO, bool NTL>
-__device__ __forceinline__ void chase_column(const DevProblem &p, const ColRef &k) {
-    constexpr int U = SM <= 1 ? 1 : (SM <= 3 ? 2 : 4);
-    constexpr bool FULL = (SM & 1) == 0;
-    if constexpr (SM == 0)
-        row16_column<IO, 1, NTL, true>(p, k);
-    else
-        lean_column<IO, U, 2, NTL, FULL, true, true>(p, k);
+extern "C" __device__ uint64_t mrnnt_llvm_dispatch_id() __asm("llvm.amdgcn.dispatch.id");
+
+#ifdef MRNNT_DEVTOOLS
+__device__ unsigned long long g_chase_helped;  // development build: columns a recursion wave computed itself
+#endif
+
+// this launch's ready tag (scalar unit): a bijection of the dispatch id for a given epoch and queue
+__device__ __forceinline__ unsigned long long launch_tag(unsigned long long epoch) {
+    uint64_t x = epoch ^ ((mrnnt_llvm_dispatch_id() + 0x9E3779B97F4A7C15ull) * 0xBF58476D1CE4E5B9ull);
+    x ^= (uint64_t)(uintptr_t)__builtin_amdgcn_queue_ptr() * 0x94D049BB133111EBull;
+    x ^= x >> 31;
+    x *= 0xD6E8FEB86659FD93ull;
+    x ^= x >> 32;
+    return x ? x : 1;
 }
 
-// SM: the log-softmax body -- 0 rows on 16-lane groups (rows of <= 64 vectors), 2 / 3 single-chunk rows of <= 128
-// vectors (U = 2), 4 / 5 of <= 256 (U = 4), even = every chunk full (the product launch_u's choices for these rows).
+__device__ __forceinline__ uint32_t clock100() { return (uint32_t)__builtin_amdgcn_s_memrealtime(); }
+
+// The log-softmax body of the chase launch. SM: 0 rows on 16-lane groups (rows of <= 64 vectors), 2 / 3
+// single-chunk rows of <= 128 vectors (U = 2), 4 / 5 of <= 256 (U = 4), even = every chunk full (the product
+// launch_u's choices for these rows). NWV / wv / [rlo, rhi]: the producers (4 waves, every row) or one wave's
+// self-help (its rows; R = 1: the same per-row arithmetic with fewer registers live beside the recursion).
+template <int SM, class IO, bool NTL, int NWV>
+__device__ __forceinline__ void chase_column(const DevProblem &p, const ColRef &k, int wv = -1, int rlo = 0,
+                                             int rhi = 1 << 30) {
+    constexpr int U = SM <= 1 ? 1 : (SM <= 3 ? 2 : 4);
+    constexpr bool FULL = (SM & 1) == 0;
+    constexpr int R = NWV == 1 ? 1 : 2;
+    if constexpr (SM == 0)
+        row16_column<IO, 1, NTL, true, NWV>(p, k, wv, rlo, rhi);
+    else
+        lean_column<IO, U, R, NTL, FULL, true, true, NWV>(p, k, wv, rlo, rhi);
+}
+
+// A recursion wave's self-help: column t of its utterance, rows [rlo, rhi], computed by this wave and stored
+// write-through like a producer's, then drained (the wave reads them back with sc1 loads). (Inlined: as a call, the
+// ABI's saves around it cost more registers in the whole kernel than the body does inline.)
+template <int SM, class IO, bool NTL>
+struct SelfHelp {
+    const DevProblem *p;
+    Utt u;
+    int b, rlo, rhi;
+    __device__ __forceinline__ void operator()(int t) const {
+        ColRef k;
+        k.b = b;
+        k.T = u.T;
+        k.S = u.S;
+        k.t = t;
+        k.c = u.c0 + t;
+        k.rowc = u.r0 + (int64_t)t * (u.S + 1);
+        chase_column<SM, IO, NTL, 1>(*p, k, 0, rlo, rhi);
+        drain_stores();
+#ifdef MRNNT_DEVTOOLS
+        if ((threadIdx.x & 63) == 0) atomicAdd(&g_chase_helped, 1ull);
+#endif
+    }
+};
+
+// The gate of the direct form (mrnnt_dp.h passes, Ch = Chase): a wave keeps the run of walk positions known ready
+// (rdy). At the start of every prefetch block it reads the poll it issued one block earlier -- the flags of the 64
+// positions from rdy, one vector load -- and issues the next: unconditional, so the compiler's wait for it counts the
+// lp loads issued since and does not drain them, and a wave that runs behind the producers never stalls on a poll
+// round trip. A frame beyond rdy waits in a blocking poll, for at most `budget` ticks, then is self-helped.
+template <class Help>
+struct Chase {
+    static constexpr bool kOn = true;
+    const unsigned long long *flags;  // ready flag of frame 0 of this utterance
+    unsigned long long want;          // this launch's tag
+    int T;
+    bool fwd;       // alpha walks t = 0, 1, ...; beta t = T - 1, T - 2, ...
+    int rdy;        // walk positions [0, rdy) known ready (wave-uniform)
+    int ahead_at;   // `ahead`: this lane's flag of walk position ahead_at + lane (a poll issued earlier)
+    unsigned long long ahead;
+    uint32_t budget;
+    const Help *help;
+
+    __device__ __forceinline__ Chase(const unsigned long long *f, unsigned long long w, int T_, bool forward,
+                                     uint32_t bud, const Help *h)
+        : flags(f), want(w), T(T_), fwd(forward), rdy(0), ahead_at(0), ahead(0), budget(bud), help(h) {}
+    // this lane's flag of walk position u + lane (positions past the walk read as ready)
+    __device__ __forceinline__ unsigned long long poll(int u) const {
+        const int i = u + (int)(threadIdx.x & 63);
+        return i < T ? load_wt(&flags[fwd ? i : T - 1 - i]) : want;
+    }
+    __device__ __forceinline__ int run_of(unsigned long long v) const {
+        const unsigned long long miss = ~__ballot(v == want);
+        return miss ? __builtin_ctzll(miss) : 64;
+    }
+    __device__ __forceinline__ void refresh() {
+        const int run = run_of(ahead);
+        if (ahead_at <= rdy) rdy = max(rdy, ahead_at + run);
+        ahead_at = min(rdy, T);
+        ahead = poll(ahead_at);
+    }
+    __device__ __forceinline__ void gate(int f) {
+        const int u = fwd ? f : T - 1 - f;
+        if (u < rdy) return;
+        const uint32_t t0 = clock100();
+        for (;;) {
+            const int run = run_of(poll(u));
+            if (run > 0) {
+                rdy = u + run;
+                return;
+            }
+            if (clock100() - t0 >= budget) {
+                (*help)(f);
+                rdy = u + 1;
+                return;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+};
+
+// ---- one-wave recursion with LDS-staged frames -----------------------------------------------------------------
+
+constexpr int kRing = 16;  // lp frames in the LDS ring (1 KiB each: 16 KiB, which keeps 8 workgroups per CU)
+
+struct StageLds {
+    Lp ring[kRing][64];
+    int loaded;    // walk positions [0, loaded) are in the ring (the loader wave)
+    int consumed;  // walk positions [0, consumed) have been read by the recursion wave
+};
+struct NoStage {};
+
+__device__ __forceinline__ int lds_get(const int *w) {
+    return __builtin_amdgcn_readfirstlane(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+__device__ __forceinline__ void lds_put(int *w, int v) {
+    __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Wave 1: walk position u (frame fwd ? u : T - 1 - u) into ring slot u % kRing, lane l <- lp row min(l, S) of that
+// frame. One iteration = one poll round trip: the explicit vmcnt(0) before publishing `loaded` covers every DMA
+// issued before the poll, then the DMAs of the frames the poll found ready (as far as the ring has room) are issued.
+template <class Help>
+__device__ __forceinline__ void stage_loader(const DevProblem &p, const Utt &u, bool fwd, const unsigned long long *flags,
+                                             unsigned long long want, uint32_t budget, const Help &help,
+                                             StageLds &st) {
+    const int lane = threadIdx.x & 63;
+    const int T = u.T, W = u.S + 1;
+    const unsigned col = (unsigned)min(lane, u.S);
+    const __amdgpu_buffer_rsrc_t rs = lp_rsrc(p);
+    int issued = 0;
+    uint32_t t_wait = 0;
+    bool waiting = false;
+    for (;;) {
+        const int i = issued + lane;
+        const unsigned long long v = i < T ? load_wt(&flags[fwd ? i : T - 1 - i]) : want;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the poll and every earlier DMA have landed
+        lds_put(&st.loaded, issued);
+        if (issued >= T) return;
+        const unsigned long long miss = ~__ballot(v == want);
+        int ready = issued + (miss ? __builtin_ctzll(miss) : 64);
+        if (ready == issued) {
+            const uint32_t now = clock100();
+            if (!waiting) {
+                waiting = true;
+                t_wait = now;
+            }
+            if (now - t_wait >= budget) {
+                help(fwd ? issued : T - 1 - issued);
+                ready = issued + 1;
+            } else {
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        if (ready > issued) waiting = false;
+        const int room = lds_get(&st.consumed) + kRing;
+        const int end = min(min(ready, room), T);
+        for (; issued < end; ++issued) {
+            const int t = fwd ? issued : T - 1 - issued;
+            const unsigned off = (unsigned)((u.r0 + (int64_t)t * W) * (int64_t)sizeof(Lp)) + col * (unsigned)sizeof(Lp);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)&st.ring[issued % kRing][0],
+                                                     16, off, 0, 0, kAuxSc1);
+        }
+        if (end < ready && ready > issued) __builtin_amdgcn_s_sleep(1);  // ring full: the recursion wave catches up
+    }
+}
+
+// Wave 0: walk position u's lp row from the ring (its own row; the same value the direct pass loads), P frames ahead
+template <int P>
+struct RingReader {
+    StageLds &st;
+    int avail = 0;
+    __device__ __forceinline__ explicit RingReader(StageLds &s) : st(s) {}
+    __device__ __forceinline__ Lp read(int u) {
+        while (avail <= u) {
+            avail = lds_get(&st.loaded);
+            if (avail <= u) __builtin_amdgcn_s_sleep(1);
+        }
+        asm volatile("" ::: "memory");
+        return st.ring[u % kRing][threadIdx.x & 63];
+    }
+    __device__ __forceinline__ void done(int u) {  // walk position u's slot may be refilled
+        if ((threadIdx.x & 63) == 0) lds_put(&st.consumed, u + 1);
+    }
+};
+
+// the steps of alpha_pass_halo / beta_pass_halo at NW = 1, HL = 0, lean (the same operations, so the same bits)
+template <int P>
+__device__ __forceinline__ void alpha_staged(const DevProblem &p, const Utt &u, int b, float *__restrict__ costs,
+                                             StageLds &st) {
+    const int lane = threadIdx.x & 63;
+    const int T = u.T, S = u.S, W = S + 1;
+    const bool own = lane < W;
+    RingReader<P> rr(st);
+    double a = (lane == 0) ? 0.0 : NEG_INF_D;
+    Lp q[P];
+#pragma unroll
+    for (int d = 0; d < P; ++d) q[d] = rr.read(min(d, T - 1));
+    double *ap = p.alpha + u.r0;
+    auto step = [&](int t, int d) {
+        double y = dpp_shr1_bc(a + q[d].e);  // alpha(t-1, s-1) + lpe(t, s-1), from lane s-1
+        if (lane == 0) y = NEG_INF_D;
+        a = lse2(a + q[d].b, y);
+        if (own) ap[lane] = a;
+        ap += W;
+        rr.done(t);
+        if (t + P < T) q[d] = rr.read(t + P);
+    };
+    int t0 = 0;
+    for (; t0 + P <= T; t0 += P) {
+#pragma unroll
+        for (int d = 0; d < P; ++d) step(t0 + d, d);
+    }
+#pragma unroll
+    for (int d = 0; d < P; ++d) {
+        if (t0 + d >= T) break;
+        step(t0 + d, d);
+    }
+    if (own && lane == S) {
+        p.ll[b] = a;
+        if (costs) costs[b] = (float)(-a);
+    }
+}
+
+template <int P>
+__device__ __forceinline__ void beta_staged(const DevProblem &p, const Utt &u, int b, StageLds &st) {
+    const int lane = threadIdx.x & 63;
+    const int T = u.T, S = u.S, W = S + 1;
+    const bool own = lane < W;
+    RingReader<P> rr(st);
+    double bn = (lane == S) ? 0.0 : NEG_INF_D;  // beta(T, s)
+    Lp q[P];
+#pragma unroll
+    for (int d = 0; d < P; ++d) q[d] = rr.read(min(d, T - 1));
+    double *bp = p.beta + u.r0 + (int64_t)(T - 1) * W;
+    auto step = [&](int w, int d) {  // walk position w = frame T - 1 - w
+        double carry = dpp_shl1_bc(bn);
+        if (lane == 63) carry = NEG_INF_D;
+        bn = lse2(bn + q[d].b, carry + q[d].e);
+        if (own) bp[lane] = bn;
+        bp -= W;
+        rr.done(w);
+        if (w + P < T) q[d] = rr.read(w + P);
+    };
+    int w0 = 0;
+    for (; w0 + P <= T; w0 += P) {
+#pragma unroll
+        for (int d = 0; d < P; ++d) step(w0 + d, d);
+    }
+#pragma unroll
+    for (int d = 0; d < P; ++d) {
+        if (w0 + d >= T) break;
+        step(w0 + d, d);
+    }
+    if (lane == 0) p.llb[b] = bn;
+}
+
+// ---- the launch ------------------------------------------------------------------------------------------------
+
 // NW: recursion waves (1: S + 1 <= 64, one cell per lane; 4: the halo recursion with 56 own cells per wave, S + 1 <=
-// 224). D: lp rows prefetched per lane (8: 16-byte rows, 0.8 us ahead; 16 in the development build).
-template <class IO, int SM, bool NTL, int NW, int D>
+// 224). STG (NW = 1): frames staged in LDS by a loader wave (else the direct gated loads, development A/B). D: lp rows
+// the direct form prefetches per lane. DYN: device-resident lengths.
+template <class IO, int SM, bool NTL, int NW, bool STG, bool DYN>
 __global__ __launch_bounds__(256) void chase_kernel(DevProblem p, ChaseArgs c, int with_beta, float *__restrict__ costs) {
     constexpr int HL = NW > 1 ? 8 : 0;
+    constexpr int D = 8;
     __shared__ double xh[2][8][HL > 0 ? HL : 1];
-    __shared__ int fail;
+    __shared__ typename std::conditional<STG && NW == 1, StageLds, NoStage>::type st;
     const int nrec = with_beta ? 2 * p.B : p.B;
+    const unsigned long long tag = launch_tag(c.epoch);
+    WaveLengths wl;
+    if constexpr (DYN) wl = wave_lengths(p);
     if ((int)blockIdx.x < nrec) {
         // ---- recursion workgroup ----
-        if (threadIdx.x >= 64 * NW) return;  // one-wave recursion: the other waves of the workgroup have no work
-        if constexpr (kVariants) {
-            if (c.probe == 1 || c.probe == 2) return;  // (development probes: the log-softmax side alone; no costs)
-        }
         const int b = with_beta ? (int)(blockIdx.x >> 1) : (int)blockIdx.x;
         const bool bwd = with_beta && (blockIdx.x & 1);
-        if (threadIdx.x == 0) fail = 0;
-        if (NW > 1) __syncthreads();
-        Chase ch;
-        unsigned long long *mine = c.flags + (bwd ? c.cols : 0) + p.col_off[b];
-        ch.init(mine, c.epoch, p.T[b], !bwd, &fail);
-        if constexpr (kVariants) {
-            ch.nowait = c.probe >= 3;  // (development probes: the recursion without waiting)
-            if (c.probe == 5) {        // (development probe: the two-kernel recursion pass inside this launch)
-                if (bwd)
-                    beta_pass_halo<D, NW, HL, false, 1>(p, b, xh);
-                else
-                    alpha_pass_halo<D, NW, HL, false, 1>(p, b, costs, xh);
+        Utt u;
+        if constexpr (DYN) {
+            if (!wl.ok) {  // lengths failed validation: touch no lattice array (publish_lengths reports it)
+                if (threadIdx.x == 0) {
+                    if (bwd) {
+                        p.llb[b] = __builtin_nan("");
+                    } else {
+                        p.ll[b] = __builtin_nan("");
+                        if (costs) costs[b] = __builtin_nanf("");
+                    }
+                }
                 return;
             }
-            if (c.probe == 6) {  // (development probe: the chase pass with plain lp loads, not waiting)
-                if (bwd)
-                    beta_pass_halo<D, NW, HL, false, 1, true, false>(p, b, xh, &ch);
-                else
-                    alpha_pass_halo<D, NW, HL, false, 1, true, false>(p, b, costs, xh, &ch);
-                return;
-            }
+            u.T = __builtin_amdgcn_readlane(wl.T, b);
+            u.S = __builtin_amdgcn_readlane(wl.S, b);
+            u.c0 = b ? readlane64(wl.cols, b - 1) : 0;
+            u.r0 = b ? readlane64(wl.rows, b - 1) : 0;
+        } else {
+            u = utt_of(p, b);
         }
+        const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        const unsigned long long *flags = c.flags + u.c0;
+        if constexpr (STG && NW == 1) {
+            if (threadIdx.x == 0) {  // (LDS holds whatever the CU's previous workgroup left)
+                st.loaded = 0;
+                st.consumed = 0;
+            }
+            __syncthreads();
+            if (wave >= 2) return;
+            if (wave == 1) {
+                const SelfHelp<SM, IO, NTL> help{&p, u, b, 0, u.S};
+                stage_loader(p, u, !bwd, flags, tag, c.budget, help, st);
+                return;
+            }
+            if (bwd)
+                beta_staged<4>(p, u, b, st);
+            else
+                alpha_staged<4>(p, u, b, costs, st);
+            return;
+        }
+        if (wave >= NW) return;  // one-wave direct recursion: the other waves of the workgroup have no work
+        // the rows this wave's lanes read (alpha: cells wave * 56 - HL + lane, beta: wave * 56 + lane; clamped to S)
+        const int first = bwd ? wave * (64 - HL) : wave * (64 - HL) - HL;
+        const SelfHelp<SM, IO, NTL> help{&p, u, b, max(first, 0), min(first + 63, u.S)};
+        Chase<SelfHelp<SM, IO, NTL>> ch(flags, tag, u.T, !bwd, c.budget, &help);
         if (bwd)
-            beta_pass_halo<D, NW, HL, false, 1, true>(p, b, xh, &ch);
+            beta_pass_halo<D, NW, HL, false, 1>(p, u, b, xh, &ch);
         else
-            alpha_pass_halo<D, NW, HL, false, 1, true>(p, b, costs, xh, &ch);
-        drain_stores();  // this wave's ll / cost store lands before the NaN below (same address, other wave)
-        if (NW > 1) __syncthreads();  // (every wave is past its last poll)
-        if (threadIdx.x == 0 && fail) {  // a wave gave up waiting: its cells may have read unpublished rows
-            if (bwd) {
-                p.llb[b] = __builtin_nan("");
-            } else {
-                p.ll[b] = __builtin_nan("");
-                if (costs) costs[b] = __builtin_nanf("");
-            }
-        }
-        for (int i = threadIdx.x; i < p.T[b]; i += 64 * NW) mine[i] = 0ull;  // cleared for the next launch
+            alpha_pass_halo<D, NW, HL, false, 1>(p, u, b, costs, xh, &ch);
         return;
     }
     // ---- log-softmax workgroups: slots si, si + G, ... of the production order (G = the producer grid) ----
-    if constexpr (kVariants) {
-        if (c.probe >= 4) return;  // (development probes: the recursion side alone)
-    }
-    const int64_t per = with_beta ? 2 * (int64_t)p.B : (int64_t)p.B;
-    const int64_t G = (int64_t)gridDim.x - nrec;
-    if (blockIdx.x == (unsigned)nrec && threadIdx.x < 64) {  // the lp pads around [0, N)
+    if constexpr (DYN) {
+        if (blockIdx.x == (unsigned)nrec) publish_lengths(p, wl);  // offsets, status, lp pads (wave 0)
+        if (!wl.ok) return;
+    } else if (blockIdx.x == (unsigned)nrec && threadIdx.x < 64) {  // the lp pads around [0, N)
         const int i = threadIdx.x;
         p.lp[i - 64] = Lp{0.0, 0.0};
         p.lp[p.num_rows + i] = Lp{0.0, 0.0};
     }
-    for (int64_t si = (int64_t)blockIdx.x - nrec; si < c.slots; si += G) {
+    if constexpr (kVariants) {
+        if (c.delay) {  // (development probe: producers held back, so the recursion has to help itself)
+            const uint32_t t0 = clock100();
+            while (clock100() - t0 < c.delay) __builtin_amdgcn_s_sleep(64);
+        }
+    }
+    const int64_t per = with_beta ? 2 * (int64_t)p.B : (int64_t)p.B;
+    const int64_t G = (int64_t)gridDim.x - nrec;
+    int64_t slots = c.slots;
+    if constexpr (DYN) {
+        int tmax = wl.T;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) tmax = max(tmax, __shfl_xor(tmax, off));
+        tmax = __builtin_amdgcn_readfirstlane(tmax);
+        slots = (with_beta ? (int64_t)(tmax + 1) / 2 : (int64_t)tmax) * per;
+    }
+    for (int64_t si = (int64_t)blockIdx.x - nrec; si < slots; si += G) {
         const int kr = (int)(si / per);
         const int r = (int)(si - (int64_t)kr * per);
         const int b = with_beta ? (r >> 1) : r;
-        const int T = p.T[b];
+        ColRef k;
+        k.b = b;
+        if constexpr (DYN) {
+            k.T = __builtin_amdgcn_readlane(wl.T, b);
+            k.S = __builtin_amdgcn_readlane(wl.S, b);
+        } else {
+            k.T = p.T[b];
+            k.S = p.S[b];
+        }
+        const int T = k.T;
         int t;
         if (!with_beta) {
             if (kr >= T) continue;
@@ -124,29 +433,19 @@ __global__ __launch_bounds__(256) void chase_kernel(DevProblem p, ChaseArgs c, i
             if (2 * kr > T - 1) continue;
             t = kr;
         }
-        ColRef k;
-        k.b = b;
-        k.T = T;
-        k.S = p.S[b];
         k.t = t;
-        k.c = p.col_off[b] + t;
-        k.rowc = p.row_off[b] + (int64_t)t * (k.S + 1);
-        if constexpr (kVariants) {
-            if (c.probe == 2) {  // (development probe: the production order alone -- plain stores, no hand-off)
-                if constexpr (SM == 0)
-                    row16_column<IO, 1, NTL, false>(p, k);
-                else
-                    lean_column<IO, SM <= 3 ? 2 : 4, 2, NTL, (SM & 1) == 0, true, false>(p, k);
-                continue;
-            }
+        if constexpr (DYN) {
+            k.c = (b ? readlane64(wl.cols, b - 1) : 0) + t;
+            k.rowc = (b ? readlane64(wl.rows, b - 1) : 0) + (int64_t)t * (k.S + 1);
+            if (threadIdx.x == 0) const_cast<int *>(p.col_b)[k.c] = b;  // the gradient pass's column map
+        } else {
+            k.c = p.col_off[b] + t;
+            k.rowc = p.row_off[b] + (int64_t)t * (k.S + 1);
         }
-        chase_column<SM, IO, NTL>(p, k);
+        chase_column<SM, IO, NTL, 4>(p, k);
         drain_stores();  // every wave: its write-through rows have landed
         __syncthreads();
-        if (threadIdx.x == 0) {
-            store_wt(&c.flags[k.c], c.epoch);
-            if (with_beta) store_wt(&c.flags[c.cols + k.c], c.epoch);
-        }
+        if (threadIdx.x == 0) store_wt(&c.flags[k.c], tag);
     }
 }
 
@@ -154,65 +453,67 @@ __global__ __launch_bounds__(256) void chase_kernel(DevProblem p, ChaseArgs c, i
 // 16-byte aligned rows of <= 256 vectors (V <= 1024), the same shapes launch_u picks for them.
 int chase_body(const DevProblem &p, int elem) {
     if (elem != ELEM_F32 || p.V % 4 || (reinterpret_cast<uintptr_t>(p.acts) & 15)) return -1;
-    const int VL = p.V / 4;
-    if (VL <= 64) return 0;
-    if (VL >= 96 && VL <= 128) return VL == 128 ? 2 : 3;
-    if (VL >= 192 && VL <= 256) return VL == 256 ? 4 : 5;
-    return -1;
+    return chase_body_shape(p.V);
 }
 
-template <int SM, bool NTL, int D>
-static void launch_d(const DevProblem &p, const ChaseArgs &c, int nw, int with_beta, float *costs, int64_t grid,
-                     hipStream_t stream) {
-    if (nw == 1)
-        chase_kernel<IoF32, SM, NTL, 1, D><<<(unsigned)grid, 256, 0, stream>>>(p, c, with_beta, costs);
-    else
-        chase_kernel<IoF32, SM, NTL, 4, D><<<(unsigned)grid, 256, 0, stream>>>(p, c, with_beta, costs);
-}
-
-template <int SM, bool NTL>
+template <int SM, bool NTL, bool DYN>
 static void launch_sm(const DevProblem &p, const ChaseArgs &c, int nw, int with_beta, float *costs, int64_t grid,
                       hipStream_t stream) {
-    if constexpr (kVariants) {
-        if (tuning().chase_depth == 16) {
-            launch_d<SM, NTL, 16>(p, c, nw, with_beta, costs, grid, stream);
-            return;
+    if (nw == 1) {
+        if constexpr (kVariants) {
+            if (!c.stage) {
+                chase_kernel<IoF32, SM, NTL, 1, false, DYN><<<(unsigned)grid, 256, 0, stream>>>(p, c, with_beta, costs);
+                return;
+            }
         }
+        chase_kernel<IoF32, SM, NTL, 1, true, DYN><<<(unsigned)grid, 256, 0, stream>>>(p, c, with_beta, costs);
+    } else {
+        chase_kernel<IoF32, SM, NTL, 4, false, DYN><<<(unsigned)grid, 256, 0, stream>>>(p, c, with_beta, costs);
     }
-    launch_d<SM, NTL, 8>(p, c, nw, with_beta, costs, grid, stream);
 }
 
-template <bool NTL>
+template <bool NTL, bool DYN>
 static void launch_ntl(const DevProblem &p, const ChaseArgs &c, int sm, int nw, int with_beta, float *costs,
                        int64_t grid, hipStream_t stream) {
     switch (sm) {
-        case 0: launch_sm<0, NTL>(p, c, nw, with_beta, costs, grid, stream); break;
-        case 2: launch_sm<2, NTL>(p, c, nw, with_beta, costs, grid, stream); break;
-        case 3: launch_sm<3, NTL>(p, c, nw, with_beta, costs, grid, stream); break;
-        case 4: launch_sm<4, NTL>(p, c, nw, with_beta, costs, grid, stream); break;
-        default: launch_sm<5, NTL>(p, c, nw, with_beta, costs, grid, stream); break;
+        case 0: launch_sm<0, NTL, DYN>(p, c, nw, with_beta, costs, grid, stream); break;
+        case 2: launch_sm<2, NTL, DYN>(p, c, nw, with_beta, costs, grid, stream); break;
+        case 3: launch_sm<3, NTL, DYN>(p, c, nw, with_beta, costs, grid, stream); break;
+        case 4: launch_sm<4, NTL, DYN>(p, c, nw, with_beta, costs, grid, stream); break;
+        default: launch_sm<5, NTL, DYN>(p, c, nw, with_beta, costs, grid, stream); break;
     }
-}
-
-int64_t chase_slots(const DevProblem &p, int T_max, int with_beta) {
-    const int64_t rounds = with_beta ? (T_max + 1) / 2 : T_max;
-    const int64_t per = with_beta ? 2 * (int64_t)p.B : (int64_t)p.B;
-    return rounds * per;
 }
 
 hipError_t launch_chase(const DevProblem &p, const ChaseArgs &c, int elem, int S_max, int with_beta, int producers,
                         float *costs, hipStream_t stream) {
     const int sm = chase_body(p, elem);
     const int W = S_max + 1;
-    if (sm < 0 || W > 4 * 56 || p.min_s || p.dyn || producers < 1) return hipErrorInvalidValue;
+    if (sm < 0 || W > 4 * 56 || p.min_s || producers < 1) return hipErrorInvalidValue;
+    if (p.dyn && p.B > 64) return hipErrorInvalidValue;  // wave_lengths: one utterance per lane
     const int64_t grid = (with_beta ? 2 * (int64_t)p.B : (int64_t)p.B) + producers;
     if (grid > (int64_t)1 << 22) return hipErrorInvalidValue;
     const int nw = W <= 64 ? 1 : 4;
-    if (nt_acts_loads(p, sizeof(float)))
-        launch_ntl<true>(p, c, sm, nw, with_beta, costs, grid, stream);
-    else
-        launch_ntl<false>(p, c, sm, nw, with_beta, costs, grid, stream);
+    const bool nt = nt_acts_loads(p, sizeof(float));
+    if (p.dyn) {
+        if (nt) launch_ntl<true, true>(p, c, sm, nw, with_beta, costs, grid, stream);
+        else launch_ntl<false, true>(p, c, sm, nw, with_beta, costs, grid, stream);
+    } else {
+        if (nt) launch_ntl<true, false>(p, c, sm, nw, with_beta, costs, grid, stream);
+        else launch_ntl<false, false>(p, c, sm, nw, with_beta, costs, grid, stream);
+    }
     return hipGetLastError();
 }
+
+#ifdef MRNNT_DEVTOOLS
+unsigned long long chase_helped(bool reset) {
+    unsigned long long v = 0;
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_chase_helped), sizeof(v)) != hipSuccess) return ~0ull;
+    if (reset) {
+        const unsigned long long z = 0;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_chase_helped), &z, sizeof(z)) != hipSuccess) return ~0ull;
+    }
+    return v;
+}
+#endif
 
 }  // namespace mrnnt

@@ -33,80 +33,21 @@ __device__ __forceinline__ double dpp_shl1_bc(double v) {
     return __hiloint2double(hi, lo);
 }
 
-// The recursion side of the chase launch (mrnnt_chase.hip). A lattice column of the utterance may be read once its
-// log-softmax workgroup has published it: its ready flag (one 64-bit word per column and direction) reads `want`.
-// A wave keeps the run of walk positions known ready (rdy). At the start of every prefetch block it reads the poll
-// it issued one block earlier -- the flags of the 64 positions from rdy, one vector load -- and issues the next:
-// unconditional, so the compiler's wait for it counts the lp loads issued since and does not drain them, and a
-// wave that runs behind the producers never stalls on a poll round trip. A frame beyond rdy waits in a blocking
-// poll. Spins are bounded: a wave that gives up marks the workgroup failed (its costs become NaN) and stops waiting.
-constexpr unsigned kChaseSpins = 1u << 20;
+// One utterance's lattice as a recursion pass walks it: lengths and the offsets of its first row and column. The
+// recursion kernels read them from the lattice arrays; the chase launch under device-resident lengths takes them from
+// the lengths every wave holds in registers (wave_lengths), before the arrays are published.
+struct Utt {
+    int T, S;
+    int64_t r0, c0;
+};
 
-struct Chase {
-    const unsigned long long *flags;  // ready flag of frame 0 of this utterance, this direction
-    unsigned long long want;          // the value this launch's producers store (its epoch)
-    int T;
-    bool fwd;               // alpha walks t = 0, 1, ...; beta t = T - 1, T - 2, ...
-    int rdy;                // walk positions [0, rdy) known ready (wave-uniform)
-    int ahead_at;           // `ahead`: this lane's flag of walk position ahead_at + lane (a poll issued earlier)
-    unsigned long long ahead;
-    unsigned spins;
-    bool failed;
-    bool nowait;            // (development probe: never wait)
-    int *fail_lds;          // the workgroup's failure word (LDS)
+__device__ __forceinline__ Utt utt_of(const DevProblem &p, int b) { return Utt{p.T[b], p.S[b], p.row_off[b], p.col_off[b]}; }
 
-    __device__ __forceinline__ void init(const unsigned long long *f, unsigned long long w, int T_, bool forward,
-                                         int *lds) {
-        flags = f;
-        want = w;
-        T = T_;
-        fwd = forward;
-        rdy = 0;
-        ahead_at = 0;
-        ahead = 0;  // (no poll yet: reads as not ready)
-        spins = 0;
-        failed = false;
-        nowait = false;
-        fail_lds = lds;
-    }
-    // this lane's flag of walk position u + lane (positions past the walk read as ready)
-    __device__ __forceinline__ unsigned long long poll(int u) const {
-        const int i = u + (int)(threadIdx.x & 63);
-        return i < T ? load_wt(&flags[fwd ? i : T - 1 - i]) : want;
-    }
-    __device__ __forceinline__ int run_of(unsigned long long v) const {
-        const unsigned long long miss = ~__ballot(v == want);
-        return miss ? __builtin_ctzll(miss) : 64;
-    }
-    // start of a prefetch block: take the earlier poll's run, issue the next poll
-    __device__ __forceinline__ void refresh() {
-        const int run = run_of(ahead);
-        if (ahead_at <= rdy) rdy = max(rdy, ahead_at + run);
-        ahead_at = min(rdy, T);
-        ahead = poll(ahead_at);
-    }
-    // frame f is about to be read
-    __device__ __forceinline__ void gate(int f) {
-        const int u = fwd ? f : T - 1 - f;
-        if (u < rdy) return;
-        if (kVariants && nowait) return;
-        for (;;) {
-            const int run = run_of(poll(u));
-            if (run > 0) {
-                rdy = u + run;
-                return;
-            }
-            if (++spins > kChaseSpins) {
-                failed = true;
-                rdy = T;
-                return;
-            }
-            __builtin_amdgcn_s_sleep(2);
-        }
-    }
-    __device__ __forceinline__ void finish() {
-        if (failed && (threadIdx.x & 63) == 0) *fail_lds = 1;
-    }
+// The passes without a chase (mrnnt_recursion.hip): nothing gates the lp loads.
+struct NoChase {
+    static constexpr bool kOn = false;
+    __device__ __forceinline__ void refresh() {}
+    __device__ __forceinline__ void gate(int) {}
 };
 
 // Halo recursion (64 < S+1 <= 8 * (64 - HL)): NW waves, one cell per lane, and no per-step barrier. Wave w
@@ -114,9 +55,12 @@ struct Chase {
 // neighbouring wave owns (alpha: the cells below, beta: the cells above). Those halo lanes lose one valid lane
 // per step (their outer neighbour is not in the wave), so the own cells stay exact for HL steps; then the
 // neighbour's HL boundary cells are copied in through LDS (one barrier per HL steps instead of one per step).
-template <int D, int NW, int HL, bool BAND, int LEAN, bool CH = false, bool SC1 = CH>
-__device__ __forceinline__ void alpha_pass_halo(const DevProblem &p, int b, float *__restrict__ costs,
-                                                double (*xh)[8][HL > 0 ? HL : 1], Chase *ch = nullptr) {
+// Ch: NoChase, or the chase launch's gate (mrnnt_chase.hip: every lp row is read only after its column's ready flag,
+// with sc1 loads).
+template <int D, int NW, int HL, bool BAND, int LEAN, class Ch = NoChase>
+__device__ __forceinline__ void alpha_pass_halo(const DevProblem &p, const Utt &u, int b, float *__restrict__ costs,
+                                                double (*xh)[8][HL > 0 ? HL : 1], Ch *ch = nullptr) {
+    constexpr bool CH = Ch::kOn;
     static_assert(!CH || (LEAN && !BAND), "the chase launch runs the lean, unrestricted step");
     static_assert((HL == 0 ? NW == 1 : D % HL == 0) && NW <= 8,
                   "halo refreshes at prefetch-block positions (HL = 0: one wave, no halo); xh sized for <= 8 waves");
@@ -124,8 +68,8 @@ __device__ __forceinline__ void alpha_pass_halo(const DevProblem &p, int b, floa
     constexpr int HLD = HL > 0 ? HL : 1;  // divisor for the (compiled-out when HL == 0) refresh logic
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int T = p.T[b], S = p.S[b], W = S + 1;
-    const int64_t r0 = p.row_off[b], c0 = p.col_off[b];
+    const int T = u.T, S = u.S, W = S + 1;
+    const int64_t r0 = u.r0, c0 = u.c0;
     const int s0 = wave * C - HL + lane;  // negative for the halo lanes of wave 0 (always out of band)
     const bool own = lane >= HL && s0 < W;
     // LEAN: every row access is a uniform row pointer (SGPRs) + an unsigned lane offset; the halo lanes of wave 0
@@ -138,7 +82,7 @@ __device__ __forceinline__ void alpha_pass_halo(const DevProblem &p, int b, floa
     // under an exec branch would cost the prefetch its overlap); the halo lanes of wave 0 read row 0 as before.
     const unsigned slc = CH ? min(sl, (unsigned)S) : sl;
     auto ld = [&](const Lp *row) -> Lp {
-        if constexpr (CH && SC1)
+        if constexpr (CH)
             return load_lp_wt(lp_rsrc(p), slc * (unsigned)sizeof(Lp), (unsigned)((row - p.lp) * (int64_t)sizeof(Lp)));
         else
             return row[slc];
@@ -150,7 +94,7 @@ __device__ __forceinline__ void alpha_pass_halo(const DevProblem &p, int b, floa
 #pragma unroll
     for (int d = 0; d < D; ++d) {
         const int tt = min(d, T - 1);
-        if (CH) ch->gate(tt);
+        if constexpr (CH) ch->gate(tt);
         const Lp l = LEAN ? ld(p.lp + (r0 + (int64_t)tt * W)) : p.lp[r0 + (int64_t)tt * W + s0];
         pb[d] = l.b;
         pe[d] = l.e;
@@ -177,7 +121,7 @@ __device__ __forceinline__ void alpha_pass_halo(const DevProblem &p, int b, floa
         // row pointers advance by W per frame (no per-frame 64-bit multiply on the scalar unit)
         if (own) ap[sl] = a;
         ap += W;
-        if (CH) ch->gate(min(t + D, T - 1));
+        if constexpr (CH) ch->gate(min(t + D, T - 1));
         const Lp l = ld(lpp);
         pb[d] = l.b;
         pe[d] = l.e;
@@ -213,7 +157,7 @@ __device__ __forceinline__ void alpha_pass_halo(const DevProblem &p, int b, floa
     for (; t0 + D <= T; t0 += D) {
 #pragma unroll
         for (int d = 0; d < D; ++d) {
-            if (CH && d == 0) ch->refresh();
+            if constexpr (CH) if (d == 0) ch->refresh();
             step(t0 + d, d);
             if (HL > 0 && (d + 1) % HLD == 0 && (d + 1 < D || t0 + D < T)) {
                 const int par = ((t0 + d) / HLD) & 1;
@@ -238,12 +182,12 @@ __device__ __forceinline__ void alpha_pass_halo(const DevProblem &p, int b, floa
         p.ll[b] = a;
         if (costs) costs[b] = (float)(-a);
     }
-    if (CH) ch->finish();
 }
 
-template <int D, int NW, int HL, bool BAND, int LEAN, bool CH = false, bool SC1 = CH>
-__device__ __forceinline__ void beta_pass_halo(const DevProblem &p, int b, double (*xh)[8][HL > 0 ? HL : 1],
-                                               Chase *ch = nullptr) {
+template <int D, int NW, int HL, bool BAND, int LEAN, class Ch = NoChase>
+__device__ __forceinline__ void beta_pass_halo(const DevProblem &p, const Utt &u, int b,
+                                               double (*xh)[8][HL > 0 ? HL : 1], Ch *ch = nullptr) {
+    constexpr bool CH = Ch::kOn;
     static_assert(!CH || (LEAN && !BAND), "the chase launch runs the lean, unrestricted step");
     static_assert((HL == 0 ? NW == 1 : D % HL == 0) && NW <= 8,
                   "halo refreshes at prefetch-block positions (HL = 0: one wave, no halo); xh sized for <= 8 waves");
@@ -251,8 +195,8 @@ __device__ __forceinline__ void beta_pass_halo(const DevProblem &p, int b, doubl
     constexpr int HLD = HL > 0 ? HL : 1;  // divisor for the (compiled-out when HL == 0) refresh logic
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int T = p.T[b], S = p.S[b], W = S + 1;
-    const int64_t r0 = p.row_off[b], c0 = p.col_off[b];
+    const int T = u.T, S = u.S, W = S + 1;
+    const int64_t r0 = u.r0, c0 = u.c0;
     const int s0 = wave * C + lane;  // lanes >= C: halo, the first HL cells of the wave above
     const bool own = lane < C && s0 < W;
     const unsigned sl = (unsigned)s0;
@@ -260,7 +204,7 @@ __device__ __forceinline__ void beta_pass_halo(const DevProblem &p, int b, doubl
     // (clamped offset, unconditional load; as alpha_pass_halo)
     const unsigned slc = CH ? min(sl, (unsigned)S) : sl;
     auto ld = [&](const Lp *row) -> Lp {
-        if constexpr (CH && SC1)
+        if constexpr (CH)
             return load_lp_wt(lp_rsrc(p), slc * (unsigned)sizeof(Lp), (unsigned)((row - p.lp) * (int64_t)sizeof(Lp)));
         else
             return row[slc];
@@ -272,7 +216,7 @@ __device__ __forceinline__ void beta_pass_halo(const DevProblem &p, int b, doubl
 #pragma unroll
     for (int d = 0; d < D; ++d) {
         const int tt = max(T - 1 - d, 0);
-        if (CH) ch->gate(tt);
+        if constexpr (CH) ch->gate(tt);
         const Lp l = ld(p.lp + (r0 + (int64_t)tt * W));
         pb[d] = l.b;
         pe[d] = l.e;
@@ -301,7 +245,7 @@ __device__ __forceinline__ void beta_pass_halo(const DevProblem &p, int b, doubl
         }
         if (own) bp_[sl] = bn;
         bp_ -= W;
-        if (CH) ch->gate(max(t - D, 0));
+        if constexpr (CH) ch->gate(max(t - D, 0));
         const Lp l = ld(lpp);
         pb[d] = l.b;
         pe[d] = l.e;
@@ -341,7 +285,7 @@ __device__ __forceinline__ void beta_pass_halo(const DevProblem &p, int b, doubl
     for (; t0 - D + 1 >= 0; t0 -= D) {
 #pragma unroll
         for (int d = 0; d < D; ++d) {
-            if (CH && d == 0) ch->refresh();
+            if constexpr (CH) if (d == 0) ch->refresh();
             step(t0 - d, d);
             if (HL > 0 && (d + 1) % HLD == 0 && (d + 1 < D || t0 - D >= 0)) {  // refresh from the wave above
                 const int par = ((T - 1 - t0 + d) / HLD) & 1;
@@ -363,7 +307,6 @@ __device__ __forceinline__ void beta_pass_halo(const DevProblem &p, int b, doubl
         }
     }
     if (threadIdx.x == 0) p.llb[b] = bn;
-    if (CH) ch->finish();
 }
 
 }  // namespace mrnnt

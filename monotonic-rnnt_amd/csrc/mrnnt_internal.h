@@ -123,16 +123,8 @@ struct Tuning {
     int nt_load = 2;              // loads of acts in both streaming kernels: 1 nontemporal, 0 default policy,
                                   // 2 by size (nt_acts_loads)
     int occ_skip = 1;             // gradient: no acts read for rows with log-occupancy < kDeadLogOcc
-    int joint_nbuf = 2;           // fused joint kernels: LDS buffers for the weight chunks (2 or 3)
-    int joint_nw = 8;             // fused joint kernels: waves per workgroup (8: one workgroup per CU; 4: two)
-    int joint_mfma = 32;          // fused joint forward: MFMA tile, 32 (v_mfma_f32_32x32x16_bf16) or 16 (16x16x32)
-    int joint_bwd_mfma = 16;      // fused joint backward: the same
-    int joint_pipe = 0;           // fused joint forward: 1 -> the pipelined one-wave-per-SIMD kernel (H <= 512)
-    int joint_fwd_opt = 0;        // fused joint 8-wave forward: bit 0 bias as the initial accumulator, bit 1 label logit
-                                  // as a dot product (development A/B)
-    int joint_fwd_persist = 0;    // fused joint forward: 1 -> persistent 8-wave kernel (W stream across tiles, next tile's
-                                  // row positions prefetched)
-    int joint_ring = 2;           // fused joint 32x32 tile: A fragments in flight (development build: 2, 4, 8)
+    int joint_bwd_mfma = 16;      // fused joint backward MFMA tile for H <= 512: 16 (v_mfma_f32_16x16x32_bf16) or 32
+                                  // (32x32x16, development build); H = 640 always 32
     int joint_reduce_sparse = 0;  // joint d_enc/d_pred reduce: 0 row-parallel kernel below 4 live rows per column,
                                   // 1 always frame by frame, 2 always row-parallel
     int dp_halo = 2;              // alpha/beta: halo recursion (one barrier per 8 steps, 8 / 16-step prefetch
@@ -144,10 +136,13 @@ struct Tuning {
     int dyn_fused = 1;            // device-resident lengths, B <= 64, no alignment: plan inside the log-softmax launch
                                   // (0: a separate setup kernel)
     int chase = 1;                // forward as one launch, the recursion chasing the log-softmax (mrnnt_chase.hip) where
-                                  // it applies (host lengths, no alignment, f32 rows of <= 256 vectors, S + 1 <= 224)
-    int chase_depth = 8;          // lp rows the chase recursion prefetches (8; 16 in the development build)
+                                  // it applies (no alignment, f32 rows of <= 256 vectors, S + 1 <= 224; device lengths:
+                                  // B <= 64) and pays (chase_pays)
     int chase_grid_per_cu = 0;    // log-softmax workgroups of the chase launch per CU (0: one per slot)
-    int chase_probe = 0;          // development build: 1 -> the chase's log-softmax side alone, 2 -> also no hand-off
+    int chase_wait_us = 100;      // a chase recursion wave computes a column itself after waiting this long for it
+    int chase_stage = 1;          // one-wave chase recursion: lp frames staged in LDS by a loader wave (0: direct
+                                  // gated loads; development build)
+    int chase_delay_us = 0;       // development probe: every chase producer workgroup starts this late
     int col_xcd = 0;              // XCD-chunked column order (visit_col, col_mul < 0; overrides col_scatter): bit 0
                                   // log-softmax, bit 1 gradient
 };
@@ -214,19 +209,35 @@ hipError_t launch_mask_state(const DevProblem &p, double *alpha, double *beta, h
 hipError_t launch_dp(const DevProblem &p, int S_max, int with_beta, float *costs, hipStream_t stream);
 
 // The chase launch (mrnnt_chase.hip): log-softmax and alpha / beta recursion in one launch, the recursion consuming
-// columns as they are published. Ready flags: `cols` 64-bit words for alpha, then `cols` for beta, tagged with the
-// launch's epoch.
+// columns as they are published. Ready flags: one 64-bit word per lattice column, holding the tag of the launch that
+// published it (never cleared: every launch derives a tag of its own from its dispatch id).
 struct ChaseArgs {
     unsigned long long *flags;
-    int64_t cols;              // the flag stride between the directions
-    int64_t slots;             // of the production order (chase_slots)
-    unsigned long long epoch;  // fresh per call (never 0)
-    int probe;                 // development build only (tuning().chase_probe): 1 no recursion, 2 no hand-off either,
-                               // 3 recursion without waiting, 4 recursion alone without waiting
+    int64_t slots;             // of the production order (host lengths: chase_slots; device lengths: 0, planned on the
+                               // device from the lengths)
+    unsigned long long epoch;  // fresh per call (never 0), mixed with the dispatch id into the launch's tag
+    uint32_t budget;           // ticks of the 100 MHz constant clock a recursion wave waits for a column before it
+                               // computes the column itself
+    uint32_t delay;            // development probe (ticks): producer workgroups start this late
+    int stage;                 // one-wave recursion: LDS-staged frames (the product's only form) or direct loads
 };
-// the log-softmax body the chase launch has for this problem, -1 for none (f32 rows of <= 256 vectors only)
+// The log-softmax body the chase launch carries for f32 rows of V elements: 0 rows on 16-lane groups (<= 64
+// vectors), 2 / 3 single-chunk rows of <= 128 vectors (full / partial chunk), 4 / 5 of <= 256; -1 none.
+inline int chase_body_shape(int V) {
+    if (V <= 0 || V % 4) return -1;
+    const int VL = V / 4;
+    if (VL <= 64) return 0;
+    if (VL >= 96 && VL <= 128) return VL == 128 ? 2 : 3;
+    if (VL >= 192 && VL <= 256) return VL == 256 ? 4 : 5;
+    return -1;
+}
+// the body for this problem (f32 acts, 16-byte aligned), -1 for none
 int chase_body(const DevProblem &p, int elem);
-int64_t chase_slots(const DevProblem &p, int T_max, int with_beta);
+inline int64_t chase_slots(int B, int T_max, int with_beta) {
+    return (with_beta ? (int64_t)(T_max + 1) / 2 : (int64_t)T_max) * (with_beta ? 2 * (int64_t)B : (int64_t)B);
+}
+// development build: columns chase recursion waves computed themselves (since the last reset)
+unsigned long long chase_helped(bool reset);
 hipError_t launch_chase(const DevProblem &p, const ChaseArgs &c, int elem, int S_max, int with_beta, int producers,
                         float *costs, hipStream_t stream);
 hipError_t launch_grad(const DevProblem &p, int elem, const float *scale, void *grads, int grid, hipStream_t stream);

@@ -53,20 +53,6 @@ __device__ __forceinline__ f2 fast_tanh2(f2 x) {
     return (f2){copysignf(y.x, x.x), copysignf(y.y, x.y)};
 }
 
-// acc + h . w over 8 bf16: 4 v_dot2_f32_bf16 (the VOP3P form, explicit accumulator operand: through
-// __builtin_amdgcn_fdot2_f32_bf16 hipcc emits the tied-accumulator v_dot2c form, and inside this kernel that gave
-// wrong dot products -- the tests with the builtin failed, the same kernel with this form or with FMAs passes)
-__device__ __forceinline__ float dot8(const bf16x8 &h, const u4 &w, float acc) {
-    const u4 hu = __builtin_bit_cast(u4, h);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        float r;
-        asm("v_dot2_f32_bf16 %0, %1, %2, %3" : "=v"(r) : "v"(hu[q]), "v"(w[q]), "v"(acc));
-        acc = r;
-    }
-    return acc;
-}
-
 // ---------------------------------------------------------------------------------------------------------
 // row lists: entries (column, s) in column order, s ascending; mode 0 = in-band rows, 1 = live rows
 
@@ -254,33 +240,11 @@ struct WTile {
         }
     }
 
-    // piece ii (of NI / NW) of this wave's share of stage<NW>
-    template <int NW>
-    __device__ static __forceinline__ void stage_piece(const JointArgs &j, int V, int c, unsigned short *wbuf, int ii) {
-        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-        const int i = NW * ii + wave;
-        const int L = 64 * i + lane;
-        const int r = L / CPR, pc = L % CPR;
-        const int v = min(32 * c + r, V - 1);
-        const unsigned short *g = j.W + (int64_t)v * H + 8 * (pc ^ (r & 15));
-        __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void *)(wbuf + 512 * i), 16, 0, 0);
-    }
-
     // one 32x32 output tile: D[vocab][row] = sum_k W[vocab][k] h[row][k]; A fragments stream from LDS
     // through a 4-deep register ring so no MFMA waits on a ds_read it has just issued. The swizzled piece of
     // k-step ks = 8m + k' is 16m + ((2k' + half) ^ (r & 15)): 8 base addresses, m in the immediate offset.
     template <int RING = 4>
     __device__ static __forceinline__ f32x16 mma(const unsigned short *wbuf, const bf16x8 (&bfr)[KS], int lane) {
-        f32x16 zero;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) zero[i] = 0.0f;
-        return mma_from<RING>(wbuf, bfr, lane, zero);
-    }
-
-    // the same accumulating onto acc0 (the forward passes the bias there: z comes out of the MFMA chain)
-    template <int RING = 4>
-    __device__ static __forceinline__ f32x16 mma_from(const unsigned short *wbuf, const bf16x8 (&bfr)[KS], int lane,
-                                                      const f32x16 &acc0) {
         const int r = lane & 31, half = lane >> 5;
         const unsigned short *row = wbuf + r * H;
         const unsigned short *base[8];
@@ -291,7 +255,9 @@ struct WTile {
         bf16x8 a[D];
 #pragma unroll
         for (int d = 0; d < D; ++d) a[d] = rd(d);
-        f32x16 acc = acc0;
+        f32x16 acc;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks % D], bfr[ks], acc, 0, 0, 0);
@@ -449,10 +415,7 @@ __device__ __forceinline__ float *load_bias(const JointArgs &j, int V, unsigned 
 }
 
 // two waves per SIMD: the compiler keeps each kernel within 256 registers per lane
-// OPT (development A/B, joint_fwd_opt): bit 0 -- the bias is the MFMA chain's initial accumulator (no bias adds in
-// the epilogue); bit 1 -- the label logit as a dot product W[label] . h beside the activation build (no per-chunk
-// label select tree)
-template <int KS, int NB, int NW, int RG, int OPT = 0>
+template <int KS, int NB, int NW, int RG>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2))) void joint_fwd_kernel(DevProblem p,
                                                                                              JointArgs j) {
     extern __shared__ __attribute__((aligned(16))) unsigned short wsh[];
@@ -469,38 +432,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const f2 l2e = {kLog2e, kLog2e};
     float m = NEG_INF_F, sum = 0.0f, zb = 0.0f, ze = 0.0f;
     bool fb = false, fe = false;
-    if constexpr (OPT & 2) {  // W[label] . h over this lane's k half (rows without a label: row 0, unused)
-        const unsigned short *wl = j.W + (int64_t)(q.lab >= 0 ? q.lab : 0) * (16 * KS) + 8 * half;
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) ze = dot8(bfr[ks], *reinterpret_cast<const u4 *>(wl + 16 * ks), ze);
-        fe = q.lab >= 0;
-    }
-    auto mma = [&](const unsigned short *wb, int c) {
-        if constexpr (OPT & 1) {
-            f32x16 b0;
-#pragma unroll
-            for (int q4 = 0; q4 < 4; ++q4) {
-                const f4 bv = *reinterpret_cast<const f4 *>(bias + 32 * c + 8 * q4 + 4 * half);
-                b0[4 * q4] = bv.x;
-                b0[4 * q4 + 1] = bv.y;
-                b0[4 * q4 + 2] = bv.z;
-                b0[4 * q4 + 3] = bv.w;
-            }
-            return WTile<KS>::template mma_from<RG>(wb, bfr, lane, b0);
-        } else {
-            return WTile<KS>::template mma<RG>(wb, bfr, lane);
-        }
-    };
-    int c_mma = 0;
-    chunk_loop_with<KS, NB, NW>(j, V, wsh, 0, [&](const unsigned short *wb) { return mma(wb, c_mma++); },
-                                [&](const f32x16 &acc, int c) {
+    chunk_loop<KS, NB, NW, RG>(j, V, wsh, bfr, lane, 0, [&](const f32x16 &acc, int c) {
         f2 z[8];
-        if constexpr (OPT & 1) {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) z[k] = (f2){acc[2 * k], acc[2 * k + 1]};
-        } else {
-            logits2(acc, bias, c, half, z);
-        }
+        logits2(acc, bias, c, half, z);
         float cm = fmaxf(z[0].x, z[0].y);
 #pragma unroll
         for (int k = 1; k < 8; ++k) cm = max3(cm, z[k].x, z[k].y);
@@ -523,16 +457,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
                 fb = true;
             }
         }
-        if constexpr (!(OPT & 2)) {
-            const int jl = q.lab - 32 * c;
-            const int rl = acc_reg_of(jl & 31, half);
-            const bool mine = q.lab >= 0 && jl >= 0 && jl < 32 && rl >= 0;
-            if (__ballot(mine)) {  // most chunks hold some lane's label; skip the select when none does
-                const float x = tree_pick(z, rl);
-                if (mine) {
-                    ze = x;
-                    fe = true;
-                }
+        const int jl = q.lab - 32 * c;
+        const int rl = acc_reg_of(jl & 31, half);
+        const bool mine = q.lab >= 0 && jl >= 0 && jl < 32 && rl >= 0;
+        if (__ballot(mine)) {  // most chunks hold some lane's label; skip the select when none does
+            const float x = tree_pick(z, rl);
+            if (mine) {
+                ze = x;
+                fe = true;
             }
         }
     });
@@ -544,136 +476,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const float mr = (mn == NEG_INF_F) ? 0.0f : mn;
     sum = sum * fast_exp2((m - mr) * kLog2e) + s2 * fast_exp2((m2 - mr) * kLog2e);
     if (!fb && fb2) zb = zb2;
-    if constexpr (OPT & 2) {
-        ze = ze + ze2 + ((j.bias && q.lab >= 0) ? j.bias[q.lab] : 0.0f);  // the two k halves, then the bias
-    } else {
-        if (!fe && fe2) ze = ze2;
-    }
+    if (!fe && fe2) ze = ze2;
     if (q.valid && half == 0) {
         const double den = -(double)mn - log_row_sum(sum);
         p.den[q.row] = (float)den;
         p.lp[q.row] = Lp{(double)zb + den, (q.lab >= 0 ? (double)ze : (q.lab == -2 ? __builtin_nan("") : 0.0)) + den};
     }
-}
-
-// Persistent form of the forward (development A/B, joint_fwd_persist): one 8-wave workgroup per CU walks its tiles;
-// the W-chunk stream runs on across tiles (the next tile's first chunk lands during the current tile's last), the
-// bias is staged once, and the next tile's row positions -- a chain of dependent loads (list entry -> utterance ->
-// lattice offsets, lengths, label) -- are fetched one link per third of the current tile's chunks, so no tile starts
-// with that chain or with a cold W chunk.
-template <int KS, int NB, int NW>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2))) void joint_fwd_persist_kernel(
-    DevProblem p, JointArgs j) {
-    using WT = WTile<KS>;
-    extern __shared__ __attribute__((aligned(16))) unsigned short wsh[];
-    constexpr int ROWS = 32 * NW;
-    const int64_t n = list_len(j);
-    const int64_t ntiles = (n + ROWS - 1) / ROWS;
-    int64_t tile = blockIdx.x;
-    if (tile >= ntiles) return;
-    const int lane = threadIdx.x & 63, half = lane >> 5;
-    const int V = p.V, blank = p.blank;
-    const int nch = (V + 31) / 32;
-    const float *bias = load_bias<KS, NB>(j, V, wsh);
-    auto row_of = [&](int64_t t) { return t * ROWS + (threadIdx.x >> 6) * 32 + (lane & 31); };
-    int c_issue = 0, b_issue = 0, b_use = 0;
-    auto stage_next = [&]() {
-        WT::template stage<NW>(j, V, c_issue, wsh + b_issue * WT::ELEMS);
-        c_issue = c_issue + 1 == nch ? 0 : c_issue + 1;
-        b_issue = b_issue + 1 == NB ? 0 : b_issue + 1;
-    };
-#pragma unroll
-    for (int k = 0; k < NB - 1; ++k) stage_next();
-    RowPos q = row_pos(p, j, row_of(tile));
-    __syncthreads();  // bias in LDS
-    const int sA = 0, sB = nch / 3, sC = (2 * nch) / 3;
-    const f2 l2e = {kLog2e, kLog2e};
-    for (;;) {
-        bf16x8 bfr[KS];
-        build_act<KS, false>(j, q, half, row_of(tile), bfr);
-        const int64_t inext = row_of(tile + gridDim.x);
-        const bool vnext = inext < n;
-        int ncol = 0, ns = 0, nb = 0;
-        RowPos qn{false, 0, 0, 0, 1, 0, -1, 0};
-        float m = NEG_INF_F, sum = 0.0f, zb = 0.0f, ze = 0.0f;
-        bool fb = false, fe = false;
-        for (int c = 0; c < nch; ++c) {
-            wait_dma();
-            __builtin_amdgcn_s_barrier();
-            stage_next();
-            const f32x16 acc = WT::template mma<2>(wsh + b_use * WT::ELEMS, bfr, lane);
-            b_use = b_use + 1 == NB ? 0 : b_use + 1;
-            f2 z[8];
-            logits2(acc, bias, c, half, z);
-            float cm = fmaxf(z[0].x, z[0].y);
-#pragma unroll
-            for (int k = 1; k < 8; ++k) cm = max3(cm, z[k].x, z[k].y);
-            const float mn = fmaxf(m, cm);
-            const float mr = (mn == NEG_INF_F) ? 0.0f : mn;
-            const f2 nb2 = {-mr * kLog2e, -mr * kLog2e};
-            f2 s2 = {0.0f, 0.0f};
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const f2 t = fma2(z[k], l2e, nb2);
-                s2 = add2(s2, (f2){fast_exp2(t.x), fast_exp2(t.y)});
-            }
-            sum = sum * fast_exp2((m - mr) * kLog2e) + (s2.x + s2.y);
-            m = mn;
-            const int jb = blank - 32 * c;  // wave-uniform: one chunk holds the blank
-            if (jb >= 0 && jb < 32) {
-                const int rb = acc_reg_of(jb, half);
-                if (rb >= 0) {
-                    zb = tree_pick(z, rb);
-                    fb = true;
-                }
-            }
-            const int jl = q.lab - 32 * c;
-            const int rl = acc_reg_of(jl & 31, half);
-            const bool mine = q.lab >= 0 && jl >= 0 && jl < 32 && rl >= 0;
-            if (__ballot(mine)) {
-                const float x = tree_pick(z, rl);
-                if (mine) {
-                    ze = x;
-                    fe = true;
-                }
-            }
-            // the next tile's row positions, one dependent link at a time
-            if (c == sA && vnext) {
-                ncol = j.lcol[inext];
-                ns = j.ls[inext];
-            }
-            if (c == sB && vnext) nb = p.col_b[ncol];
-            if (c == sC && vnext) {
-                qn.valid = true;
-                qn.s = ns;
-                qn.b = nb;
-                qn.t = (int)(ncol - p.col_off[nb]);
-                qn.T = p.T[nb];
-                qn.S = p.S[nb];
-                qn.row = p.row_off[nb] + (int64_t)qn.t * (qn.S + 1) + ns;
-                const int l = ns < qn.S ? p.labels[(int64_t)nb * p.label_stride + ns] : -1;
-                qn.lab = (ns < qn.S && (unsigned)l >= (unsigned)p.V) ? -2 : l;
-            }
-        }
-        const float m2 = __shfl_xor(m, 32), s2 = __shfl_xor(sum, 32);
-        const float zb2 = __shfl_xor(zb, 32), ze2 = __shfl_xor(ze, 32);
-        const int fb2 = __shfl_xor((int)fb, 32), fe2 = __shfl_xor((int)fe, 32);
-        const float mn = fmaxf(m, m2);
-        const float mr = (mn == NEG_INF_F) ? 0.0f : mn;
-        sum = sum * fast_exp2((m - mr) * kLog2e) + s2 * fast_exp2((m2 - mr) * kLog2e);
-        if (!fb && fb2) zb = zb2;
-        if (!fe && fe2) ze = ze2;
-        if (q.valid && half == 0) {
-            const double den = -(double)mn - log_row_sum(sum);
-            p.den[q.row] = (float)den;
-            p.lp[q.row] =
-                Lp{(double)zb + den, (q.lab >= 0 ? (double)ze : (q.lab == -2 ? __builtin_nan("") : 0.0)) + den};
-        }
-        tile += gridDim.x;
-        if (tile >= ntiles) break;
-        q = qn;
-    }
-    wait_dma();  // the stream's last DMA lands before the workgroup's LDS is released
 }
 
 template <int KS, int NB, int NW, int RG>
@@ -765,95 +573,6 @@ __device__ __forceinline__ void logits8(const typename WTile16<KS>::Acc &acc, co
     for (int vt = 0; vt < 2; ++vt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) x[4 * vt + r] = acc.d[vt][rt][r] + bv[vt][r];
-}
-
-template <int KS, int NB, int NW>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2))) void joint_fwd16_kernel(
-    DevProblem p, JointArgs j) {
-    extern __shared__ __attribute__((aligned(16))) unsigned short wsh[];
-    constexpr int K32 = KS / 2;
-    if ((int64_t)blockIdx.x * (32 * NW) >= list_len(j)) return;  // whole workgroup past a shorter list
-    const int lane = threadIdx.x & 63, c16 = lane & 15, g = lane >> 4;
-    const int64_t i0 = (int64_t)blockIdx.x * (32 * NW) + (threadIdx.x >> 6) * 32 + c16;
-    const RowPos q[2] = {row_pos(p, j, i0), row_pos(p, j, i0 + 16)};
-    const int V = p.V, blank = p.blank;
-    const float *bias = load_bias<KS, NB>(j, V, wsh);
-    __syncthreads();
-    bf16x8 bfr[2][K32];
-    build_row<K32, 32, false>(j, q[0], 8 * g, i0, bfr[0]);
-    build_row<K32, 32, false>(j, q[1], 8 * g, i0 + 16, bfr[1]);
-
-    float m[2] = {NEG_INF_F, NEG_INF_F}, sum[2] = {0.0f, 0.0f}, zb[2] = {0.0f, 0.0f}, ze[2] = {0.0f, 0.0f};
-    bool fb = false, fe[2] = {false, false};
-    chunk_loop_with<KS, NB, NW>(
-        j, V, wsh, 0, [&](const unsigned short *wb) { return WTile16<KS>::template mma<4>(wb, bfr, lane); },
-        [&](const typename WTile16<KS>::Acc &acc, int c) {
-            const f4 bv[2] = {*reinterpret_cast<const f4 *>(bias + 32 * c + 4 * g),
-                              *reinterpret_cast<const f4 *>(bias + 32 * c + 16 + 4 * g)};
-            const int jb = blank - 32 * c;  // wave-uniform: one chunk holds the blank
-            const bool hb = jb >= 0 && jb < 32 && ((jb >> 2) & 3) == g;
-#pragma unroll
-            for (int rt = 0; rt < 2; ++rt) {
-                float z[8];
-                logits8<KS>(acc, bv, rt, z);
-                const float cm = max3(max3(z[0], z[1], z[2]), max3(z[3], z[4], z[5]), fmaxf(z[6], z[7]));
-                const float mn = fmaxf(m[rt], cm);
-                const float mr = (mn == NEG_INF_F) ? 0.0f : mn;
-                const float nb = -mr * kLog2e;
-                float s0 = 0.0f, s1 = 0.0f;
-#pragma unroll
-                for (int k = 0; k < 8; k += 2) {
-                    s0 += fast_exp2(fmaf(z[k], kLog2e, nb));
-                    s1 += fast_exp2(fmaf(z[k + 1], kLog2e, nb));
-                }
-                sum[rt] = sum[rt] * fast_exp2((m[rt] - mr) * kLog2e) + (s0 + s1);
-                m[rt] = mn;
-                if (jb >= 0 && jb < 32) {
-                    const float x = pick8(z, pick8_index(jb));
-                    if (hb) zb[rt] = x;
-                }
-                const int jl = q[rt].lab - 32 * c;
-                const bool mine = q[rt].lab >= 0 && jl >= 0 && jl < 32 && ((jl >> 2) & 3) == g;
-                if (__ballot(mine)) {  // most chunks hold some lane's label; skip the select when none does
-                    const float x = pick8(z, pick8_index(jl & 31));
-                    if (mine) {
-                        ze[rt] = x;
-                        fe[rt] = true;
-                    }
-                }
-            }
-            if (hb) fb = true;
-        });
-    // merge the four lane groups (same rows, disjoint vocabulary)
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
-        bool fbr = fb;
-#pragma unroll
-        for (int off = 16; off <= 32; off <<= 1) {
-            const float m2 = __shfl_xor(m[rt], off), s2 = __shfl_xor(sum[rt], off);
-            const float zb2 = __shfl_xor(zb[rt], off), ze2 = __shfl_xor(ze[rt], off);
-            const int fb2 = __shfl_xor((int)fbr, off), fe2 = __shfl_xor((int)fe[rt], off);
-            const float mn = fmaxf(m[rt], m2);
-            const float mr = (mn == NEG_INF_F) ? 0.0f : mn;
-            sum[rt] = sum[rt] * fast_exp2((m[rt] - mr) * kLog2e) + s2 * fast_exp2((m2 - mr) * kLog2e);
-            m[rt] = mn;
-            if (!fbr && fb2) {
-                zb[rt] = zb2;
-                fbr = true;
-            }
-            if (!fe[rt] && fe2) {
-                ze[rt] = ze2;
-                fe[rt] = true;
-            }
-        }
-        const RowPos &qr = q[rt];
-        if (qr.valid && g == 0) {
-            const double den = -(double)m[rt] - log_row_sum(sum[rt]);
-            p.den[qr.row] = (float)den;
-            p.lp[qr.row] =
-                Lp{(double)zb[rt] + den, (qr.lab >= 0 ? (double)ze[rt] : (qr.lab == -2 ? __builtin_nan("") : 0.0)) + den};
-        }
-    }
 }
 
 template <int KS, int NB, int NW>
@@ -964,349 +683,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
             if (t != 0.0f) atomicAdd(&j.dbias[v], t);
         }
     }
-}
-
-// ---------------------------------------------------------------------------------------------------------
-// Pipelined forward (joint_fwd_pipe): ONE wave per SIMD (4-wave workgroup, 512 registers per lane), persistent over
-// tiles of 128 rows. The activations of the NEXT tile are built while the current tile's MFMAs run: chunk c of the
-// current tile carries fragment c of the next tile's B operand (double-buffered in registers), and the online-softmax
-// epilogue of chunk c - 1 (two accumulators), both in the gaps between the chunk's 32 MFMAs, so the matrix pipe is not
-// left idle during an activation-build phase or an epilogue (the 8-wave kernel above spends ~26 % of a wave's life in
-// the build with both waves of a SIMD building at once). The blank and label logits are not picked from the
-// accumulators (a select tree per chunk) but formed as two dot products per row, fragment by fragment, beside the
-// build: z_blank = W[blank] . h + bias[blank] (fp32, v_dot2c_f32_bf16 -- the same exact bf16 products as the MFMA, in
-// another summation order: ~1e-7 relative).
-
-// scalar tanh (packed f32 beside MFMAs costs more issue time than two scalar ops)
-__device__ __forceinline__ float tanh1(float x) {
-    const float e = fast_exp2(fabsf(x) * (-2.0f * kLog2e));
-    return copysignf((1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e), x);
-}
-
-// one B fragment: 8 bf16 of tanh(enc + pred) (rows past the list read row 0: finite, and only their own discarded
-// output column and dot products see them)
-__device__ __forceinline__ bf16x8 act8(const u4 &ev, const u4 &pv) {
-    bf16x8 h;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-        h[2 * w] = (__bf16)tanh1(bf16_lo(ev[w]) + bf16_lo(pv[w]));
-        h[2 * w + 1] = (__bf16)tanh1(bf16_hi(ev[w]) + bf16_hi(pv[w]));
-    }
-    return h;
-}
-
-// the same with fp32 FMAs on unpacked bf16 (development check)
-__device__ __forceinline__ float dot8f(const bf16x8 &h, const u4 &w, float acc) {
-    const u4 hu = __builtin_bit_cast(u4, h);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        acc = fmaf(bf16_lo(hu[q]), bf16_lo(w[q]), acc);
-        acc = fmaf(bf16_hi(hu[q]), bf16_hi(w[q]), acc);
-    }
-    return acc;
-}
-
-// the inputs of one fragment of a row: enc / pred slices and the W[label] / W[blank] slices of the same k range
-struct FragIn {
-    u4 e, p, wl, wb;
-};
-
-struct RowSrc {
-    const unsigned short *e, *p, *wl, *wb;  // this lane's k = 8 half + 16 ks slices start here (ks added per load)
-    float keep;
-};
-
-template <int KS>
-__device__ __forceinline__ RowSrc row_src(const JointArgs &j, const RowPos &q, int half, int blank) {
-    constexpr int H = 16 * KS;
-    const bool v = q.valid;
-    RowSrc r;
-    r.e = j.enc + (v ? (int64_t)q.b * j.enc_sb + (int64_t)q.t * H : 0) + 8 * half;
-    r.p = j.pred + (v ? (int64_t)q.b * j.pred_sb + (int64_t)q.s * H : 0) + 8 * half;
-    r.wl = j.W + (int64_t)(q.lab >= 0 ? q.lab : 0) * H + 8 * half;
-    r.wb = j.W + (int64_t)blank * H + 8 * half;
-    r.keep = v ? 1.0f : 0.0f;
-    return r;
-}
-
-__device__ __forceinline__ FragIn frag_load(const RowSrc &r, int ks) {
-    return FragIn{*reinterpret_cast<const u4 *>(r.e + 16 * ks), *reinterpret_cast<const u4 *>(r.p + 16 * ks),
-                  *reinterpret_cast<const u4 *>(r.wl + 16 * ks), *reinterpret_cast<const u4 *>(r.wb + 16 * ks)};
-}
-
-// the per-row online log-sum-exp over one chunk's 16 logits of this lane (branch-free)
-__device__ __forceinline__ void softmax_chunk(const f32x16 &acc, const float *bias, int c, int half, float &m,
-                                              float &sum) {
-    f2 z[8];
-    logits2(acc, bias, c, half, z);
-    float cm = fmaxf(z[0].x, z[0].y);
-#pragma unroll
-    for (int k = 1; k < 8; ++k) cm = max3(cm, z[k].x, z[k].y);
-    const float mn = fmaxf(m, cm);
-    const float mr = (mn == NEG_INF_F) ? 0.0f : mn;
-    const float nb = -mr * kLog2e;
-    float s0 = 0.0f, s1 = 0.0f;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        s0 += fast_exp2(fmaf(z[k].x, kLog2e, nb));
-        s1 += fast_exp2(fmaf(z[k].y, kLog2e, nb));
-    }
-    sum = sum * fast_exp2((m - mr) * kLog2e) + (s0 + s1);
-    m = mn;
-}
-
-template <int KS>
-__device__ __forceinline__ void put_frag(bf16x8 (&b)[KS], int f, const bf16x8 &h) {
-    switch (f) {  // uniform f: a scalar jump, no indexed register access
-#define MRNNT_PUT(k) \
-    case k:          \
-        if constexpr (k < KS) b[k] = h; \
-        break;
-        MRNNT_PUT(0) MRNNT_PUT(1) MRNNT_PUT(2) MRNNT_PUT(3) MRNNT_PUT(4) MRNNT_PUT(5) MRNNT_PUT(6) MRNNT_PUT(7)
-        MRNNT_PUT(8) MRNNT_PUT(9) MRNNT_PUT(10) MRNNT_PUT(11) MRNNT_PUT(12) MRNNT_PUT(13) MRNNT_PUT(14) MRNNT_PUT(15)
-        MRNNT_PUT(16) MRNNT_PUT(17) MRNNT_PUT(18) MRNNT_PUT(19) MRNNT_PUT(20) MRNNT_PUT(21) MRNNT_PUT(22) MRNNT_PUT(23)
-        MRNNT_PUT(24) MRNNT_PUT(25) MRNNT_PUT(26) MRNNT_PUT(27) MRNNT_PUT(28) MRNNT_PUT(29) MRNNT_PUT(30) MRNNT_PUT(31)
-#undef MRNNT_PUT
-        default: break;
-    }
-}
-
-template <class F, int... I>
-__device__ __forceinline__ void static_for_impl(F &f, std::integer_sequence<int, I...>) {
-    (f(std::integral_constant<int, I>{}), ...);
-}
-template <int N, class F>
-__device__ __forceinline__ void static_for(F &&f) {
-    static_for_impl(f, std::make_integer_sequence<int, N>{});
-}
-
-// One pipelined chunk, scheduled by hand: the KS MFMAs of the chunk (A fragments through a 3-deep LDS read ring) and,
-// in their gaps, the online softmax of the previous chunk's accumulator (35 work units, EPI) and the next tile's
-// fragment from its loaded enc / pred slices with its two blank / label dot products (18 work units), spread evenly;
-// a sched_barrier after each gap keeps this order (the compiler otherwise issues the MFMAs back to back and the VALU
-// after them, MI355X_MICROARCH.md 'MFMA gap' rows: <= 5 issues per 32x32x16 gap hide).
-template <int KS, bool EPI, int NMEM = 0, class Mem = std::nullptr_t>
-__device__ __forceinline__ f32x16 pipe_chunk(const unsigned short *wbuf, const bf16x8 (&bfr)[KS], int lane,
-                                             const f32x16 &accp, const float *bias_c, float &m, float &sum,
-                                             const FragIn &cur, bf16x8 &hout, float &zbd, float &zed,
-                                             Mem &&mem = nullptr) {
-    constexpr int H = 16 * KS, D = 3, NS = 35, NBU = 18;
-    const int r = lane & 31, hf = lane >> 5;
-    const unsigned short *row = wbuf + r * H;
-    const unsigned short *base[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) base[k] = row + 8 * ((2 * k + hf) ^ (r & 15));
-    auto rd = [&](int ks) { return *reinterpret_cast<const bf16x8 *>(base[ks & 7] + 128 * (ks >> 3)); };
-    bf16x8 a[D];
-#pragma unroll
-    for (int d = 0; d < D; ++d) a[d] = rd(d);
-    f32x16 acc;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
-    // softmax state
-    f4 bv[4];
-    f2 z[8];
-    float cm = 0.0f, mn = 0.0f, mr = 0.0f, nb = 0.0f, s0 = 0.0f, s1 = 0.0f;
-    // build state
-    float xin[8], ex[8];
-    unsigned hu[4];
-    auto sm_unit = [&](auto uc) {
-        constexpr int u = decltype(uc)::value;
-        if constexpr (u == 0) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) bv[q] = *reinterpret_cast<const f4 *>(bias_c + 8 * q);
-        } else if constexpr (u <= 8) {
-            constexpr int k = u - 1, q = k >> 1, o = 4 * q + 2 * (k & 1);
-            z[k] = (f2){accp[o] + ((k & 1) ? bv[q].z : bv[q].x), accp[o + 1] + ((k & 1) ? bv[q].w : bv[q].y)};
-        } else if constexpr (u == 9) {
-            cm = fmaxf(z[0].x, z[0].y);
-        } else if constexpr (u <= 16) {
-            cm = max3(cm, z[u - 9].x, z[u - 9].y);
-        } else if constexpr (u == 17) {
-            mn = fmaxf(m, cm);
-            mr = (mn == NEG_INF_F) ? 0.0f : mn;
-            nb = -mr * kLog2e;
-        } else if constexpr (u <= 33) {
-            constexpr int e = u - 18, k = e >> 1;
-            if constexpr (e & 1) s1 += fast_exp2(fmaf(z[k].y, kLog2e, nb));
-            else s0 += fast_exp2(fmaf(z[k].x, kLog2e, nb));
-        } else {
-            sum = sum * fast_exp2((m - mr) * kLog2e) + (s0 + s1);
-            m = mn;
-        }
-    };
-    auto b_unit = [&](auto uc) {
-        constexpr int u = decltype(uc)::value;
-        if constexpr (u < 16) {
-            constexpr int w2 = u >> 1, w = w2 >> 1;
-            if constexpr ((u & 1) == 0) {
-                xin[w2] = (w2 & 1) ? bf16_hi(cur.e[w]) + bf16_hi(cur.p[w]) : bf16_lo(cur.e[w]) + bf16_lo(cur.p[w]);
-                ex[w2] = fast_exp2(fabsf(xin[w2]) * (-2.0f * kLog2e));
-            } else {
-                xin[w2] = copysignf((1.0f - ex[w2]) * __builtin_amdgcn_rcpf(1.0f + ex[w2]), xin[w2]);
-                if constexpr (w2 & 1) {
-                    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-                    hu[w] = __builtin_bit_cast(unsigned, __builtin_convertvector((f2){xin[w2 - 1], xin[w2]}, bf16x2));
-                }
-            }
-        } else if constexpr (u == 16) {
-            hout = __builtin_bit_cast(bf16x8, (u4){hu[0], hu[1], hu[2], hu[3]});
-            zbd = dot8(hout, cur.wb, 0.0f);
-        } else {
-            zed = dot8(hout, cur.wl, 0.0f);
-        }
-    };
-    static_for<KS>([&](auto kc) {
-        constexpr int ks = decltype(kc)::value;
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks % D], bfr[ks], acc, 0, 0, 0);
-        if constexpr (ks + D < KS) a[ks % D] = rd(ks + D);
-        if constexpr (EPI) {
-            constexpr int lo = ks * NS / KS, hi = (ks + 1) * NS / KS;
-            static_for<hi - lo>([&](auto ic) { sm_unit(std::integral_constant<int, lo + decltype(ic)::value>{}); });
-        }
-        constexpr int blo = ks * NBU / KS, bhi = (ks + 1) * NBU / KS;
-        static_for<bhi - blo>([&](auto ic) { b_unit(std::integral_constant<int, blo + decltype(ic)::value>{}); });
-        if constexpr (NMEM > 0 && ks < KS / 2) {  // the next chunk's DMA and the next fragment's loads: first half
-            constexpr int mlo = ks * NMEM / (KS / 2), mhi = (ks + 1) * NMEM / (KS / 2);
-            static_for<mhi - mlo>([&](auto ic) { mem(std::integral_constant<int, mlo + decltype(ic)::value>{}); });
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    });
-    return acc;
-}
-
-template <int KS, int NB, bool PIPE, bool MEMGAP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void joint_fwd_pipe_kernel(DevProblem p,
-                                                                                                   JointArgs j) {
-    static_assert(KS <= 32, "put_frag covers 32 fragments");
-    using WT = WTile<KS>;
-    constexpr int NW = 4, ROWS = 32 * NW;
-    extern __shared__ __attribute__((aligned(16))) unsigned short wsh[];
-    const int64_t ntiles = (list_len(j) + ROWS - 1) / ROWS;
-    int64_t tile = blockIdx.x;
-    if (tile >= ntiles) return;
-    const int lane = threadIdx.x & 63, half = lane >> 5, wave = threadIdx.x >> 6;
-    const int V = p.V, blank = p.blank;
-    const int nch = (V + 31) / 32;
-    const float *bias = load_bias<KS, NB>(j, V, wsh);
-    auto row_of = [&](int64_t t) { return t * ROWS + wave * 32 + (lane & 31); };
-
-    // the W chunk stream runs on across tiles (chunk index wrapping at nch, buffer at NB); NB - 1 chunks in flight
-    int c_issue = 0, b_issue = 0, b_use = 0;
-    auto stage_next = [&]() {
-        WT::template stage<NW>(j, V, c_issue, wsh + b_issue * WT::ELEMS);
-        c_issue = c_issue + 1 == nch ? 0 : c_issue + 1;
-        b_issue = b_issue + 1 == NB ? 0 : b_issue + 1;
-    };
-#pragma unroll
-    for (int k = 0; k < NB - 1; ++k) stage_next();
-
-    // prologue: the first tile's activations and blank / label dot products, outside the MFMA loop
-    RowPos q = row_pos(p, j, row_of(tile));
-    bf16x8 bcur[KS], bnext[KS];
-    float zb = 0.0f, ze = 0.0f;
-    {
-        const RowSrc r = row_src<KS>(j, q, half, blank);
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-            const FragIn in = frag_load(r, ks);
-            bcur[ks] = act8(in.e, in.p);
-            zb = PIPE ? dot8(bcur[ks], in.wb, zb) : dot8f(bcur[ks], in.wb, zb);
-            ze = PIPE ? dot8(bcur[ks], in.wl, ze) : dot8f(bcur[ks], in.wl, ze);
-        }
-    }
-    __syncthreads();  // bias in LDS
-
-    for (;;) {
-        const int64_t tnext = tile + gridDim.x;
-        const RowPos qn = row_pos(p, j, row_of(tnext));  // past the list: builds from row 0, never written
-        const RowSrc rn = row_src<KS>(j, qn, half, blank);
-        float zbn = 0.0f, zen = 0.0f, m = NEG_INF_F, sum = 0.0f;
-        FragIn in = frag_load(rn, 0);
-        f32x16 accp;
-        // chunk c: the 32 MFMAs of chunk c, the softmax of chunk c - 1 and fragment c of the next tile in one basic
-        // block (no branch between them), so the scheduler can place the VALU in the MFMA gaps
-        auto body = [&](int c, auto epi_tag) {
-            wait_dma();  // chunk c's DMA and fragment c's inputs (issued one chunk ago)
-            __builtin_amdgcn_s_barrier();
-            const FragIn cur = in;
-            if constexpr (!MEMGAP) {
-                stage_next();
-                in = frag_load(rn, min(c + 1, KS - 1));
-            }
-            bf16x8 h;
-            float zbd, zed;
-            f32x16 acc;
-            if constexpr (MEMGAP) {  // the DMA pieces and the fragment loads in the MFMA gaps too
-                constexpr int NPW = WT::NI / NW;
-                unsigned short *wb_is = wsh + b_issue * WT::ELEMS;
-                const int c_is = c_issue;
-                acc = pipe_chunk<KS, decltype(epi_tag)::value, NPW + 1>(
-                    wsh + b_use * WT::ELEMS, bcur, lane, accp, bias + 32 * (c - 1) + 4 * half, m, sum, cur, h, zbd,
-                    zed, [&](auto uc) {
-                        constexpr int u = decltype(uc)::value;
-                        if constexpr (u < NPW) WT::template stage_piece<NW>(j, V, c_is, wb_is, u);
-                        else in = frag_load(rn, min(c + 1, KS - 1));
-                    });
-                c_issue = c_issue + 1 == nch ? 0 : c_issue + 1;
-                b_issue = b_issue + 1 == NB ? 0 : b_issue + 1;
-            } else if constexpr (PIPE) {
-                acc = pipe_chunk<KS, decltype(epi_tag)::value>(wsh + b_use * WT::ELEMS, bcur, lane, accp,
-                                                               bias + 32 * (c - 1) + 4 * half, m, sum, cur, h, zbd, zed);
-            } else {  // development check: the same stream and build, compiler-scheduled
-                acc = WT::template mma<2>(wsh + b_use * WT::ELEMS, bcur, lane);
-                if constexpr (decltype(epi_tag)::value) softmax_chunk(accp, bias, c - 1, half, m, sum);
-                h = act8(cur.e, cur.p);
-                zbd = dot8f(h, cur.wb, 0.0f);
-                zed = dot8f(h, cur.wl, 0.0f);
-            }
-            b_use = b_use + 1 == NB ? 0 : b_use + 1;
-            {  // keep all of it in the chunk's block (the compiler would sink it past the fragment switch)
-                u4 hv = __builtin_bit_cast(u4, h);
-                asm volatile("" : "+v"(m), "+v"(sum), "+v"(zbd), "+v"(zed), "+v"(hv));
-                h = __builtin_bit_cast(bf16x8, hv);
-            }
-            const float carry = c < KS ? 1.0f : 0.0f;  // chunks past the last fragment carry nothing (branch-free)
-            zbn = fmaf(carry, zbd, zbn);
-            zen = fmaf(carry, zed, zen);
-            put_frag<KS>(bnext, c, h);
-            accp = acc;
-        };
-        body(0, std::false_type{});
-        for (int c = 1; c < nch; ++c) body(c, std::true_type{});
-        softmax_chunk(accp, bias, nch - 1, half, m, sum);
-        for (int f = nch; f < KS; ++f) {  // V < 32 KS: the fragments no chunk carried
-            const FragIn fi = frag_load(rn, f);
-            const bf16x8 h = act8(fi.e, fi.p);
-            zbn = dot8(h, fi.wb, zbn);
-            zen = dot8(h, fi.wl, zen);
-            put_frag<KS>(bnext, f, h);
-        }
-        // finish the current tile: merge the two lane halves (same row, disjoint vocabulary / k)
-        {
-            const float m2 = __shfl_xor(m, 32), s2 = __shfl_xor(sum, 32);
-            const float zbt = zb + __shfl_xor(zb, 32), zet = ze + __shfl_xor(ze, 32);
-            const float mn = fmaxf(m, m2);
-            const float mr = (mn == NEG_INF_F) ? 0.0f : mn;
-            const float st = sum * fast_exp2((m - mr) * kLog2e) + s2 * fast_exp2((m2 - mr) * kLog2e);
-            if (q.valid && half == 0) {
-                const double den = -(double)mn - log_row_sum(st);
-                const float bb = j.bias ? j.bias[blank] : 0.0f;
-                const float bl = (j.bias && q.lab >= 0) ? j.bias[q.lab] : 0.0f;
-                p.den[q.row] = (float)den;
-                p.lp[q.row] = Lp{(double)(zbt + bb) + den,
-                                 (q.lab >= 0 ? (double)(zet + bl) : (q.lab == -2 ? __builtin_nan("") : 0.0)) + den};
-            }
-        }
-        tile = tnext;
-        if (tile >= ntiles) break;
-        q = qn;
-        zb = zbn;
-        ze = zen;
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) bcur[ks] = bnext[ks];
-    }
-    wait_dma();  // the stream's last DMA must land before the workgroup's LDS is released
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -1497,16 +873,15 @@ hipError_t launch_joint_reduce(const DevProblem &p, const JointArgs &j, const in
     return hipGetLastError();
 }
 
-// kernel of a launch shape: MF = MFMA tile (32: 32x32x16, 16: 16x16x32), RG = A-fragment ring of the 32x32 tile
-template <int KS, int NB, int NW, int MF, bool BWD, int RG, int OPT = 0>
+// kernel of a launch shape: MF = the backward's MFMA tile (32: 32x32x16, 16: 16x16x32); the forward runs 32x32x16
+template <int KS, int NB, int NW, int MF, bool BWD, int RG>
 static hipError_t launch_knw(const DevProblem &p, const JointArgs &j, size_t lds, hipStream_t stream) {
     const int64_t blocks = (j.n + 32 * NW - 1) / (32 * NW);
     if (blocks * 64 * NW > 0xffffffffll) return hipErrorInvalidValue;  // 32-bit dispatch size in work-items
     void (*kern)(DevProblem, JointArgs);
     if constexpr (MF == 16 && BWD) kern = joint_bwd16_kernel<KS, NB, NW>;
-    else if constexpr (MF == 16) kern = joint_fwd16_kernel<KS, NB, NW>;
     else if constexpr (BWD) kern = joint_bwd_kernel<KS, NB, NW, RG>;
-    else kern = joint_fwd_kernel<KS, NB, NW, RG, OPT>;
+    else kern = joint_fwd_kernel<KS, NB, NW, RG>;
     if (lds > 65536) {
         const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1516,107 +891,28 @@ static hipError_t launch_knw(const DevProblem &p, const JointArgs &j, size_t lds
     return hipGetLastError();
 }
 
-// One workgroup of 8 waves per CU (two per SIMD, 256 rows sharing each W chunk), two DMA buffers; the development
-// build adds three buffers (joint_nbuf = 3), 4-wave workgroups (joint_nw = 4) and deeper A-fragment rings
-// (joint_ring = 4 / 8) of the 32x32 tile.
+// One workgroup of 8 waves per CU (two per SIMD, 256 rows sharing each W chunk), two DMA buffers. (Measured and
+// removed, DESIGN.md §4a: three buffers, two 4-wave workgroups per CU, deeper A-fragment rings, the forward on the
+// 16x16x32 tile, a persistent forward, the pipelined one-wave-per-SIMD forward, the bias as the initial accumulator
+// and the label logit as a dot product.)
 template <int KS, int MF, bool BWD>
 static hipError_t launch_kt(const DevProblem &p, const JointArgs &j, hipStream_t stream) {
     // the 16x16x32 backward keeps its dbias column sums behind the bias
     const size_t bias = sizeof(float) * ((p.V + 31) / 32 * 32) * (MF == 16 && BWD ? 2 : 1);
     if (j.dbias && !(MF == 16 && BWD)) return hipErrorInvalidValue;
     const size_t tile = sizeof(unsigned short) * WTile<KS>::ELEMS;
-    if constexpr (kVariants) {
-        if (tuning().joint_nbuf >= 3 && 3 * tile + bias <= 160 * 1024)
-            return launch_knw<KS, 3, 8, MF, BWD, 2>(p, j, 3 * tile + bias, stream);
-        // 4-wave workgroups, two per CU when their LDS fits twice: each wave still shares its SIMD with one other,
-        // now of ANOTHER workgroup, which started at another time -- one's activation build can overlap the other's
-        // MFMAs; 128 rows share each W chunk
-        if (tuning().joint_nw == 4 && WTile<KS>::NI % 4 == 0 && 2 * (2 * tile + bias) <= 160 * 1024)
-            return launch_knw<KS, 2, 4, MF, BWD, 2>(p, j, 2 * tile + bias, stream);
-        if constexpr (MF == 32 && !BWD) {
-            const int o = tuning().joint_fwd_opt;
-            if (2 * tile + bias <= 160 * 1024 && o == 1) return launch_knw<KS, 2, 8, MF, BWD, 2, 1>(p, j, 2 * tile + bias, stream);
-            if (2 * tile + bias <= 160 * 1024 && o == 2) return launch_knw<KS, 2, 8, MF, BWD, 2, 2>(p, j, 2 * tile + bias, stream);
-            if (2 * tile + bias <= 160 * 1024 && o == 3) return launch_knw<KS, 2, 8, MF, BWD, 2, 3>(p, j, 2 * tile + bias, stream);
-        }
-        if constexpr (MF == 32 && (KS == 16 || KS == 32)) {
-            if (2 * tile + bias <= 160 * 1024 && tuning().joint_ring == 4)
-                return launch_knw<KS, 2, 8, MF, BWD, 4>(p, j, 2 * tile + bias, stream);
-            if (2 * tile + bias <= 160 * 1024 && tuning().joint_ring == 8)
-                return launch_knw<KS, 2, 8, MF, BWD, 8>(p, j, 2 * tile + bias, stream);
-        }
-    }
     if (2 * tile + bias <= 160 * 1024) return launch_knw<KS, 2, 8, MF, BWD, 2>(p, j, 2 * tile + bias, stream);
     return hipErrorInvalidValue;
 }
 
-// MFMA tile per pass: the tuned defaults only in the product library (forward 32x32x16, backward 16x16x32: the
-// backward's epilogue carries no per-row running state, and there the 16x16 tile's higher clock pays; the forward's
-// two rows of online-softmax state per lane cost more than it gains); both in the development build (joint_mfma,
-// joint_bwd_mfma). H = 640 keeps the 32x32 tile everywhere (the 16x16 one spills there: two rows' state per lane
-// beside 160 B-operand registers).
-static int cu_count() {
-    static int n[64] = {0};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
-    if (n[dev] == 0) {
-        int c = 0;
-        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
-        n[dev] = c;
-    }
-    return n[dev];
-}
-
-// the pipelined forward: one persistent 4-wave workgroup per CU (its 512-register waves fill the CU's register file)
-template <int KS>
-static hipError_t launch_pipe(const DevProblem &p, const JointArgs &j, hipStream_t stream) {
-    const size_t lds = 2 * sizeof(unsigned short) * WTile<KS>::ELEMS + sizeof(float) * ((p.V + 31) / 32 * 32);
-    if (lds > 160 * 1024) return hipErrorInvalidValue;
-    const int64_t tiles = (j.n + 127) / 128;
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(tiles, cu_count()));
-    auto kern = joint_fwd_pipe_kernel<KS, 2, true, true>;
-    if constexpr (kVariants) {
-        if (tuning().joint_pipe == 2) kern = joint_fwd_pipe_kernel<KS, 2, false, false>;
-        if (tuning().joint_pipe == 3) kern = joint_fwd_pipe_kernel<KS, 2, true, false>;
-    }
-    if (lds > 65536) {
-        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-    }
-    kern<<<grid, 256, lds, stream>>>(p, j);
-    return hipGetLastError();
-}
-
-// the persistent 8-wave forward: one workgroup per CU
-template <int KS>
-static hipError_t launch_persist(const DevProblem &p, const JointArgs &j, hipStream_t stream) {
-    const size_t lds = 2 * sizeof(unsigned short) * WTile<KS>::ELEMS + sizeof(float) * ((p.V + 31) / 32 * 32);
-    if (lds > 160 * 1024) return hipErrorInvalidValue;
-    const int64_t tiles = (j.n + 255) / 256;
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(tiles, cu_count()));
-    auto kern = joint_fwd_persist_kernel<KS, 2, 8>;
-    if (lds > 65536) {
-        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-    }
-    kern<<<grid, 512, lds, stream>>>(p, j);
-    return hipGetLastError();
-}
-
+// The backward's MFMA tile: 16x16x32 for H <= 512 (its epilogue carries no per-row running state, and there the
+// 16x16 tile's higher clock pays), 32x32x16 at H = 640 (the 16x16 one spills there: two rows' state per lane beside
+// 160 B-operand registers); the development build can force 32x32x16 (joint_bwd_mfma = 32).
 template <int KS, bool BWD>
 static hipError_t launch_kb(const DevProblem &p, const JointArgs &j, hipStream_t stream) {
-    constexpr int kDefault = KS > 32 ? 32 : BWD ? Tuning{}.joint_bwd_mfma : Tuning{}.joint_mfma;
-    if constexpr (!BWD && (kVariants || Tuning{}.joint_fwd_persist)) {
-        if (tuning().joint_fwd_persist) return launch_persist<KS>(p, j, stream);
-    }
-    if constexpr (!BWD && KS <= 32 && (kVariants || Tuning{}.joint_pipe)) {
-        if (tuning().joint_pipe) return launch_pipe<KS>(p, j, stream);
-    }
-    if constexpr (kVariants && KS <= 32) {
-        const int mf = BWD ? tuning().joint_bwd_mfma : tuning().joint_mfma;
-        return mf == 16 ? launch_kt<KS, 16, BWD>(p, j, stream) : launch_kt<KS, 32, BWD>(p, j, stream);
+    constexpr int kDefault = KS > 32 ? 32 : BWD ? Tuning{}.joint_bwd_mfma : 32;
+    if constexpr (kVariants && KS <= 32 && BWD) {
+        if (tuning().joint_bwd_mfma == 32) return launch_kt<KS, 32, BWD>(p, j, stream);
     }
     return launch_kt<KS, kDefault, BWD>(p, j, stream);
 }

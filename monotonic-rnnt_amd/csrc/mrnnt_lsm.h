@@ -21,9 +21,15 @@ __device__ __forceinline__ void st_lp(const DevProblem &p, int64_t row, Lp v) {
 
 // rows of the column that are not reduced: finite lp (the recursion reads them, masked) and den (the gradient's
 // per-row coefficient of such a row meets alpha or beta = -inf and comes out exactly 0)
-template <bool WT>
-__device__ __forceinline__ void zero_fill_outside_band(const DevProblem &p, int64_t rowc, int S, int lo, int hi) {
-    for (int s = threadIdx.x; s <= S; s += blockDim.x)
+// NWV: the waves sharing the column (4: the whole workgroup; 1: one wave alone, the chase launch's self-help), rows
+// [rlo, rhi] of the column only
+template <bool WT, int NWV = 4>
+__device__ __forceinline__ void zero_fill_outside_band(const DevProblem &p, int64_t rowc, int S, int lo, int hi,
+                                                       int rlo = 0, int rhi = 1 << 30) {
+    const int first = NWV == 1 ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
+    const int stride = NWV == 1 ? 64 : (int)blockDim.x;
+    const int end = min(S, rhi);
+    for (int s = rlo + first; s <= end; s += stride)
         if (s < lo || s > hi) {
             st_lp<WT>(p, rowc + s, Lp{0.0, 0.0});
             p.den[rowc + s] = 0.0f;
@@ -61,13 +67,17 @@ __device__ __forceinline__ float lane_pick(const float (&x)[N], int k) {
 // ONE: the row is a single chunk (VL <= 64 U, every configuration up to V = 1024): the wave max is reduced first and
 // every lane's exps are taken against it, so there is no per-lane running max, no rescale of lane partial sums
 // before the wave sum (one exp and its bookkeeping per row fewer), and the R rows' DPP chains interleave.
-template <class IO, int U, int R, bool NTL, bool FULL, bool ONE, bool WT>
-__device__ __forceinline__ void lean_column(const DevProblem &p, const ColRef &k) {
+// NWV / wv / [rlo, rhi]: the waves sharing the column, this wave's index among them and the rows to produce (the
+// producers: 4 waves, every row; the chase launch's self-help: one wave, the rows its recursion lanes read). A row's
+// value does not depend on which rows share its pass, so every split produces the same bits.
+template <class IO, int U, int R, bool NTL, bool FULL, bool ONE, bool WT, int NWV = 4>
+__device__ __forceinline__ void lean_column(const DevProblem &p, const ColRef &k, int wv = -1, int rlo = 0,
+                                            int rhi = 1 << 30) {
     constexpr int E = IO::E;
     constexpr int CH = 64 * U;  // vectors per chunk
     typedef typename IO::V Vec;
     const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wave = wv >= 0 ? wv : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int VL = p.V / E;
     const Vec *__restrict__ av = reinterpret_cast<const Vec *>(p.acts);
     const int blank = p.blank;
@@ -79,10 +89,12 @@ __device__ __forceinline__ void lean_column(const DevProblem &p, const ColRef &k
     int lo = max(0, t - (T - S)), hi = min(t, S);
     align_window(p, c, t, lo, hi);
     const int *__restrict__ lab_b = p.labels + (int64_t)b * p.label_stride;
-    zero_fill_outside_band<WT>(p, rowc, S, lo, hi);
+    zero_fill_outside_band<WT, NWV>(p, rowc, S, lo, hi, rlo, rhi);
+    lo = max(lo, rlo);
+    hi = min(hi, rhi);
 
     if constexpr (ONE) {
-        for (int s = lo + wave * R; s <= hi; s += 4 * R) {
+        for (int s = lo + wave * R; s <= hi; s += NWV * R) {
             const int nrow = __builtin_amdgcn_readfirstlane(min(R, hi - s + 1));
             Vec x[R][U];
 #pragma unroll
@@ -145,7 +157,7 @@ __device__ __forceinline__ void lean_column(const DevProblem &p, const ColRef &k
         }
         return;  // next column
     }
-    for (int s = lo + wave * R; s <= hi; s += 4 * R) {
+    for (int s = lo + wave * R; s <= hi; s += NWV * R) {
         const int nrow = __builtin_amdgcn_readfirstlane(min(R, hi - s + 1));
         float m[R], sum[R], zb[R], ze[R];
         int lab[R];
@@ -245,14 +257,15 @@ __device__ __forceinline__ float dpp16(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, 0xf, 0xf, false));
 }
 
-template <class IO, int NR, bool NTL, bool WT>
-__device__ __forceinline__ void row16_column(const DevProblem &p, const ColRef &k) {
+template <class IO, int NR, bool NTL, bool WT, int NWV = 4>
+__device__ __forceinline__ void row16_column(const DevProblem &p, const ColRef &k, int wv = -1, int rlo = 0,
+                                             int rhi = 1 << 30) {
     constexpr int E = IO::E;
     typedef typename IO::V Vec;
     typedef typename IO::S Sc;
     const int lane = threadIdx.x & 63;
     const int g = lane >> 4, l16 = lane & 15;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wave = wv >= 0 ? wv : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int VL = p.V / E;  // <= 64: up to 4 vectors per lane of a group
     const Vec *__restrict__ av = reinterpret_cast<const Vec *>(p.acts);
     const Sc *__restrict__ as = reinterpret_cast<const Sc *>(p.acts);
@@ -265,10 +278,12 @@ __device__ __forceinline__ void row16_column(const DevProblem &p, const ColRef &
     int lo = max(0, t - (T - S)), hi = min(t, S);
     align_window(p, c, t, lo, hi);
     const int *__restrict__ lab_b = p.labels + (int64_t)b * p.label_stride;
-    zero_fill_outside_band<WT>(p, rowc, S, lo, hi);
+    zero_fill_outside_band<WT, NWV>(p, rowc, S, lo, hi, rlo, rhi);
+    lo = max(lo, rlo);
+    hi = min(hi, rhi);
 
-    // wave w, pass k: rows lo + 16 k + 4 NR w + 4 r + g (r < NR) -- a row per 16-lane group
-    for (int s0 = lo + wave * 4 * NR; s0 <= hi; s0 += 16 * NR) {
+    // wave w, pass k: rows lo + 4 NWV NR k + 4 NR w + 4 r + g (r < NR) -- a row per 16-lane group
+    for (int s0 = lo + wave * 4 * NR; s0 <= hi; s0 += NWV * 4 * NR) {
         Vec x[NR][4];
         float zb[NR], ze[NR];
         bool ok[NR];

@@ -205,10 +205,11 @@ __global__ __launch_bounds__(64 * NW) void recursion_halo_kernel(DevProblem p, i
     const int b = with_beta ? (int)(blockIdx.x >> 1) : (int)blockIdx.x;
     const bool bwd = with_beta && (blockIdx.x & 1);
     if (dyn_failed(p, b, bwd, costs)) return;
+    const Utt u = utt_of(p, b);
     if (bwd)
-        beta_pass_halo<D, NW, HL, BAND, LEAN>(p, b, xh);
+        beta_pass_halo<D, NW, HL, BAND, LEAN>(p, u, b, xh);
     else
-        alpha_pass_halo<D, NW, HL, BAND, LEAN>(p, b, costs, xh);
+        alpha_pass_halo<D, NW, HL, BAND, LEAN>(p, u, b, costs, xh);
 }
 
 template <int NW, int HL = 8>

@@ -27,6 +27,14 @@ int mrnnt_read_probe(const void *src, size_t bytes, void *sink, hipStream_t stre
  * the copy probe alone. */
 int mrnnt_write_probe(void *dst, size_t bytes, hipStream_t stream);
 
+/* out[2 * slot] = the dispatch id the launch sees (the AQL packet index of its queue), out[2 * slot + 1] = its queue
+ * address: what makes the chase launch's ready tags unique per launch, including HIP-graph replays. */
+int mrnnt_dispatch_probe(uint64_t *out, int slot, hipStream_t stream);
+
+/* Occupies every workgroup slot it gets (blocks_per_cu 256-thread workgroups per CU) for `us` microseconds of the
+ * constant 100 MHz clock, then exits: a co-running kernel that holds the CUs, for scheduling tests. */
+int mrnnt_occupy(int us, int blocks_per_cu, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

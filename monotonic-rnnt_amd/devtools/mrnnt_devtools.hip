@@ -92,6 +92,21 @@ __global__ __launch_bounds__(256) void read_probe_kernel(const u4 *__restrict__ 
     if (acc == 0x9E3779B9u) sink[0] = acc;  // practically never: the loads cannot be dropped
 }
 
+extern "C" __device__ uint64_t mrnnt_dev_dispatch_id() __asm("llvm.amdgcn.dispatch.id");
+
+__global__ void dispatch_probe_kernel(uint64_t *out, int slot) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        out[2 * slot] = mrnnt_dev_dispatch_id();
+        out[2 * slot + 1] = (uint64_t)(uintptr_t)__builtin_amdgcn_queue_ptr();
+    }
+}
+
+// every wave sleeps until `ticks` of the 100 MHz constant clock have passed since its workgroup started
+__global__ __launch_bounds__(256) void occupy_kernel(uint64_t ticks) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(32);
+}
+
 // slab size and grid of the probes: 32 workgroups per CU, each streaming >= 8 slabs in turn (a single pass
 // of one slab per workgroup measures the launch tail, not the memory); slabs of 16 KiB .. 800 KiB
 int probe_grid(int64_t n, int64_t *slab, int64_t *blocks) {
@@ -160,6 +175,24 @@ int mrnnt_write_probe(void *dst, size_t bytes, hipStream_t stream) {
     const hipError_t stale = hipGetLastError();
     write_probe_kernel<<<(int)blocks, 256, 0, stream>>>(static_cast<u4 *>(dst), n, slab);
     return launch_status("write probe", stale);
+}
+
+int mrnnt_dispatch_probe(uint64_t *out, int slot, hipStream_t stream) {
+    if (!out || slot < 0) return 2;
+    const hipError_t stale = hipGetLastError();
+    dispatch_probe_kernel<<<1, 64, 0, stream>>>(out, slot);
+    return launch_status("dispatch probe", stale);
+}
+
+int mrnnt_occupy(int us, int blocks_per_cu, hipStream_t stream) {
+    if (us < 0 || us > 10000000 || blocks_per_cu < 1 || blocks_per_cu > 8) return 2;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return 3;
+    const hipError_t stale = hipGetLastError();
+    occupy_kernel<<<cus * blocks_per_cu, 256, 0, stream>>>((uint64_t)us * 100);
+    return launch_status("occupy", stale);
 }
 
 }  // extern "C"

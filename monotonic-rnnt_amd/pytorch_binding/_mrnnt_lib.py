@@ -152,6 +152,7 @@ def _bind(path: str, dev: bool = False) -> ctypes.CDLL:
     }
     if dev:
         sig["mrnnt_tune"] = (i, [ctypes.c_char_p, i])
+        sig["mrnnt_chase_helped"] = (ctypes.c_ulonglong, [i])
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
         fn.restype = res
@@ -221,6 +222,10 @@ def devtools() -> ctypes.CDLL:
             t.mrnnt_write_probe.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
             t.mrnnt_read_probe.restype = ctypes.c_int
             t.mrnnt_read_probe.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
+            t.mrnnt_dispatch_probe.restype = ctypes.c_int
+            t.mrnnt_dispatch_probe.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+            t.mrnnt_occupy.restype = ctypes.c_int
+            t.mrnnt_occupy.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
             _tools = t
         return _tools
 

@@ -1,12 +1,16 @@
-"""The chase launch (mrnnt_chase.hip): log-softmax and alpha / beta recursion in one launch, the
-recursion workgroups consuming each lattice column as its log-softmax workgroup publishes it (write-through rows +
-a ready flag per column, Guideline 16 R1). The reference runs the two back to back (gpu_rnnt.h:99-191).
+"""The chase launch (mrnnt_chase.hip): log-softmax and alpha / beta recursion in
+one launch, the recursion workgroups consuming each lattice column as its log-softmax workgroup publishes it
+(write-through rows + a ready flag per column, Guideline 16 R1). The reference runs the two back to back
+(gpu_rnnt.h:99-191).
 
 Every value the chase computes is the one the two-kernel path computes, so the tests compare bit for bit against
 the development build with the chase off (chase = 0), over every log-softmax body the chase carries (16-lane rows,
-single-chunk U = 2 / 4, full and partial chunks), both recursion shapes (one wave, 4-wave halo with idle waves),
-both prefetch depths, both acts load policies, ragged / odd / T = 1 / S = 0 lattices, the padded layout, forward
-only (alpha alone), HIP-graph replay (flags cleared by the memset node each replay) and two streams at once.
+single-chunk U = 2 / 4, full and partial chunks), both recursion shapes (one wave with its frames staged in LDS by a
+loader wave, or read directly; 4-wave halo with idle waves), both acts load policies, ragged / odd / T = 1 / S = 0
+lattices, the padded layout, forward only (alpha alone), host and device-resident lengths, HIP-graph replay (ready
+tags derived per launch from the dispatch id: no flag is ever cleared), two streams at once, and the progress
+guarantee: a recursion wave that waits too long for a column computes it itself (budget 0: every column; producers
+held back; a kernel holding the CUs on another stream) -- still the same bits.
 """
 import numpy as np
 import pytest
@@ -83,19 +87,24 @@ def _assert_same(a, b):
         assert torch.equal(ga.view(torch.int32), gb.view(torch.int32))
 
 
-@pytest.mark.parametrize("depth", [16, 8])
+@pytest.mark.parametrize("stage", [1, 0])
 @pytest.mark.parametrize("name", list(CASES))
-def test_chase_bit_identical_to_two_kernels(op, dev, name, depth):
+def test_chase_bit_identical_to_two_kernels(op, dev, name, stage):
+    """stage: the one-wave recursion's frames staged in LDS by a loader wave (the product) or read directly."""
     acts, labels, T, S, a, lab = _problem(name, dev)
     Tt, St = torch.from_numpy(T), torch.from_numpy(S)
     scale = torch.linspace(0.5, 2.0, len(T), device=dev)
     with knobs(chase=0):
         ref = _run(op, a, lab, Tt, St, scale=scale)
-    with knobs(chase=1, chase_depth=depth):
+    with knobs(chase=1, chase_stage=stage):
         n = _launches(lambda: _run(op, a, lab, Tt, St, scale=scale))
         got = _run(op, a, lab, Tt, St, scale=scale)
     assert n["chase"] == 1 and n["log_softmax"] == 0 and n["alpha_beta"] == 0, n
     _assert_same(got, ref)
+    if name.startswith("c2"):  # the product library takes the same launch
+        n = _launches(lambda: _run(op, a, lab, Tt, St, scale=scale))
+        assert n["chase"] == 1, n
+        _assert_same(_run(op, a, lab, Tt, St, scale=scale), ref)
     if name.startswith("c2") or name.startswith("ragged"):
         cr, gr = O.oracle_rnnt(acts, labels, T, S)
         assert_costs(got[0].cpu().numpy().astype(np.float64), cr)
@@ -157,11 +166,15 @@ def test_chase_not_taken_outside_its_shapes(op, dev):
     assert n["chase"] == 0 and n["log_softmax"] == 1, n
 
 
-def test_chase_graph_replay_follows_new_acts(op, dev):
-    """A captured step replays the flag memset + the chase launch: every replay waits for its own producers (a
-    replay reading the previous replay's flags would return the previous acts' costs)."""
+@pytest.mark.parametrize("lengths", ["host", "device"])
+def test_chase_graph_replay_follows_new_acts(op, dev, lengths):
+    """A captured step replays the chase launch with the kernel arguments frozen at capture: every replay derives its
+    own ready tag from its dispatch id, so it waits for its own producers (a replay matching the previous replay's
+    flags would return the previous acts' costs)."""
     _, _, T, S, a0, lab = _problem("c2_row16_one_wave", dev)
     Tt, St = torch.from_numpy(T), torch.from_numpy(S)
+    if lengths == "device":
+        Tt, St = Tt.to(dev), St.to(dev)
     static = a0.clone().requires_grad_(True)
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
@@ -183,7 +196,7 @@ def test_chase_graph_replay_follows_new_acts(op, dev):
         g.replay()
         torch.cuda.synchronize()
         with knobs(chase=0):
-            ref = _run(op, new, lab, Tt, St)
+            ref = _run(op, new, lab, Tt.cpu(), St.cpu())
         _assert_same((costs.detach(), static.grad), ref)
 
 
@@ -208,3 +221,150 @@ def test_chase_two_streams_at_once(op, dev):
     torch.cuda.synchronize()
     _assert_same(outs["a"], ra)
     _assert_same(outs["b"], rb)
+
+
+def test_dispatch_ids_are_unique_per_replay(dev):
+    """The ready tags rest on this: every launch -- each kernel of each HIP-graph replay included -- sees its own
+    dispatch id (the AQL packet index on its queue)."""
+    import ctypes
+
+    import _mrnnt_lib as L
+    t = L.devtools()
+    out = torch.zeros(16, dtype=torch.int64, device=dev)
+    ptr = ctypes.c_void_p(out.data_ptr())
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            cs = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+            assert t.mrnnt_dispatch_probe(ptr, 0, cs) == 0
+            assert t.mrnnt_dispatch_probe(ptr, 1, cs) == 0
+    seen = []
+    for _ in range(4):
+        g.replay()
+        torch.cuda.synchronize()
+        v = out[:4].tolist()
+        seen += [v[0], v[2]]
+    assert len(set(seen)) == len(seen), seen
+
+
+@pytest.mark.parametrize("name", ["c2_row16_one_wave", "ragged_row16_t1_s0", "halo_u2_full_idle_waves",
+                                  "u4_partial_v1000"])
+def test_chase_device_lengths_bit_identical_to_host_lengths(op, dev, name):
+    """The reference's calling convention (lengths on the GPU, monotonic_rnnt.cu:85-88) takes the chase launch too:
+    the launch plans from acts.size(0) / labels.size(1), locates columns from the lengths in registers and publishes
+    the lattice for the gradient pass -- the same bits as host lengths and as the two-kernel path."""
+    acts, labels, T, S, a, _ = _problem(name, dev)
+    lab = torch.from_numpy(labels[:, :max(1, int(S.max()))].copy()).to(dev)  # tight label rows: the S_b bound
+    Tt, St = torch.from_numpy(T), torch.from_numpy(S)
+    Td, Sd = Tt.to(dev), St.to(dev)
+    scale = torch.linspace(0.5, 2.0, len(T), device=dev)
+    with knobs(chase=0):
+        ref = _run(op, a, lab, Tt, St, scale=scale)
+    host = _run(op, a, lab, Tt, St, scale=scale)
+    n = _launches(lambda: _run(op, a, lab, Td, Sd, scale=scale))
+    got = _run(op, a, lab, Td, Sd, scale=scale)
+    _assert_same(host, ref)
+    _assert_same(got, ref)
+    if name == "c2_row16_one_wave":
+        assert n["chase"] == 1 and n["setup"] == 0 and n["log_softmax"] == 0, n
+    with knobs(chase=1, chase_stage=0):
+        _assert_same(_run(op, a, lab, Td, Sd, scale=scale), ref)
+    op.check_lengths()
+
+
+def test_chase_device_lengths_invalid_is_nan_and_reported(op, dev):
+    """Device lengths that fail validation inside the chase launch: NaN costs and gradients, reported by
+    check_lengths() -- the same contract as the two-kernel path."""
+    _, _, T, S, a, lab = _problem("c2_row16_one_wave", dev)
+    T2 = T.copy()
+    T2[3] += 1  # sum_b T_b (S_b + 1) no longer matches acts.size(0)
+    Td, Sd = torch.from_numpy(T2).to(dev), torch.from_numpy(S).to(dev)
+    n = _launches(lambda: _run(op, a, lab, Td, Sd))
+    assert n["chase"] == 1, n
+    with pytest.raises(RuntimeError, match="failed validation"):
+        op.check_lengths()
+    c, g = _run(op, a, lab, Td, Sd)
+    assert torch.isnan(c).all() and torch.isnan(g).all()
+    with pytest.raises(RuntimeError, match="failed validation"):
+        op.check_lengths()
+
+
+def _helped(reset=True):
+    import _mrnnt_lib as L
+    return int(L.load_dev().mrnnt_chase_helped(1 if reset else 0))
+
+
+@pytest.mark.parametrize("stage", [1, 0])
+@pytest.mark.parametrize("name", ["c2_row16_one_wave", "ragged_row16_t1_s0", "halo_u2_full_idle_waves"])
+def test_chase_self_help_every_column_bit_identical(op, dev, name, stage):
+    """Wait budget 0: a recursion wave computes every column it does not find published itself, with the producers'
+    own column body on its rows -- the result does not change (and the columns were helped)."""
+    _, _, T, S, a, lab = _problem(name, dev)
+    Tt, St = torch.from_numpy(T), torch.from_numpy(S)
+    with knobs(chase=0):
+        ref = _run(op, a, lab, Tt, St)
+    with knobs(chase=1, chase_stage=stage, chase_wait_us=0, chase_delay_us=200):
+        _helped()
+        got = _run(op, a, lab, Tt, St)
+        helped = _helped()
+    _assert_same(got, ref)
+    assert helped > 0, helped
+
+
+def test_chase_producers_held_back_progress_and_replay(op, dev):
+    """Producers that start late (2 ms): the recursion waves give up waiting after 20 us and help themselves; the
+    producers still publish afterwards. Replaying the captured step on new logits must still follow them: late
+    publications of one launch never satisfy the next (its tag differs)."""
+    _, _, T, S, a0, lab = _problem("c2_row16_one_wave", dev)
+    Tt, St = torch.from_numpy(T), torch.from_numpy(S)
+    with knobs(chase=1, chase_wait_us=20, chase_delay_us=2000):
+        static = a0.clone().requires_grad_(True)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                static.grad = None
+                op.monotonic_rnnt_loss(static, lab, Tt, St).sum().backward()
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        static.grad = None
+        with torch.cuda.graph(g):
+            costs = op.monotonic_rnnt_loss(static, lab, Tt, St)
+            costs.sum().backward()
+        _helped()
+        gen = torch.Generator(device=dev).manual_seed(9)
+        news = []
+        for i in range(3):
+            new = torch.randn(a0.shape, device=dev, generator=gen)
+            news.append(new)
+            with torch.no_grad():
+                static.copy_(new)
+            g.replay()
+            torch.cuda.synchronize()
+            news[-1] = (new, costs.detach().clone(), static.grad.clone())
+        helped = _helped()
+    assert helped > 0
+    with knobs(chase=0):
+        for new, c, gr in news:
+            _assert_same((c, gr), _run(op, new, lab, Tt, St))
+
+
+def test_chase_beside_a_kernel_holding_the_cus(op, dev):
+    """A kernel on another stream occupies every workgroup slot of the chip for 30 ms while the chase launch starts:
+    its recursion workgroups and producers get the CUs piecemeal -- the costs are right, never NaN."""
+    import ctypes
+
+    import _mrnnt_lib as L
+    _, _, T, S, a, lab = _problem("c2_row16_one_wave", dev)
+    Tt, St = torch.from_numpy(T), torch.from_numpy(S)
+    with knobs(chase=0):
+        ref = _run(op, a, lab, Tt, St)
+    side = torch.cuda.Stream()
+    for k in range(3):
+        with torch.cuda.stream(side):
+            assert L.devtools().mrnnt_occupy(30000, 2 + 3 * k, ctypes.c_void_p(side.cuda_stream)) == 0
+        got = _run(op, a, lab, Tt, St)
+        _assert_same(got, ref)
+    torch.cuda.synchronize()

@@ -250,8 +250,9 @@ def test_pybind_names_with_device_lengths(op, dev, path):
 
 @pytest.mark.parametrize("B", [16, 70])
 def test_device_lengths_launch_count(op, dev, B):
-    """A batch of <= 64 utterances plans its lengths inside the log-softmax launch (no setup kernel at all); a larger
-    one runs exactly one setup kernel per forward -- never the host-lengths setup kernels."""
+    """A batch of <= 64 utterances plans its lengths inside its first launch (no setup kernel at all) -- here the
+    chase launch, which runs the whole forward (mrnnt_chase.hip); a larger one runs exactly one setup kernel per
+    forward, then the log-softmax and the recursion -- never the host-lengths setup kernels."""
     import _mrnnt_lib as L
     rng = np.random.default_rng(B)
     acts, labels, T, S = random_problem(rng, B, (5, 12), 4, 16)
@@ -264,4 +265,8 @@ def test_device_lengths_launch_count(op, dev, B):
     finally:
         L.profile_enable(False)
     assert prof["setup"][1] == (0 if B <= 64 else 1), prof
-    assert prof["log_softmax"][1] == 1 and prof["alpha_beta"][1] == 1 and prof["grad"][1] == 1
+    if B <= 64:
+        assert prof["chase"][1] == 1 and prof["log_softmax"][1] == 0 and prof["alpha_beta"][1] == 0, prof
+    else:
+        assert prof["chase"][1] == 0 and prof["log_softmax"][1] == 1 and prof["alpha_beta"][1] == 1, prof
+    assert prof["grad"][1] == 1, prof

@@ -26,7 +26,7 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture(scope="module")
 def jop():
     import monotonic_rnnt_joint
-    # sweeps through another launch variant (development build): MRNNT_FUZZ_TUNE="joint_nbuf=3,joint_reduce_sparse=2"
+    # sweeps through another launch variant (development build): MRNNT_FUZZ_TUNE="joint_bwd_mfma=32,joint_reduce_sparse=2"
     kv = dict(x.split("=") for x in filter(None, os.environ.get("MRNNT_FUZZ_TUNE", "").split(",")))
     if not kv:
         yield monotonic_rnnt_joint
@@ -237,34 +237,28 @@ def test_joint_alignment_restricted(jop, dev, k):
     close(db, db_r, name="d_bias")
 
 
-@pytest.mark.parametrize("H,V", [(512, 256), (256, 1000), (128, 64)])
-def test_joint_four_wave_workgroups_bit_identical(dev, H, V):
-    """joint_nw = 4 (development build): two 4-wave workgroups per CU instead of one of 8 -- the same tiles, chunk
-    order and epilogues per wave, so the same bits (d_bias aside: at H = 512 the gradient pass adds its column sums
-    with fp32 atomics, whose order is not fixed -- equal to ~1e-6 relative)."""
+@pytest.mark.parametrize("H,V", [(512, 256), (256, 1000), (128, 64), (384, 130), (640, 64)])
+def test_joint_gradients_bitwise_reproducible(dev, H, V):
+    """Two calls on the same inputs give the same bits in the costs and in every gradient: the
+    column sums of d_bias and the d_pred sums over frames are fixed-order reductions (per-workgroup partials, then
+    one ordered pass), not float atomics, as the reference's own op is deterministic."""
     import monotonic_rnnt_joint as jm
     enc, pred, w, bias, labels, T, S = make_case(7 + H, 5, (10, 60), 20, H, V)
     ref = run_joint(jm, dev, enc, pred, w, bias, labels, T, S)
-    with knobs(joint_nw=4):
+    for _ in range(2):
         got = run_joint(jm, dev, enc, pred, w, bias, labels, T, S)
-    assert np.array_equal(ref[0], got[0])
-    for a, b in zip(ref[1:4], got[1:4]):
-        assert torch.equal(a, b)
-    db_ref, db = ref[4].double().cpu(), got[4].double().cpu()
-    assert (db - db_ref).abs().max().item() <= 1e-6 * db_ref.abs().max().item() + 1e-7
+        assert np.array_equal(ref[0], got[0])
+        for a, b in zip(ref[1:], got[1:]):
+            assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("tile", ["joint_mfma=16", "joint_bwd_mfma=32", "joint_ring=4", "joint_ring=8", "joint_pipe=1", "joint_pipe=2", "joint_pipe=3",
-                                  "joint_fwd_opt=1", "joint_fwd_opt=2", "joint_fwd_opt=3", "joint_fwd_persist=1"])
+@pytest.mark.parametrize("tile", ["joint_bwd_mfma=32"])
 @pytest.mark.parametrize("H,V,blank", [(512, 1024, 517), (512, 1000, 0), (256, 17, 16), (128, 64, 37), (384, 130, 129),
                                        (256, 2, 1)])
 def test_joint_tile_variants_vs_host(dev, H, V, blank, tile):
-    """The launch variants of the development build against the host reference at this file's tolerances:
-    joint_mfma = 16 (the forward on the v_mfma_f32_16x16x32_bf16 tile: two rows per lane, four lane groups of disjoint
-    vocabulary merged at the end; the product's backward already runs that tile), joint_bwd_mfma = 32 (the backward
-    on the 32x32x16 tile), joint_ring = 4 / 8 (deeper A-fragment rings of the 32x32 tile; H = 256 / 512 only, others
-    run the default). Blank and labels in every lane group and vocabulary tile, tail chunks (V = 1000, 130, 17, 2),
-    ragged rows past the list end."""
+    """The launch variant of the development build against the host reference at this file's tolerances:
+    joint_bwd_mfma = 32 (the backward on the 32x32x16 tile, which H = 640 runs anyway). Blank and labels in every lane
+    group and vocabulary tile, tail chunks (V = 1000, 130, 17, 2), ragged rows past the list end."""
     import monotonic_rnnt_joint as jm
     enc, pred, w, bias, labels, T, S = make_case(31 + H + V, 4, (10, 50), 16, H, V)
     labels = np.where(labels == blank, (blank + 1) % V, labels).astype(np.int32)
@@ -280,24 +274,3 @@ def test_joint_tile_variants_vs_host(dev, H, V, blank, tile):
     close(db, db_r, name="d_bias")
     for b in range(len(T)):
         assert torch.all(de[b, T[b]:] == 0) and torch.all(dp[b, S[b] + 1:] == 0)
-
-
-@pytest.mark.parametrize("knob", ["joint_pipe=1", "joint_fwd_persist=1"])
-@pytest.mark.parametrize("H,V", [(512, 1024), (256, 100), (384, 32)])
-def test_joint_pipe_many_tiles_per_workgroup(dev, H, V, knob):
-    """joint_pipe = 1 with more 128-row tiles than CUs (each persistent workgroup walks several, building every next
-    tile's activations during the current one's MFMAs): costs and all gradients against the 8-wave forward within this
-    file's tolerances (blank / label logits come from dot products there, from the accumulators here)."""
-    import monotonic_rnnt_joint as jm
-    enc, pred, w, bias, labels, T, S = make_case(91 + H, 32, (150, 200), 60, H, V)
-    blank = V // 2
-    labels = np.where(labels == blank, (blank + 1) % V, labels).astype(np.int32)
-    ref = run_joint(jm, dev, enc, pred, w, bias, labels, T, S, blank=blank)
-    k, v = knob.split("=")
-    with knobs(**{k: int(v)}):
-        got = run_joint(jm, dev, enc, pred, w, bias, labels, T, S, blank=blank)
-    inband = sum(min(t, s) - max(0, t - (tt - s)) + 1 for tt, s in zip(T.tolist(), S.tolist()) for t in range(tt))
-    assert inband > 300 * 128, inband  # more 128-row tiles than the 256 workgroups
-    assert np.all(np.abs(got[0] - ref[0]) <= 1e-5 * np.maximum(1.0, np.abs(ref[0]))), (got[0], ref[0])
-    for a, b, name in zip(got[1:], ref[1:], ["d_enc", "d_pred", "d_weight", "d_bias"]):
-        close(a.cpu(), b.cpu().double(), name=name)
