@@ -740,7 +740,7 @@ namespace {
 struct JointPlan {
     Plan base;
     int64_t n_inband = 0;
-    size_t off_cnt = 0, off_lcol = 0, off_ls = 0, off_total = 0, total = 0;
+    size_t off_cnt = 0, off_lcol = 0, off_ls = 0, off_total = 0, off_dbias = 0, total = 0;
 };
 
 mrnnt_problem base_problem(const mrnnt_joint_problem *jp) {
@@ -800,6 +800,8 @@ RNNTStatus make_joint_plan(const mrnnt_joint_problem *jp, JointPlan *jl) {
     q.off_lcol = take(sizeof(int) * std::max<int64_t>(1, q.n_inband));
     q.off_ls = take(sizeof(int) * std::max<int64_t>(1, q.n_inband));
     q.off_total = take(sizeof(unsigned long long));
+    // the gradient pass's per-workgroup dbias column sums (fixed-order reduction), when there is a bias
+    q.off_dbias = (jp->bias && H <= 512) ? take(joint_dbias_part_bytes(std::max<int64_t>(1, q.n_inband), jp->V)) : 0;
     q.total = o;
     *jl = q;
     return RNNT_STATUS_SUCCESS;
@@ -925,8 +927,15 @@ RNNTStatus mrnnt_joint_backward(const mrnnt_joint_problem *jp, void *ws, int64_t
     j.scale = grad_scale;
     j.dbias = jp->dbias;
     if (jp->dbias && jp->H > 512) return fail(RNNT_STATUS_INVALID_VALUE, "dbias in the gradient pass needs H <= 512");
-    const hipError_t e = timed(K_JOINT_BWD, stream, [&] { return launch_joint_backward(d, j, stream); });
+    if (jp->dbias && !jl.off_dbias)
+        return fail(RNNT_STATUS_INVALID_VALUE, "dbias needs a bias (the workspace holds its partial sums only then)");
+    if (jp->dbias) j.dbias_part = reinterpret_cast<float *>(static_cast<char *>(ws) + jl.off_dbias);
+    hipError_t e = timed(K_JOINT_BWD, stream, [&] { return launch_joint_backward(d, j, stream); });
     if (e != hipSuccess) return fail_hip(e, "joint gradient kernel");
+    if (jp->dbias && n_live > 0) {
+        e = launch_joint_dbias_sum(j, jp->V, stream);
+        if (e != hipSuccess) return fail_hip(e, "joint dbias sum kernels");
+    }
     return RNNT_STATUS_SUCCESS;
 }
 

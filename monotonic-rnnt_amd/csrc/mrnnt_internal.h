@@ -94,6 +94,8 @@ struct JointArgs {
     int64_t *bs_idx;             // [n] b * pred_sb / H + s  (row of pred viewed as [B * S_slots, H])
     const float *scale;          // [B] upstream dL/dcost or nullptr
     float *dbias;                // [V] fp32: the backward adds sum_i G[i] into it (16x16x32 backward only), or nullptr
+    float *dbias_part;           // with dbias: the backward's per-workgroup column sums, then the segment sums
+                                 // (joint_dbias_part_bytes), summed in order by launch_joint_dbias_sum
 };
 
 // Row lists over the lattice: mode 0 = every in-band row, mode 1 = live rows (needs alpha/beta/ll).
@@ -104,6 +106,9 @@ hipError_t launch_joint_backward(const DevProblem &p, const JointArgs &j, hipStr
 hipError_t launch_joint_reduce(const DevProblem &p, const JointArgs &j, const int64_t *off, int T_max, int S_max,
                                const unsigned short *dH, float *d_enc, float *d_pred, hipStream_t stream);
 hipError_t launch_zero(void *ptr, size_t bytes, hipStream_t stream);
+// dbias: the fixed-order sum of the backward's per-workgroup column sums (scratch: joint_dbias_part_bytes)
+size_t joint_dbias_part_bytes(int64_t n_max, int V);
+hipError_t launch_joint_dbias_sum(const JointArgs &j, int V, hipStream_t stream);
 // LDS the fused joint kernels need at least (two weight-tile buffers + the bias row); at most 160 KiB per CU
 size_t joint_min_lds_bytes(int H, int V);
 
@@ -125,8 +130,9 @@ struct Tuning {
     int occ_skip = 1;             // gradient: no acts read for rows with log-occupancy < kDeadLogOcc
     int joint_bwd_mfma = 16;      // fused joint backward MFMA tile for H <= 512: 16 (v_mfma_f32_16x16x32_bf16) or 32
                                   // (32x32x16, development build); H = 640 always 32
-    int joint_reduce_sparse = 0;  // joint d_enc/d_pred reduce: 0 row-parallel kernel below 4 live rows per column,
-                                  // 1 always frame by frame, 2 always row-parallel
+    int joint_reduce_sparse = 0;  // joint d_enc/d_pred reduce: 0 / 1 frame by frame, one workgroup per utterance and
+                                  // hidden slice (fixed order, bitwise reproducible); 2 (development build) the
+                                  // row-parallel kernel with float atomics
     int dp_halo = 2;              // alpha/beta: halo recursion (one barrier per 8 steps, 8 / 16-step prefetch
                                   // blocks: 1 / 2) for S+1 <= 448; 0: one barrier per step
     int dp_lean = 1;              // halo recursion without an alignment: 1 -> the lean step (row pointers advanced

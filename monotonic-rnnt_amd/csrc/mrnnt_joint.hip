@@ -600,12 +600,22 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     }
     const int V = p.V, blank = p.blank;
     const float *bias = load_bias<KS, NB>(j, V, wsh);
-    // dbias: column sums of this workgroup's G in LDS behind the bias (launch_kt sizes the LDS for it)
+    // dbias: this workgroup's column sums of G in LDS behind the bias, in a fixed order (bitwise reproducible): per
+    // chunk, each wave's 32 column sums (a DPP row reduction over each lane group's 16 rows) go to its own slot, and
+    // after the next chunk's barrier wave 0 adds the NW slots in wave order; the workgroup's row of sums then goes to
+    // dbias_part[blockIdx.x] for the ordered sum over workgroups (dbias_sum_kernel). launch_kt sizes the LDS for it.
     const int vpad = (V + 31) / 32 * 32;
+    const int wave = threadIdx.x >> 6;
     float *dbl = const_cast<float *>(bias) + vpad;
-    if (j.dbias)
-        for (int v = threadIdx.x; v < vpad; v += blockDim.x) dbl[v] = 0.0f;
-    __syncthreads();
+    float *dpart = dbl + vpad;  // [2][NW][32]
+    auto fold_chunk = [&](int cc) {  // wave 0, lanes 0..31: chunk cc's column sums in wave order
+        if (wave == 0 && lane < 32) {
+            float t = 0.0f;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) t += dpart[((cc & 1) * NW + w) * 32 + lane];
+            dbl[32 * cc + lane] = t;
+        }
+    };
     bf16x8 bfr[2][K32];
     build_row<K32, 32, true>(j, q[0], 8 * g, i0, bfr[0]);
     build_row<K32, 32, true>(j, q[1], 8 * g, i0 + 16, bfr[1]);
@@ -618,6 +628,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     chunk_loop_with<KS, NB, NW>(
         j, V, wsh, leave ? 4 : -1, [&](const unsigned short *wb) { return WTile16<KS>::template mma<4>(wb, bfr, lane); },
         [&](const typename WTile16<KS>::Acc &acc, int c) {
+            if (j.dbias && c > 0) fold_chunk(c - 1);  // every wave's slots of chunk c - 1 are complete (barrier)
             const f4 bv[2] = {*reinterpret_cast<const f4 *>(bias + 32 * c + 4 * g),
                               *reinterpret_cast<const f4 *>(bias + 32 * c + 16 + 4 * g)};
             const int jb = blank - 32 * c;
@@ -655,8 +666,13 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
                     if (hb) grow[rt][blank] = IoBF16::from_f((gb - rc[rt].cb) * s);
                     if (mine) grow[rt][rc[rt].lab] = IoBF16::from_f((gl - rc[rt].ce) * s);
                     if (j.dbias) {  // the two corrected entries: the column sums above hold them uncorrected
-                        if (hb) atomicAdd(&dbl[blank], -rc[rt].cb * s);
-                        if (mine) atomicAdd(&dbl[rc[rt].lab], -rc[rt].ce * s);
+                        const int kb = hb ? pick8_index(jb) : -1, kl = mine ? pick8_index(jl & 31) : -1;
+                        const float db = rc[rt].cb * s, dl = rc[rt].ce * s;
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) {
+                            if (k == kb) cs[k] -= db;
+                            if (k == kl) cs[k] -= dl;
+                        }
                     }
                 }
             }
@@ -671,70 +687,100 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
                     cs[k] = v;
                 }
                 if (c16 == 15) {
+                    float *slot = dpart + ((c & 1) * NW + wave) * 32;
 #pragma unroll
-                    for (int k = 0; k < 8; ++k) atomicAdd(&dbl[32 * c + 16 * (k >> 2) + 4 * g + (k & 3)], cs[k]);
+                    for (int k = 0; k < 8; ++k) slot[16 * (k >> 2) + 4 * g + (k & 3)] = cs[k];
                 }
+                // the slots are in LDS before this wave reaches the next chunk's barrier (whose wait leaves LDS
+                // operations unwaited)
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             }
         });
     if (j.dbias) {
         __syncthreads();
-        for (int v = threadIdx.x; v < V; v += blockDim.x) {
-            const float t = dbl[v];
-            if (t != 0.0f) atomicAdd(&j.dbias[v], t);
-        }
+        fold_chunk((V + 31) / 32 - 1);
+        __syncthreads();
+        float *row = j.dbias_part + (int64_t)blockIdx.x * vpad;
+        for (int v = threadIdx.x; v < vpad; v += blockDim.x) row[v] = dbl[v];
     }
+}
+
+// dbias += the column sums of the backward's per-workgroup rows, in a fixed order: stage 1 sums segments of
+// kDbiasSeg rows (64 columns x 4 row lanes per workgroup, each lane its rows in order, the 4 lanes in order),
+// stage 2 the segments in order. Bitwise reproducible, unlike float atomics (cdna_hip_programming.md Guideline 12).
+constexpr int kDbiasSeg = 256;
+
+__global__ __launch_bounds__(256) void dbias_seg_kernel(const float *__restrict__ part, int64_t nrows, int vpad,
+                                                        float *__restrict__ seg_out) {
+    __shared__ float red[4][64];
+    const int col = blockIdx.x * 64 + (threadIdx.x & 63), rl = threadIdx.x >> 6;
+    const int64_t r0 = (int64_t)blockIdx.y * kDbiasSeg, r1 = min(r0 + kDbiasSeg, nrows);
+    float t = 0.0f;
+    if (col < vpad)
+        for (int64_t r = r0 + rl; r < r1; r += 4) t += part[r * vpad + col];
+    red[rl][threadIdx.x & 63] = t;
+    __syncthreads();
+    if (rl == 0 && col < vpad)
+        seg_out[(int64_t)blockIdx.y * vpad + col] = ((red[0][col & 63] + red[1][col & 63]) + red[2][col & 63]) +
+                                                    red[3][col & 63];
+}
+
+__global__ __launch_bounds__(256) void dbias_total_kernel(const float *__restrict__ seg, int nseg, int vpad, int V,
+                                                          float *__restrict__ dbias) {
+    const int v = blockIdx.x * 256 + threadIdx.x;
+    if (v >= V) return;
+    float t = 0.0f;
+    for (int k = 0; k < nseg; ++k) t += seg[(int64_t)k * vpad + v];
+    dbias[v] += t;
+}
+
+int64_t joint_bwd_blocks(int64_t n) { return (n + 255) / 256; }  // the backward's workgroups (8 waves x 32 rows)
+
+size_t joint_dbias_part_bytes(int64_t n_max, int V) {
+    const int64_t vpad = (V + 31) / 32 * 32, nb = joint_bwd_blocks(n_max);
+    return sizeof(float) * (size_t)vpad * (size_t)(nb + (nb + kDbiasSeg - 1) / kDbiasSeg);
+}
+
+hipError_t launch_joint_dbias_sum(const JointArgs &j, int V, hipStream_t stream) {
+    const int vpad = (V + 31) / 32 * 32;
+    const int64_t nb = joint_bwd_blocks(j.n);
+    if (nb <= 0) return hipSuccess;
+    const int64_t nseg = (nb + kDbiasSeg - 1) / kDbiasSeg;
+    if (nseg > 65535) return hipErrorInvalidValue;
+    float *seg = j.dbias_part + nb * vpad;
+    dbias_seg_kernel<<<dim3((vpad + 63) / 64, (unsigned)nseg), 256, 0, stream>>>(j.dbias_part, nb, vpad, seg);
+    dbias_total_kernel<<<(V + 255) / 256, 256, 0, stream>>>(seg, (int)nseg, vpad, V, j.dbias);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------------------------
 // backward tail: dpre = dH * (1 - Hact^2) over the live rows, summed into denc[b, t] (over s; written once per
-// column) and dpred[b, s] (over t; accumulated in LDS over a block of TT columns, then one fp32 atomic per
-// (s, h) per block). One workgroup per (utterance, block of TT frames, slice of HS hidden units); 4 hidden
-// units per thread (8-byte loads), 256/(HS/4) rows in flight.
-
-constexpr int kReduceTT = 64;
+// column) and dpred[b, s] (over t, accumulated in LDS). One workgroup per (utterance, slice of HS hidden units) walks
+// every frame of its utterance in order, so each sum has one fixed order and one writer: bitwise reproducible (no
+// float atomics). 4 hidden units per thread (8-byte loads), 256/(HS/4) rows in flight.
 
 template <int HS>
 __global__ __launch_bounds__(256) void joint_reduce_kernel(DevProblem p, JointArgs j, const int64_t *__restrict__ off,
                                                            const unsigned short *__restrict__ dH,
-                                                           float *__restrict__ d_enc, float *__restrict__ d_pred,
-                                                           int ntb) {
+                                                           float *__restrict__ d_enc, float *__restrict__ d_pred) {
     constexpr int TPR = HS / 4;     // threads per row slice
     constexpr int RP = 256 / TPR;   // rows in parallel
     extern __shared__ float lds[];  // acc[(S_b+1) * HS] then red[RP][HS]
     const int H = j.H;
     const int nh = H / HS;
-    // the h-slices of one block of frames are consecutive workgroups: they read the same rows (L2 reuse)
-    const int bx = blockIdx.x / nh;
+    // the h-slices of one utterance are consecutive workgroups: they read the same rows (L2 reuse)
+    const int b = blockIdx.x / nh;
     const int h0 = (blockIdx.x % nh) * HS;
-    const int b = bx / ntb;
-    const int t0 = (bx % ntb) * kReduceTT;
+    const int t0 = 0;
     const int T = p.T[b], S = p.S[b];
-    if (t0 >= T) return;
     const int tid = threadIdx.x;
     const int hl = (tid % TPR) * 4, rsub = tid / TPR;
     float *acc = lds;
     float *red = lds + (S + 1) * HS;
     const int64_t tslots = j.enc_sb / H, sslots = j.pred_sb / H;
-    const int t1 = min(t0 + kReduceTT, T);
-    // label positions this block of frames touches: rows of a column are listed by ascending s, so the first and
-    // last row of each column bound them (a few labels under an alignment restriction, the band otherwise); only
-    // that slice of the d_pred accumulator is cleared and flushed
-    __shared__ int srange[2];
-    if (tid == 0) {
-        srange[0] = S + 1;
-        srange[1] = -1;
-    }
-    __syncthreads();
-    if (tid < t1 - t0) {
-        const int64_t col = p.col_off[b] + t0 + tid;
-        const int64_t r0 = off[col], r1 = off[col + 1];
-        if (r1 > r0) {
-            atomicMin(&srange[0], j.ls[r0]);
-            atomicMax(&srange[1], j.ls[r1 - 1]);
-        }
-    }
-    __syncthreads();
-    const int s_lo = srange[0], s_hi = srange[1];
+    const int t1 = T;
+    // (the whole label range: the accumulator is flushed once per utterance)
+    const int s_lo = 0, s_hi = S;
     for (int i = s_lo * HS + tid; i < (s_hi + 1) * HS; i += 256) acc[i] = 0.0f;
     __syncthreads();
     for (int t = t0; t < t1; ++t) {
@@ -772,13 +818,13 @@ __global__ __launch_bounds__(256) void joint_reduce_kernel(DevProblem p, JointAr
         }
         __syncthreads();
     }
-    for (int i = s_lo * HS + tid; i < (s_hi + 1) * HS; i += 256) {
-        const float v = acc[i];
-        if (v != 0.0f) atomicAdd(&d_pred[((int64_t)b * sslots + i / HS) * H + h0 + i % HS], v);
-    }
+    for (int i = s_lo * HS + tid; i < (s_hi + 1) * HS; i += 256)  // this workgroup is the one writer
+        d_pred[((int64_t)b * sslots + i / HS) * H + h0 + i % HS] += acc[i];
 }
 
-// Sparse variant (few live rows per frame, e.g. alignment-restricted training): the rows of a block of frames are
+constexpr int kReduceTT = 64;  // frames per workgroup of the sparse variant
+
+// Sparse variant (development build, joint_reduce_sparse = 2; float atomics: not bitwise reproducible) (few live rows per frame, e.g. alignment-restricted training): the rows of a block of frames are
 // processed all at once (TPR threads per row) instead of frame by frame, so a workgroup does not wait one
 // dependent load chain per frame; d_enc and d_pred partials meet in LDS through ds_add_f32.
 template <int HS>
@@ -850,9 +896,8 @@ hipError_t launch_joint_reduce(const DevProblem &p, const JointArgs &j, const in
                                const unsigned short *dH, float *d_enc, float *d_pred, hipStream_t stream) {
     const int ntb = (T_max + kReduceTT - 1) / kReduceTT;
     const int W = S_max + 1;
-    // fewer than 4 live rows per lattice column on average: the row-parallel sparse kernel
-    const int mode = tuning().joint_reduce_sparse;
-    const bool sparse = mode == 0 ? j.n < 4 * p.num_cols : mode == 2;
+    // the row-parallel sparse kernel with float atomics: development A/B only (joint_reduce_sparse = 2)
+    const bool sparse = kVariants && tuning().joint_reduce_sparse == 2;
     auto go = [&](auto hs_tag) {
         constexpr int HS = decltype(hs_tag)::value;
         if (sparse) {
@@ -862,7 +907,7 @@ hipError_t launch_joint_reduce(const DevProblem &p, const JointArgs &j, const in
             return;
         }
         const size_t lds = sizeof(float) * ((size_t)W * HS + 256 / (HS / 4) * HS);
-        joint_reduce_kernel<HS><<<p.B * ntb * (j.H / HS), 256, lds, stream>>>(p, j, off, dH, d_enc, d_pred, ntb);
+        joint_reduce_kernel<HS><<<p.B * (j.H / HS), 256, lds, stream>>>(p, j, off, dH, d_enc, d_pred);
     };
     if ((int64_t)p.B * ntb * (j.H / 4) > (1ll << 24)) return hipErrorInvalidValue;  // 32-bit dispatch size
     // LDS = W * HS + 4 KiB of fp32: about 30 KiB at the headline (several workgroups per CU), <= 64 KiB always
@@ -897,8 +942,8 @@ static hipError_t launch_knw(const DevProblem &p, const JointArgs &j, size_t lds
 // and the label logit as a dot product.)
 template <int KS, int MF, bool BWD>
 static hipError_t launch_kt(const DevProblem &p, const JointArgs &j, hipStream_t stream) {
-    // the 16x16x32 backward keeps its dbias column sums behind the bias
-    const size_t bias = sizeof(float) * ((p.V + 31) / 32 * 32) * (MF == 16 && BWD ? 2 : 1);
+    // the 16x16x32 backward keeps its dbias column sums and the per-wave chunk slots behind the bias
+    const size_t bias = sizeof(float) * (((p.V + 31) / 32 * 32) * (MF == 16 && BWD ? 2 : 1) + (MF == 16 && BWD ? 512 : 0));
     if (j.dbias && !(MF == 16 && BWD)) return hipErrorInvalidValue;
     const size_t tile = sizeof(unsigned short) * WTile<KS>::ELEMS;
     if (2 * tile + bias <= 160 * 1024) return launch_knw<KS, 2, 8, MF, BWD, 2>(p, j, 2 * tile + bias, stream);
@@ -922,8 +967,9 @@ static hipError_t launch_kh(const DevProblem &p, const JointArgs &j, bool bwd, h
     return bwd ? launch_kb<KS, true>(p, j, stream) : launch_kb<KS, false>(p, j, stream);
 }
 
-size_t joint_min_lds_bytes(int H, int V) {  // the 16x16x32 backward (H <= 512) adds its dbias column sums
-    return 2 * sizeof(unsigned short) * 32 * (size_t)H + (H <= 512 ? 2 : 1) * sizeof(float) * (((size_t)V + 31) / 32 * 32);
+size_t joint_min_lds_bytes(int H, int V) {  // the 16x16x32 backward (H <= 512) adds its dbias column sums + slots
+    return 2 * sizeof(unsigned short) * 32 * (size_t)H +
+           sizeof(float) * ((H <= 512 ? 2 : 1) * (((size_t)V + 31) / 32 * 32) + (H <= 512 ? 512 : 0));
 }
 
 static hipError_t launch_joint(const DevProblem &p, const JointArgs &j, bool bwd, hipStream_t stream) {
