@@ -9,9 +9,14 @@
 // use row stride max(S) and the alignment row stride max(T), as the reference does (gpu_rnnt_kernel.h:133,
 // gpu_workspace_manager.h:200).
 //
+// The reference's public data members (:58-85) are here with the same names, types and meaning: device pointers into
+// the workspace, laid out in the reference's order (:228-254), holding the reference's view of the last computation
+// -- denom of every row, fp32 alpha / beta in the dense T*(S+1) per-utterance order with -inf outside the band,
+// ll_forward / ll_backward, the [B, T_max] band, var_start_offsets / denom_start_indices, B, V, S_max, T_max. The
+// library computes in its own layout (fp64 state) and writes this view after each cost() / cost_and_grad(), so a
+// client kernel that reads wm.ll_forward or wm.alphas after the call sees what the reference's would.
+//
 // Differences:
-//  * the workspace layout is private: the reference's public data members (workspace_, denom, alphas, betas,
-//    min_allowed_s, ...) are not exposed -- their contents are, through the getters below;
 //  * restrict_to_alignment() records the alignment, and the band is built on the device at compute time instead of
 //    a host loop with blocking copies (:191-219);
 //  * the getters read the state of the last cost() / cost_and_grad() on this workspace (betas / ll_backward only
@@ -82,6 +87,37 @@ class GpuRNNTWorkspaceManager<float> : public RNNTWorkspaceManager {
 
    private:
     mrnnt_gpu_ws_state *st_;
+
+   public:
+    // the reference's public data members (gpu_workspace_manager.h:58-85); set by set_workspace()
+    void *workspace_;  // device
+
+    const int B_h;  // host
+    const int V_h;  // host
+
+    const int *T;  // device
+    const int *S;  // device
+    int *B;        // device
+    int *V;        // device
+
+    const float *const acts;  // device
+    const int *const labels;  // device
+
+    float *denom;   // workspace
+    float *alphas;  // workspace
+    float *betas;   // workspace
+
+    int *min_allowed_s;  // workspace
+    int *max_allowed_s;  // workspace
+
+    int *denom_start_indices;  // workspace
+    int *var_start_offsets;    // workspace
+
+    int *S_max;  // workspace
+    int *T_max;  // workspace
+
+    float *ll_forward;   // workspace
+    float *ll_backward;  // workspace
 };
 
 #endif  // MONOTONIC_RNNT_GPU_WORKSPACE_MANAGER_H

@@ -1111,16 +1111,61 @@ mrnnt_problem problem_of(const mrnnt_gpu_ws_state *s, const std::vector<int> &T,
     return p;
 }
 
-// The manager's workspace = the flat plan + B device floats for the costs.
+// The reference manager's public view (gpu_workspace_manager.h:58-85, laid out in its order, :228-254, 301-346).
+struct RefView {
+    size_t denom, alphas, betas, dsi, vso, llf, llb, B, V, Smax, Tmax, mn, mx, total;
+};
+
+RefView ref_view_layout(int B, int64_t N, int T_max) {
+    RefView v;
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        const size_t at = o;
+        o += bytes;
+        return at;
+    };
+    v.denom = take(sizeof(float) * N);
+    v.alphas = take(sizeof(float) * N);
+    v.betas = take(sizeof(float) * N);
+    v.dsi = take(sizeof(int) * B);
+    v.vso = take(sizeof(int) * B);
+    v.llf = take(sizeof(float) * B);
+    v.llb = take(sizeof(float) * B);
+    v.B = take(sizeof(int));
+    v.V = take(sizeof(int));
+    v.Smax = take(sizeof(int));
+    v.Tmax = take(sizeof(int));
+    v.mn = take(sizeof(int) * (size_t)B * T_max);
+    v.mx = take(sizeof(int) * (size_t)B * T_max);
+    v.total = o;
+    return v;
+}
+
+// The manager's workspace = the flat plan + B device floats for the costs + the reference's view. The view's offset
+// is fixed by the larger of the plans with and without an alignment (restrict_to_alignment may come after
+// set_workspace); the costs follow the plan of the current call.
 RNNTStatus manager_size(const mrnnt_gpu_ws_state *s, const std::vector<int> &T, const std::vector<int> &S,
-                        size_t *bytes, size_t *costs_off) {
+                        size_t *bytes, size_t *costs_off, size_t *view_off = nullptr) {
     mrnnt_problem p = problem_of(s, T, S, 0);
     // size only depends on lengths and the alignment flag; blank range is checked at compute time
-    size_t b = 0;
-    const RNNTStatus st = mrnnt_workspace_size(&p, &b);
+    size_t b = 0, b_max = 0;
+    RNNTStatus st = mrnnt_workspace_size(&p, &b);
     if (st != RNNT_STATUS_SUCCESS) return st;
+    int dummy = 0;
+    p.alignment = p.alignment ? p.alignment : &dummy;
+    p.align_stride = T.empty() ? 0 : *std::max_element(T.begin(), T.end());
+    if ((st = mrnnt_workspace_size(&p, &b_max)) != RNNT_STATUS_SUCCESS) return st;
+    p.alignment = nullptr;
+    size_t b_plain = 0;
+    if ((st = mrnnt_workspace_size(&p, &b_plain)) != RNNT_STATUS_SUCCESS) return st;
+    b_max = std::max(b_max, b_plain);
     *costs_off = align_up(b);
-    *bytes = *costs_off + align_up(sizeof(float) * std::max(1, s->B));
+    const size_t voff = align_up(align_up(b_max) + sizeof(float) * std::max(1, s->B));
+    int64_t N = 0;
+    for (size_t i = 0; i < T.size(); ++i) N += (int64_t)T[i] * (S[i] + 1);
+    const int T_max = T.empty() ? 0 : *std::max_element(T.begin(), T.end());
+    *bytes = voff + ref_view_layout(s->B, N, T_max).total;
+    if (view_off) *view_off = voff;
     return RNNT_STATUS_SUCCESS;
 }
 
@@ -1159,6 +1204,21 @@ RNNTStatus manager_compute(GpuRNNTWorkspaceManager<float> &wm, int blank, hipStr
     s->with_beta = grads != nullptr;
     s->blank = blank;
     s->stream = stream;
+    // the reference's public members: the view of this computation (betas / ll_backward only with the gradient, as
+    // the reference's cost() skips the beta pass)
+    if (wm.denom) {
+        Plan pl;
+        if ((st = make_plan(&p, &pl)) != RNNT_STATUS_SUCCESS) return st;
+        const DevProblem d = make_dev(&p, pl, s->workspace);
+        if ((st = mrnnt_read_denoms(&p, s->workspace, wm.denom, stream)) != RNNT_STATUS_SUCCESS) return st;
+        hipError_t ev = launch_state_f32(d, wm.alphas, grads ? wm.betas : nullptr, wm.ll_forward,
+                                         grads ? wm.ll_backward : nullptr, stream);
+        if (ev != hipSuccess) return fail_hip(ev, "reference view kernel");
+        const int T_max = *std::max_element(T.begin(), T.end());
+        if ((st = mrnnt_read_band(&p, s->workspace, wm.min_allowed_s, wm.max_allowed_s, T_max, stream)) !=
+            RNNT_STATUS_SUCCESS)
+            return st;
+    }
     hipError_t e = hipMemcpyAsync(costs, costs_dev, sizeof(float) * s->B, hipMemcpyDeviceToHost, stream);
     if (e != hipSuccess) return fail(RNNT_STATUS_MEMOPS_FAILED, std::string("costs D2H: ") + hipGetErrorString(e));
     e = hipStreamSynchronize(stream);
@@ -1195,36 +1255,94 @@ std::vector<Out> read_back(const mrnnt_gpu_ws_state *s, size_t n, hipStream_t st
 
 }  // namespace
 
-GpuRNNTWorkspaceManager<float>::GpuRNNTWorkspaceManager(const float *const acts, const int *const labels, const int B,
-                                                        const int *T, const int *S, const int V)
-    : st_(new mrnnt_gpu_ws_state) {
-    st_->acts = acts;
-    st_->labels = labels;
-    st_->B = B;
-    st_->V = V;
-    st_->T_dev = T;
-    st_->S_dev = S;
+GpuRNNTWorkspaceManager<float>::GpuRNNTWorkspaceManager(const float *const acts_, const int *const labels_,
+                                                        const int B_, const int *T_, const int *S_, const int V_)
+    : st_(new mrnnt_gpu_ws_state),
+      workspace_(nullptr),
+      B_h(B_),
+      V_h(V_),
+      T(T_),
+      S(S_),
+      B(nullptr),
+      V(nullptr),
+      acts(acts_),
+      labels(labels_),
+      denom(nullptr),
+      alphas(nullptr),
+      betas(nullptr),
+      min_allowed_s(nullptr),
+      max_allowed_s(nullptr),
+      denom_start_indices(nullptr),
+      var_start_offsets(nullptr),
+      S_max(nullptr),
+      T_max(nullptr),
+      ll_forward(nullptr),
+      ll_backward(nullptr) {
+    st_->acts = acts_;
+    st_->labels = labels_;
+    st_->B = B_;
+    st_->V = V_;
+    st_->T_dev = T_;
+    st_->S_dev = S_;
 }
 
 GpuRNNTWorkspaceManager<float>::~GpuRNNTWorkspaceManager() { delete st_; }
 
 RNNTStatus GpuRNNTWorkspaceManager<float>::get_workspace_size(size_t *size_bytes) const {
     if (st_->B <= 0) return fail(RNNT_STATUS_INVALID_VALUE, "B must be > 0");
-    std::vector<int> T, S;
-    if (!host_lengths(st_, T, S)) return fail(RNNT_STATUS_MEMOPS_FAILED, "copying lengths to host");
+    std::vector<int> Th, Sh;
+    if (!host_lengths(st_, Th, Sh)) return fail(RNNT_STATUS_MEMOPS_FAILED, "copying lengths to host");
     size_t coff = 0;
-    // alignment may be registered later: size for the restricted layout so either works
-    mrnnt_gpu_ws_state tmp = *st_;
-    int dummy = 0;
-    tmp.alignment = &dummy;
-    return manager_size(&tmp, T, S, size_bytes, &coff);
+    // alignment may be registered later: manager_size sizes the view for either layout
+    return manager_size(st_, Th, Sh, size_bytes, &coff);
 }
 
+// (reference :256-329) the public members point into the workspace's view region; the constants and the default band
+// are uploaded with blocking copies, as the reference's cudaMemcpy calls do
 void GpuRNNTWorkspaceManager<float>::set_workspace(void *workspace) {
     if (st_->owned && st_->workspace && st_->workspace != workspace) (void)hipFree(st_->workspace);
     st_->workspace = workspace;
     st_->owned = false;
     st_->computed = false;
+    workspace_ = workspace;
+    denom = alphas = betas = ll_forward = ll_backward = nullptr;
+    B = V = S_max = T_max = min_allowed_s = max_allowed_s = denom_start_indices = var_start_offsets = nullptr;
+    std::vector<int> Th, Sh;
+    size_t bytes = 0, coff = 0, voff = 0;
+    if (!workspace || st_->B <= 0 || !host_lengths(st_, Th, Sh) ||
+        manager_size(st_, Th, Sh, &bytes, &coff, &voff) != RNNT_STATUS_SUCCESS)
+        return;
+    std::vector<int> off(st_->B);
+    int64_t N = 0;
+    for (int b = 0; b < st_->B; ++b) {
+        off[b] = (int)N;
+        N += (int64_t)Th[b] * (Sh[b] + 1);
+    }
+    const int Tm = *std::max_element(Th.begin(), Th.end()), Sm = *std::max_element(Sh.begin(), Sh.end());
+    const RefView v = ref_view_layout(st_->B, N, Tm);
+    char *base = static_cast<char *>(workspace) + voff;
+    denom = reinterpret_cast<float *>(base + v.denom);
+    alphas = reinterpret_cast<float *>(base + v.alphas);
+    betas = reinterpret_cast<float *>(base + v.betas);
+    denom_start_indices = reinterpret_cast<int *>(base + v.dsi);
+    var_start_offsets = reinterpret_cast<int *>(base + v.vso);
+    ll_forward = reinterpret_cast<float *>(base + v.llf);
+    ll_backward = reinterpret_cast<float *>(base + v.llb);
+    B = reinterpret_cast<int *>(base + v.B);
+    V = reinterpret_cast<int *>(base + v.V);
+    S_max = reinterpret_cast<int *>(base + v.Smax);
+    T_max = reinterpret_cast<int *>(base + v.Tmax);
+    min_allowed_s = reinterpret_cast<int *>(base + v.mn);
+    max_allowed_s = reinterpret_cast<int *>(base + v.mx);
+    std::vector<int> mn((size_t)st_->B * Tm, 0), mx((size_t)st_->B * Tm);
+    for (int b = 0; b < st_->B; ++b) std::fill_n(mx.begin() + (size_t)b * Tm, Tm, Sh[b]);
+    const int consts[4] = {st_->B, st_->V, Sm, Tm};
+    bool ok = hipMemcpy(denom_start_indices, off.data(), sizeof(int) * off.size(), hipMemcpyHostToDevice) == hipSuccess;
+    ok = ok && hipMemcpy(var_start_offsets, off.data(), sizeof(int) * off.size(), hipMemcpyHostToDevice) == hipSuccess;
+    ok = ok && hipMemcpy(B, consts, sizeof(consts), hipMemcpyHostToDevice) == hipSuccess;  // B, V, S_max, T_max
+    ok = ok && hipMemcpy(min_allowed_s, mn.data(), sizeof(int) * mn.size(), hipMemcpyHostToDevice) == hipSuccess;
+    ok = ok && hipMemcpy(max_allowed_s, mx.data(), sizeof(int) * mx.size(), hipMemcpyHostToDevice) == hipSuccess;
+    if (!ok) (void)fail(RNNT_STATUS_MEMOPS_FAILED, "set_workspace: uploading the reference view's constants");
 }
 
 RNNTStatus GpuRNNTWorkspaceManager<float>::create_workspace() {
@@ -1243,6 +1361,9 @@ void GpuRNNTWorkspaceManager<float>::free_workspace() {
     st_->workspace = nullptr;
     st_->owned = false;
     st_->computed = false;
+    workspace_ = nullptr;
+    denom = alphas = betas = ll_forward = ll_backward = nullptr;
+    B = V = S_max = T_max = min_allowed_s = max_allowed_s = denom_start_indices = var_start_offsets = nullptr;
 }
 
 void GpuRNNTWorkspaceManager<float>::restrict_to_alignment(const int *const alignments, int max_shift, int blank_idx) {

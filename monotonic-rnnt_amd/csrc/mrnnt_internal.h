@@ -212,6 +212,8 @@ hipError_t launch_align(const DevProblem &p, const int *alignment, int64_t align
 hipError_t launch_softmax(const DevProblem &p, int elem, int grid, hipStream_t stream);
 // mrnnt_read_state: alpha / beta cells outside the compute band set to -inf (either may be null)
 hipError_t launch_mask_state(const DevProblem &p, double *alpha, double *beta, hipStream_t stream);
+// the reference manager's view: fp32 alpha / beta (band-masked) and log-likelihoods (any may be null)
+hipError_t launch_state_f32(const DevProblem &p, float *alpha, float *beta, float *ll, float *llb, hipStream_t stream);
 hipError_t launch_dp(const DevProblem &p, int S_max, int with_beta, float *costs, hipStream_t stream);
 
 // The chase launch (mrnnt_chase.hip): log-softmax and alpha / beta recursion in one launch, the recursion consuming

@@ -139,6 +139,40 @@ __global__ __launch_bounds__(64) void mask_state_kernel(DevProblem p, double *__
     }
 }
 
+// The reference manager's view (GpuRNNTWorkspaceManager public members): fp32 alpha / beta, -inf outside the band as
+// mask_state_kernel, and the log-likelihoods (any output may be null)
+__global__ __launch_bounds__(64) void state_f32_kernel(DevProblem p, float *__restrict__ alpha, float *__restrict__ beta,
+                                                       float *__restrict__ ll, float *__restrict__ llb) {
+    resolve_dyn(p);
+    if (blockIdx.x == 0)
+        for (int b = threadIdx.x; b < p.B; b += 64) {
+            if (ll) ll[b] = (float)p.ll[b];
+            if (llb) llb[b] = (float)p.llb[b];
+        }
+    for (int64_t c = blockIdx.x; c < p.num_cols; c += gridDim.x) {
+        const int b = p.col_b[c];
+        const int T = p.T[b], S = p.S[b];
+        const int t = (int)(c - p.col_off[b]);
+        const int64_t rowc = p.row_off[b] + (int64_t)t * (S + 1);
+        for (int s = threadIdx.x; s <= S; s += 64) {
+            if (alpha) {
+                const bool ain = !(s > min(t + 1, S) || s < t - (T - 1 - S));
+                alpha[rowc + s] = ain ? (float)p.alpha[rowc + s] : -__builtin_huge_valf();
+            }
+            if (beta) {
+                const bool bin = t == 0 ? s == 0 : (s <= t && s >= t - (T - S));
+                beta[rowc + s] = bin ? (float)p.beta[rowc + s] : -__builtin_huge_valf();
+            }
+        }
+    }
+}
+
+hipError_t launch_state_f32(const DevProblem &p, float *alpha, float *beta, float *ll, float *llb, hipStream_t stream) {
+    const int grid = (int)(p.num_cols < (1 << 16) ? p.num_cols : (1 << 16));
+    state_f32_kernel<<<grid > 0 ? grid : 1, 64, 0, stream>>>(p, alpha, beta, ll, llb);
+    return hipGetLastError();
+}
+
 hipError_t launch_mask_state(const DevProblem &p, double *alpha, double *beta, hipStream_t stream) {
     const int grid = (int)(p.num_cols < (1 << 16) ? p.num_cols : (1 << 16));
     mask_state_kernel<<<grid > 0 ? grid : 1, 64, 0, stream>>>(p, alpha, beta);

@@ -2,8 +2,10 @@
 // against libmonotonic_rnnt_amd.so: it drives GpuRNNTWorkspaceManager<float> + GpuRNNTComputer<float> the way the
 // reference's pytorch_binding/monotonic_rnnt.cu:81-152 does, then reads the workspace back through every public
 // host getter of the reference's manager (gpu_workspace_manager.h:87-190), as the reference's own computer and debug
-// paths call them (gpu_rnnt.h:28-35,53-54,118-119,133,166,180). tests/test_ref_client.py compares the read-backs
-// with the golden denom_f64 / alpha_f64 / beta_f64 of the reference itself.
+// paths call them (gpu_rnnt.h:28-35,53-54,118-119,133,166,180), and reads the manager's public data members (:58-85)
+// the way the reference's own computer reads wm.ll_forward / wm.denom on the device (gpu_rnnt.h:105-229), checking
+// them against the getters. tests/test_ref_client.py compares the read-backs with the golden denom_f64 / alpha_f64 /
+// beta_f64 of the reference itself.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -28,6 +30,43 @@ static int put(const std::vector<T> &v, T *out, size_t expect) {
     if (v.size() != expect) return 1;
     std::copy(v.begin(), v.end(), out);
     return 0;
+}
+
+template <typename T>
+static std::vector<T> from_gpu(const T *d, size_t n) {
+    std::vector<T> h(n);
+    if (!d || (n && hipMemcpy(h.data(), d, n * sizeof(T), hipMemcpyDeviceToHost) != hipSuccess)) return {};
+    return h;
+}
+
+template <typename T>
+static int same(const std::vector<T> &a, const std::vector<T> &b) {
+    return a.size() != b.size() || std::memcmp(a.data(), b.data(), a.size() * sizeof(T)) != 0;
+}
+
+static int check_members(GpuRNNTWorkspaceManager<float> &wm, int B, int V, size_t N, int T_max, bool grads) {
+    int bad = 0;
+    bad += wm.workspace_ == nullptr || wm.B_h != B || wm.V_h != V || wm.acts == nullptr || wm.labels == nullptr;
+    bad += same(from_gpu(wm.denom, N), wm.denom_host());
+    bad += same(from_gpu(wm.alphas, N), wm.alphas_host());
+    bad += same(from_gpu(wm.ll_forward, (size_t)B), wm.ll_forward_host());
+    if (grads) {
+        bad += same(from_gpu(wm.betas, N), wm.betas_host());
+        bad += same(from_gpu(wm.ll_backward, (size_t)B), wm.ll_backward_host());
+    }
+    bad += same(from_gpu(wm.min_allowed_s, (size_t)B * T_max), wm.min_allowed_s_host());
+    bad += same(from_gpu(wm.max_allowed_s, (size_t)B * T_max), wm.max_allowed_s_host());
+    bad += same(from_gpu(wm.var_start_offsets, (size_t)B), wm.var_start_offsets_host());
+    bad += same(from_gpu(wm.denom_start_indices, (size_t)B), wm.var_start_offsets_host());
+    const std::vector<int> c = {B, V, wm.S_max_host(), T_max};
+    auto one = [](const int *d) {
+        const std::vector<int> h = from_gpu(d, 1);
+        return h.empty() ? -1 : h[0];
+    };
+    const std::vector<int> got = {one(wm.B), one(wm.V), one(wm.S_max), one(wm.T_max)};
+    bad += c != got;
+    bad += same(from_gpu(wm.T, (size_t)B), wm.T_host()) + same(from_gpu(wm.S, (size_t)B), wm.S_host());
+    return bad;
 }
 
 extern "C" {
@@ -82,6 +121,9 @@ int client_gpu_getters(const float *acts, const int *labels, int B, const int *T
             sizes[3] = wm.T_max_host();
         }
         bad += wm.B_host() != B || wm.V_host() != V;
+        // the reference's public data members (gpu_workspace_manager.h:58-85): device pointers a client kernel
+        // reads after the call -- the same values as the getters, in the same layout
+        bad += check_members(wm, B, V, (size_t)N, T_max, grads != nullptr);
         const std::vector<int> Th = wm.T_host(), Sh = wm.S_host();
         bad += !std::equal(Th.begin(), Th.end(), T) || !std::equal(Sh.begin(), Sh.end(), S);
         wm.free_workspace();
