@@ -20,8 +20,11 @@ it (storage use count 1: the caller dropped the previous gradient), the module d
 allocator then honours every stream the caller recorded on it (Tensor.record_stream: the block is not reusable
 until those streams pass their events) -- and immediately asks the allocator for the same size on the current
 stream. When the block is ready the allocator's best fit returns that very block (a "hit": the fast placement is
-kept); when a side stream still uses it, or the stream differs, it returns another block, which becomes the kept
-one (a "miss", counted). A gradient the caller still holds is never reused (plain allocation). Under HIP-graph
+kept); when a side stream still uses it, or the stream differs, it returns another block (a "miss", counted): that
+block is handed out as a plain allocation -- not kept, so the caching allocator gets it back when the caller drops
+the gradient, and the module never holds a second block of that size -- and the next call tries to take the fast
+block back again (after two misses in a row it gives up on it and chooses afresh). A gradient the caller still
+holds is never reused (plain allocation). Under HIP-graph
 capture the graph's memory pool serves gradients as usual. MRNNT_GRADS_PLACEMENT=0 turns this off (plain
 torch.empty_like), and so does a torch without the storage use count; release() drops the kept buffers.
 """
@@ -50,10 +53,13 @@ def enabled() -> bool:
 
 
 class _Kept:
-    __slots__ = ("storage", "ptr", "nbytes", "gbps")
+    """The kept block (storage held), or -- after a missed take-back -- only its record (storage None): the block sits
+    in the caching allocator until the streams recorded on it pass, and the next call asks for it again."""
+    __slots__ = ("storage", "ptr", "nbytes", "gbps", "misses")
 
-    def __init__(self, storage, nbytes: int, gbps: Optional[float]):
-        self.storage, self.ptr, self.nbytes, self.gbps = storage, storage.data_ptr(), nbytes, gbps
+    def __init__(self, storage, nbytes: int, gbps: Optional[float], ptr: Optional[int] = None, misses: int = 0):
+        self.storage, self.nbytes, self.gbps, self.misses = storage, nbytes, gbps, misses
+        self.ptr = storage.data_ptr() if storage is not None else ptr
 
 
 def _fill_gbps(buf: torch.Tensor) -> float:
@@ -111,33 +117,43 @@ class GradsArena:
         key = (acts.device, acts.dtype)
         with self._lock:
             kept = self._kept.get(key)
-            if kept is not None and _use_count(kept.storage._cdata) > self._held:
+            if kept is not None and kept.storage is not None and _use_count(kept.storage._cdata) > self._held:
                 self.stats["held_by_caller"] += 1
                 return torch.empty_like(acts, memory_format=torch.contiguous_format)  # still held by the caller
+            storage = None
             if kept is not None and kept.nbytes >= nbytes:
-                ptr, kb, gbps = kept.ptr, kept.nbytes, kept.gbps
-                del self._kept[key]
-                kept = None  # the last reference: the caching allocator owns the block, with the caller's streams
-                if self._on_release:
-                    self._on_release(ptr)
-                kept = self._kept[key] = self._take_back(ptr, kb, gbps, acts.device)
+                ptr, kb, gbps, misses = kept.ptr, kept.nbytes, kept.gbps, kept.misses
+                if kept.storage is not None:
+                    # the last reference: the caching allocator owns the block, with the caller's streams
+                    self._kept[key] = _Kept(None, kb, gbps, ptr, misses)
+                    kept = None
+                    if self._on_release:
+                        self._on_release(ptr)
+                buf = self._alloc(kb, acts.device)
+                if buf.data_ptr() == ptr:
+                    self.stats["reuse_hits"] += 1
+                    storage = buf.untyped_storage()
+                    self._kept[key] = _Kept(storage, kb, gbps)
+                else:
+                    # still in use on another stream (or another stream's pool): hand the other block out plainly
+                    self.stats["reuse_misses"] += 1
+                    storage = buf.untyped_storage()
+                    if misses + 1 >= 2:
+                        del self._kept[key]  # the fast block is gone for good: choose afresh next time
+                    else:
+                        self._kept[key] = _Kept(None, kb, gbps, ptr, misses + 1)
+                    self.stats["handed_out"] += 1
+                    out = torch.empty(0, dtype=acts.dtype, device=acts.device)
+                    return out.set_(storage, 0, acts.shape, _contiguous_strides(acts.shape))
             else:
                 if kept is not None:
                     del self._kept[key]
                     kept = None  # the old block goes back to the caching allocator before the new one is chosen
                 kept = self._kept[key] = self._choose(nbytes, acts.device)
+                storage = kept.storage
             self.stats["handed_out"] += 1
             out = torch.empty(0, dtype=acts.dtype, device=acts.device)
-            return out.set_(kept.storage, 0, acts.shape, _contiguous_strides(acts.shape))
-
-    def _take_back(self, ptr: int, nbytes: int, gbps: Optional[float], dev: torch.device) -> _Kept:
-        """After the kept block went back to the caching allocator: take the same size again (see the module doc)."""
-        buf = self._alloc(nbytes, dev)
-        if buf.data_ptr() == ptr:
-            self.stats["reuse_hits"] += 1
-            return _Kept(buf.untyped_storage(), nbytes, gbps)
-        self.stats["reuse_misses"] += 1  # still in use on another stream (or another stream's pool): a new block
-        return _Kept(buf.untyped_storage(), nbytes, None)
+            return out.set_(storage, 0, acts.shape, _contiguous_strides(acts.shape))
 
     def _choose(self, nbytes: int, dev: torch.device) -> _Kept:
         cands: List[Tuple[float, torch.Tensor]] = []

@@ -149,8 +149,9 @@ def test_views_have_contiguous_strides(shape):
 
 def test_reuse_goes_back_through_the_allocator():
     """A reused gradient is the kept block handed back by the allocator (a hit); a block another stream still uses
-    (Tensor.record_stream: the device allocator holds it until that stream passes its event) is not handed back,
-    and the arena takes and keeps the block the allocator gives instead (a miss) -- never the busy one."""
+    (Tensor.record_stream: the device allocator holds it until that stream passes its event) is not handed back:
+    the block the allocator gives instead is handed out plainly, NOT kept (the module never holds a
+    second block of that size), and the next call takes the fast block back once it is free."""
     f = Fake([7000.0])
     ar = f.arena()
     a = acts()
@@ -164,10 +165,30 @@ def test_reuse_goes_back_through_the_allocator():
     g3 = ar.like(a)
     q = g3.data_ptr()
     assert q != p and ar.stats["reuse_misses"] == 1
+    assert all(k.storage is None for k in ar._kept.values())  # the arena holds neither block now
+    f.on_release(q)  # the caller drops the plain gradient: back to the allocator
     del g3
     f.busy.clear()
-    assert ar.like(a).data_ptr() in (p, q)  # either free block of the size, as the allocator's best fit picks
+    assert ar.like(a).data_ptr() == p and ar.stats["reuse_hits"] == 2  # the fast block again
     assert len(ar.log) == 1  # no new probe: placement decisions only at the first choice
+
+
+def test_two_misses_in_a_row_rechoose():
+    f = Fake([7000.0, 6900.0])
+    ar = f.arena()
+    a = acts()
+    g = ar.like(a)
+    p = g.data_ptr()
+    f.busy.add(p)
+    del g
+    for _ in range(2):  # the fast block stays busy: two plain hand-outs
+        h = ar.like(a)
+        assert h.data_ptr() != p
+        f.on_release(h.data_ptr())
+        del h
+    assert not ar._kept  # given up on
+    ar.like(a)
+    assert len(ar.log) == 2  # chosen afresh
 
 
 def test_no_use_count_means_plain(monkeypatch):
