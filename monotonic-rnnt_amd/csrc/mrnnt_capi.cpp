@@ -796,7 +796,8 @@ RNNTStatus make_joint_plan(const mrnnt_joint_problem *jp, JointPlan *jl) {
         o = align_up(o + bytes);
         return at;
     };
-    q.off_cnt = take(sizeof(int64_t) * (q.base.cols + 1));
+    // per-column counts + their exclusive scan, and the scan's tile sums (launch_row_list)
+    q.off_cnt = take(sizeof(int64_t) * (q.base.cols + 2 + (q.base.cols + 1023) / 1024));
     q.off_lcol = take(sizeof(int) * std::max<int64_t>(1, q.n_inband));
     q.off_ls = take(sizeof(int) * std::max<int64_t>(1, q.n_inband));
     q.off_total = take(sizeof(unsigned long long));

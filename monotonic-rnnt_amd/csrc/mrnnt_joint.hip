@@ -98,32 +98,52 @@ __global__ __launch_bounds__(256) void row_list_kernel(DevProblem p, int mode, i
         row_list_column<WRITE>(p, mode, cnt, lcol, ls, col, lane);
 }
 
-// exclusive scan of a[0..n) in place, a[n] = total (one workgroup; n = lattice columns)
-__global__ __launch_bounds__(1024) void scan_kernel(int64_t *__restrict__ a, int64_t n,
-                                                    unsigned long long *__restrict__ total) {
-    __shared__ int64_t part[1024];
-    const int tid = threadIdx.x;
-    const int64_t seg = (n + 1023) / 1024;
-    const int64_t lo = min(n, tid * seg), hi = min(n, lo + seg);
-    int64_t loc = 0;
-    for (int64_t i = lo; i < hi; ++i) loc += a[i];
-    part[tid] = loc;
+// exclusive scan of a[0..n) in place, a[n] = total (n = lattice columns), in two launches over tiles of 1024: the
+// tile sums (one workgroup per tile), then every workgroup adds the sums of the tiles before its own (<= a few
+// hundred, one wave) and scans its tile through LDS. (A single workgroup walking all columns took ~130 us per list
+// at the headline's 64,000 columns.)
+constexpr int kScanTile = 1024;
+
+__device__ __forceinline__ int64_t block_incl_scan1024(int64_t v, int64_t *wsum) {  // 1024 threads
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    v = wave_incl_scan64(v);
+    if (lane == 63) wsum[wave] = v;
     __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
-        const int64_t v = tid >= off ? part[tid - off] : 0;
-        __syncthreads();
-        part[tid] += v;
-        __syncthreads();
+    if (wave == 0) {
+        int64_t w = lane < 16 ? wsum[lane] : 0;
+        w = wave_incl_scan64(w);
+        if (lane < 16) wsum[lane] = w;
     }
-    int64_t run = part[tid] - loc;
-    for (int64_t i = lo; i < hi; ++i) {
-        const int64_t v = a[i];
-        a[i] = run;
-        run += v;
+    __syncthreads();
+    return v + (wave > 0 ? wsum[wave - 1] : 0);
+}
+
+__global__ __launch_bounds__(1024) void scan_tiles_kernel(const int64_t *__restrict__ a, int64_t n,
+                                                          int64_t *__restrict__ tile_sum) {
+    __shared__ int64_t wsum[16];
+    const int64_t i = (int64_t)blockIdx.x * kScanTile + threadIdx.x;
+    const int64_t v = block_incl_scan1024(i < n ? a[i] : 0, wsum);
+    if (threadIdx.x == kScanTile - 1) tile_sum[blockIdx.x] = v;
+}
+
+__global__ __launch_bounds__(1024) void scan_apply_kernel(int64_t *__restrict__ a, int64_t n,
+                                                          const int64_t *__restrict__ tile_sum,
+                                                          unsigned long long *__restrict__ total) {
+    __shared__ int64_t wsum[16];
+    __shared__ int64_t base;
+    if (threadIdx.x < 64) {  // the tiles before this one, in order
+        int64_t s = 0;
+        for (int k = threadIdx.x; k < (int)blockIdx.x; k += 64) s += tile_sum[k];
+        s = wave_incl_scan64(s);
+        if (threadIdx.x == 63) base = s;
     }
-    if (tid == 1023) {
-        a[n] = part[1023];
-        if (total) *total = (unsigned long long)part[1023];
+    const int64_t i = (int64_t)blockIdx.x * kScanTile + threadIdx.x;
+    const int64_t x = i < n ? a[i] : 0;
+    const int64_t incl = block_incl_scan1024(x, wsum);  // (its barriers also publish `base`)
+    if (i < n) a[i] = base + incl - x;
+    if (i == n - 1 || (n == 0 && i == 0)) {
+        a[n] = base + incl;
+        if (total) *total = (unsigned long long)(base + incl);
     }
 }
 
@@ -133,7 +153,13 @@ hipError_t launch_row_list(const DevProblem &p, int mode, int64_t *col_cnt, int 
     row_list_kernel<false><<<(int)blocks, 256, 0, stream>>>(p, mode, col_cnt, lcol, ls);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    scan_kernel<<<1, 1024, 0, stream>>>(col_cnt, p.num_cols, total);
+    // the tile sums live past the counts (the workspace sizes col_cnt for it: joint_scan_scratch)
+    const int64_t tiles = std::max<int64_t>(1, (p.num_cols + kScanTile - 1) / kScanTile);
+    if (tiles > (1 << 20)) return hipErrorInvalidValue;
+    int64_t *tile_sum = col_cnt + p.num_cols + 1;
+    scan_tiles_kernel<<<(unsigned)tiles, 1024, 0, stream>>>(col_cnt, p.num_cols, tile_sum);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    scan_apply_kernel<<<(unsigned)tiles, 1024, 0, stream>>>(col_cnt, p.num_cols, tile_sum, total);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     row_list_kernel<true><<<(int)blocks, 256, 0, stream>>>(p, mode, col_cnt, lcol, ls);
     return hipGetLastError();

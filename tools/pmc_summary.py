@@ -50,6 +50,15 @@ def counters(d, counter):
     return per
 
 
+def lib_sha256():
+    import hashlib
+    h = hashlib.sha256()
+    with open(os.path.join(ROOT, "monotonic-rnnt_amd", "libmonotonic_rnnt_amd.so"), "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--stats", required=True)
@@ -110,6 +119,8 @@ def main():
         "bench_hip_event_avg_ms": {"grad": bench["kernels"]["grad"]["avg_ms"],
                                    "log_softmax": bench["kernels"]["log_softmax"]["avg_ms"]},
         "correction": "FETCH_SIZE(KiB)*1024*2 (gfx950 half-count of 16-B/lane streaming reads) + WRITE_SIZE(KiB)*1024",
+        # the library build the counters were measured on: bench.py uses this record only for that very build
+        "lib_sha256": lib_sha256(),
         "source": f"profiles/{a.tag}/pmc_per_launch{sfx}.json (rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, "
                   f"python3 bench.py --config {a.config} --acts-dtype {a.dtype} --steps 3 --warmup 1 --no-cpu)",
     }
