@@ -447,6 +447,7 @@ def run(args, world):
     g_ms, g_n = tot_ms("grad")
     s_ms, s_n = tot_ms("log_softmax")
     d_ms, d_n = tot_ms("alpha_beta")
+    c_ms, c_n = tot_ms("chase")
     # the bytes of all gradient launches of the timed steps over their summed duration
     achieved = grad_bytes * prof_steps / (g_ms * 1e-3) / 1e9 if g_ms else None
     g_avg = g_ms / g_n if g_ms else None
@@ -522,6 +523,8 @@ def run(args, world):
                                                                  acts_read_gbps, 4)
                                 if s_ms and acts_read_gbps else None},
                 "alpha_beta": {"avg_ms": round(d_ms / d_n, 4) if d_ms else None},
+                "chase": {"avg_ms": round(c_ms / c_n, 4) if c_ms else None,
+                          "note": "log-softmax + alpha/beta in one launch (mrnnt_chase.hip), where it pays"},
                 "grad": {"avg_ms": round(g_avg, 4) if g_avg else None, "gbps": round(achieved, 1) if achieved else None},
             },
             "cpu_baseline": cpu,

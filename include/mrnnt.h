@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MRNNT_VERSION 8
+#define MRNNT_VERSION 9
 
 /* acts / grads element types */
 #define MRNNT_F32 0
@@ -202,7 +202,12 @@ typedef struct mrnnt_joint_problem {
                                 mrnnt_joint_backward write columns H .. hact_ld-1 of every row as [1, 0, ...],
                                 so that the dweight GEMM G^T Hact also yields dbias = sum_i G[i] in column H */
     float *dbias;            /* (version 8) device fp32 [V] or NULL: mrnnt_joint_backward ADDS sum_i G[i] (the fp32
-                                values before their bf16 rounding) into it -- zero it first; H <= 512 only */
+                                values before their bf16 rounding) into it -- zero it first; H <= 512 only, and V small
+                                enough for its per-wave LDS column sums (mrnnt_joint_backward reports otherwise). Summed
+                                in a fixed order: bitwise reproducible (version 9; version 8 used float atomics) */
+    void *reduce_scratch;    /* (version 9) device memory for mrnnt_joint_reduce, >= mrnnt_joint_reduce_scratch_bytes,
+                                or NULL (a slower one-block-per-utterance form runs); e.g. G once dH = G weight exists */
+    size_t reduce_scratch_bytes;
 } mrnnt_joint_problem;
 
 RNNTStatus mrnnt_joint_workspace_size(const mrnnt_joint_problem *p, size_t *bytes);
@@ -228,9 +233,14 @@ RNNTStatus mrnnt_joint_backward(const mrnnt_joint_problem *p, void *workspace, i
 
 /* After mrnnt_joint_backward, with dH = G weight (bf16 [n_live, H], e.g. a library GEMM): accumulate
  * dpre = dH * (1 - Hact^2) into d_enc (fp32, enc's [B, enc_stride/H, H] shape; rows (b, t < T_b) are
- * overwritten) and d_pred (fp32, pred's shape; added to: zero it first). Zero d_enc's padding rows yourself. */
+ * overwritten) and d_pred (fp32, pred's shape; added to: zero it first). Zero d_enc's padding rows yourself.
+ * Every sum has a fixed order (bitwise reproducible). p->reduce_scratch (version 9) lets it run on blocks of frames
+ * whose d_pred sums are then added in block order; see mrnnt_joint_reduce_scratch_bytes. */
 RNNTStatus mrnnt_joint_reduce(const mrnnt_joint_problem *p, void *workspace, int64_t n_live, const void *dH,
                               const void *Hact, float *d_enc, float *d_pred, hipStream_t stream);
+
+/* (version 9) Bytes of p->reduce_scratch for the blocked form of mrnnt_joint_reduce. */
+RNNTStatus mrnnt_joint_reduce_scratch_bytes(const mrnnt_joint_problem *p, size_t *bytes);
 
 /* Nontemporal zero fill of `bytes` (a multiple of 16) at `dst` (16-byte aligned device memory), in the gradient
  * pass's store pattern. The Python surface times it once over a newly allocated large grads buffer to pick a

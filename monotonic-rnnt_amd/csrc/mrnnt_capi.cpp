@@ -928,6 +928,9 @@ RNNTStatus mrnnt_joint_backward(const mrnnt_joint_problem *jp, void *ws, int64_t
     j.scale = grad_scale;
     j.dbias = jp->dbias;
     if (jp->dbias && jp->H > 512) return fail(RNNT_STATUS_INVALID_VALUE, "dbias in the gradient pass needs H <= 512");
+    if (jp->dbias && joint_dbias_lds_bytes(jp->H, jp->V) > 160 * 1024)
+        return fail(RNNT_STATUS_INVALID_VALUE, "dbias in the gradient pass: V too large for its LDS column sums at this H "
+                                               "(sum G's columns outside: dbias = NULL)");
     if (jp->dbias && !jl.off_dbias)
         return fail(RNNT_STATUS_INVALID_VALUE, "dbias needs a bias (the workspace holds its partial sums only then)");
     if (jp->dbias) j.dbias_part = reinterpret_cast<float *>(static_cast<char *>(ws) + jl.off_dbias);
@@ -957,9 +960,18 @@ RNNTStatus mrnnt_joint_reduce(const mrnnt_joint_problem *jp, void *ws, int64_t n
     const int64_t *off = reinterpret_cast<const int64_t *>(static_cast<char *>(ws) + jl.off_cnt);
     const hipError_t e = timed(K_JOINT_RED, stream, [&] {
         return launch_joint_reduce(d, j, off, jl.base.T_max, jl.base.S_max, static_cast<const unsigned short *>(dH),
-                                   d_enc, d_pred, stream);
+                                   d_enc, d_pred, jp->reduce_scratch, jp->reduce_scratch_bytes, stream);
     });
     if (e != hipSuccess) return fail_hip(e, "joint reduce kernel");
+    return RNNT_STATUS_SUCCESS;
+}
+
+RNNTStatus mrnnt_joint_reduce_scratch_bytes(const mrnnt_joint_problem *jp, size_t *bytes) {
+    if (!bytes) return fail(RNNT_STATUS_INVALID_VALUE, "null size pointer");
+    JointPlan jl;
+    const RNNTStatus st = make_joint_plan(jp, &jl);
+    if (st != RNNT_STATUS_SUCCESS) return st;
+    *bytes = joint_reduce_scratch_bytes(jl.base.B, jl.base.T_max, jl.base.S_max, jp->H);
     return RNNT_STATUS_SUCCESS;
 }
 

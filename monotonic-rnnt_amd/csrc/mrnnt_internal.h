@@ -104,13 +104,18 @@ hipError_t launch_row_list(const DevProblem &p, int mode, int64_t *col_cnt, int 
 hipError_t launch_joint_forward(const DevProblem &p, const JointArgs &j, hipStream_t stream);
 hipError_t launch_joint_backward(const DevProblem &p, const JointArgs &j, hipStream_t stream);
 hipError_t launch_joint_reduce(const DevProblem &p, const JointArgs &j, const int64_t *off, int T_max, int S_max,
-                               const unsigned short *dH, float *d_enc, float *d_pred, hipStream_t stream);
+                               const unsigned short *dH, float *d_enc, float *d_pred, void *scratch,
+                               size_t scratch_bytes, hipStream_t stream);
+// scratch of the blocked d_enc / d_pred reduce (per-block d_pred sums and label ranges)
+size_t joint_reduce_scratch_bytes(int B, int T_max, int S_max, int H);
 hipError_t launch_zero(void *ptr, size_t bytes, hipStream_t stream);
 // dbias: the fixed-order sum of the backward's per-workgroup column sums (scratch: joint_dbias_part_bytes)
 size_t joint_dbias_part_bytes(int64_t n_max, int V);
 hipError_t launch_joint_dbias_sum(const JointArgs &j, int V, hipStream_t stream);
 // LDS the fused joint kernels need at least (two weight-tile buffers + the bias row); at most 160 KiB per CU
 size_t joint_min_lds_bytes(int H, int V);
+// ... and the 16x16x32 backward when it sums dbias (one column-sum row per wave more)
+size_t joint_dbias_lds_bytes(int H, int V);
 
 // Launch-shape knobs (experiment hook: mrnnt_tune in mrnnt_capi.cpp). Defaults are the tuned values.
 struct Tuning {

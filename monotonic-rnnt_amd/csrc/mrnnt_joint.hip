@@ -626,22 +626,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     }
     const int V = p.V, blank = p.blank;
     const float *bias = load_bias<KS, NB>(j, V, wsh);
-    // dbias: this workgroup's column sums of G in LDS behind the bias, in a fixed order (bitwise reproducible): per
-    // chunk, each wave's 32 column sums (a DPP row reduction over each lane group's 16 rows) go to its own slot, and
-    // after the next chunk's barrier wave 0 adds the NW slots in wave order; the workgroup's row of sums then goes to
-    // dbias_part[blockIdx.x] for the ordered sum over workgroups (dbias_sum_kernel). launch_kt sizes the LDS for it.
+    // dbias: this workgroup's column sums of G, in a fixed order (bitwise reproducible): per chunk, each wave's 32
+    // column sums (a DPP row reduction over each lane group's 16 rows) go to that wave's own LDS row (every entry
+    // written once), and after the loop the NW rows are added in wave order; the workgroup's row of sums then goes to
+    // dbias_part[blockIdx.x] for the ordered sum over workgroups (launch_joint_dbias_sum). launch_kt sizes the LDS.
     const int vpad = (V + 31) / 32 * 32;
     const int wave = threadIdx.x >> 6;
-    float *dbl = const_cast<float *>(bias) + vpad;
-    float *dpart = dbl + vpad;  // [2][NW][32]
-    auto fold_chunk = [&](int cc) {  // wave 0, lanes 0..31: chunk cc's column sums in wave order
-        if (wave == 0 && lane < 32) {
-            float t = 0.0f;
-#pragma unroll
-            for (int w = 0; w < NW; ++w) t += dpart[((cc & 1) * NW + w) * 32 + lane];
-            dbl[32 * cc + lane] = t;
-        }
-    };
+    float *dbw = const_cast<float *>(bias) + vpad;  // [NW][vpad]
+    __syncthreads();  // the bias row in LDS
     bf16x8 bfr[2][K32];
     build_row<K32, 32, true>(j, q[0], 8 * g, i0, bfr[0]);
     build_row<K32, 32, true>(j, q[1], 8 * g, i0 + 16, bfr[1]);
@@ -654,7 +646,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     chunk_loop_with<KS, NB, NW>(
         j, V, wsh, leave ? 4 : -1, [&](const unsigned short *wb) { return WTile16<KS>::template mma<4>(wb, bfr, lane); },
         [&](const typename WTile16<KS>::Acc &acc, int c) {
-            if (j.dbias && c > 0) fold_chunk(c - 1);  // every wave's slots of chunk c - 1 are complete (barrier)
             const f4 bv[2] = {*reinterpret_cast<const f4 *>(bias + 32 * c + 4 * g),
                               *reinterpret_cast<const f4 *>(bias + 32 * c + 16 + 4 * g)};
             const int jb = blank - 32 * c;
@@ -713,21 +704,21 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
                     cs[k] = v;
                 }
                 if (c16 == 15) {
-                    float *slot = dpart + ((c & 1) * NW + wave) * 32;
+                    float *row = dbw + wave * vpad + 32 * c;
 #pragma unroll
-                    for (int k = 0; k < 8; ++k) slot[16 * (k >> 2) + 4 * g + (k & 3)] = cs[k];
+                    for (int k = 0; k < 8; ++k) row[16 * (k >> 2) + 4 * g + (k & 3)] = cs[k];
                 }
-                // the slots are in LDS before this wave reaches the next chunk's barrier (whose wait leaves LDS
-                // operations unwaited)
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             }
         });
     if (j.dbias) {
         __syncthreads();
-        fold_chunk((V + 31) / 32 - 1);
-        __syncthreads();
         float *row = j.dbias_part + (int64_t)blockIdx.x * vpad;
-        for (int v = threadIdx.x; v < vpad; v += blockDim.x) row[v] = dbl[v];
+        for (int v = threadIdx.x; v < vpad; v += blockDim.x) {
+            float t = 0.0f;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) t += dbw[w * vpad + v];
+            row[v] = t;
+        }
     }
 }
 
@@ -781,32 +772,63 @@ hipError_t launch_joint_dbias_sum(const JointArgs &j, int V, hipStream_t stream)
 
 // ---------------------------------------------------------------------------------------------------------
 // backward tail: dpre = dH * (1 - Hact^2) over the live rows, summed into denc[b, t] (over s; written once per
-// column) and dpred[b, s] (over t, accumulated in LDS). One workgroup per (utterance, slice of HS hidden units) walks
-// every frame of its utterance in order, so each sum has one fixed order and one writer: bitwise reproducible (no
-// float atomics). 4 hidden units per thread (8-byte loads), 256/(HS/4) rows in flight.
+// column) and dpred[b, s] (over t, accumulated in LDS frame by frame). One workgroup per (utterance, block of TT frames,
+// slice of HS hidden units); 4 hidden units per thread (8-byte loads), 256/(HS/4) rows in flight. Bitwise
+// reproducible: every sum has one fixed order and one writer -- a block's d_pred sums go to its own rows of a scratch
+// buffer (part, with the label range it touched in rng) and pred_sum_kernel adds the blocks in block order; without
+// scratch one block covers the whole utterance (TT = T_max) and flushes d_pred itself (fewer, longer workgroups).
+
+constexpr int kReduceTT = 64;  // frames per workgroup (blocked form, and the sparse variant)
 
 template <int HS>
 __global__ __launch_bounds__(256) void joint_reduce_kernel(DevProblem p, JointArgs j, const int64_t *__restrict__ off,
                                                            const unsigned short *__restrict__ dH,
-                                                           float *__restrict__ d_enc, float *__restrict__ d_pred) {
+                                                           float *__restrict__ d_enc, float *__restrict__ d_pred,
+                                                           int tt, int ntb, int wstride, float *__restrict__ part,
+                                                           int *__restrict__ rng) {
     constexpr int TPR = HS / 4;     // threads per row slice
     constexpr int RP = 256 / TPR;   // rows in parallel
     extern __shared__ float lds[];  // acc[(S_b+1) * HS] then red[RP][HS]
     const int H = j.H;
     const int nh = H / HS;
-    // the h-slices of one utterance are consecutive workgroups: they read the same rows (L2 reuse)
-    const int b = blockIdx.x / nh;
+    // the h-slices of one block of frames are consecutive workgroups: they read the same rows (L2 reuse)
+    const int bx = blockIdx.x / nh;
     const int h0 = (blockIdx.x % nh) * HS;
-    const int t0 = 0;
+    const int b = bx / ntb, blk = bx % ntb;
+    const int t0 = blk * tt;
     const int T = p.T[b], S = p.S[b];
     const int tid = threadIdx.x;
+    if (t0 >= T) {  // (past this utterance's frames: an empty label range for the block sum)
+        if (part && h0 == 0 && tid == 0) {
+            rng[2 * bx] = 1;
+            rng[2 * bx + 1] = 0;
+        }
+        return;
+    }
     const int hl = (tid % TPR) * 4, rsub = tid / TPR;
     float *acc = lds;
     float *red = lds + (S + 1) * HS;
     const int64_t tslots = j.enc_sb / H, sslots = j.pred_sb / H;
-    const int t1 = T;
-    // (the whole label range: the accumulator is flushed once per utterance)
-    const int s_lo = 0, s_hi = S;
+    const int t1 = min(t0 + tt, T);
+    // label positions this block of frames touches: rows of a column are listed by ascending s, so the first and
+    // last row of each column bound them (a few labels under an alignment restriction, the band otherwise); only
+    // that slice of the d_pred accumulator is cleared and flushed (min / max: order-independent)
+    __shared__ int srange[2];
+    if (tid == 0) {
+        srange[0] = S + 1;
+        srange[1] = -1;
+    }
+    __syncthreads();
+    for (int t = t0 + tid; t < t1; t += 256) {
+        const int64_t col = p.col_off[b] + t;
+        const int64_t r0 = off[col], r1 = off[col + 1];
+        if (r1 > r0) {
+            atomicMin(&srange[0], j.ls[r0]);
+            atomicMax(&srange[1], j.ls[r1 - 1]);
+        }
+    }
+    __syncthreads();
+    const int s_lo = srange[0], s_hi = srange[1];
     for (int i = s_lo * HS + tid; i < (s_hi + 1) * HS; i += 256) acc[i] = 0.0f;
     __syncthreads();
     for (int t = t0; t < t1; ++t) {
@@ -844,11 +866,40 @@ __global__ __launch_bounds__(256) void joint_reduce_kernel(DevProblem p, JointAr
         }
         __syncthreads();
     }
-    for (int i = s_lo * HS + tid; i < (s_hi + 1) * HS; i += 256)  // this workgroup is the one writer
-        d_pred[((int64_t)b * sslots + i / HS) * H + h0 + i % HS] += acc[i];
+    if (!part) {  // one block per utterance: this workgroup is the one writer
+        for (int i = s_lo * HS + tid; i < (s_hi + 1) * HS; i += 256)
+            d_pred[((int64_t)b * sslots + i / HS) * H + h0 + i % HS] += acc[i];
+        return;
+    }
+    float *pb = part + (int64_t)bx * wstride * H;
+    for (int i = s_lo * HS + tid; i < (s_hi + 1) * HS; i += 256) pb[(int64_t)(i / HS) * H + h0 + i % HS] = acc[i];
+    if (h0 == 0 && tid == 0) {
+        rng[2 * bx] = s_lo;
+        rng[2 * bx + 1] = s_hi;
+    }
 }
 
-constexpr int kReduceTT = 64;  // frames per workgroup of the sparse variant
+// d_pred[b, s, :] += the blocks' sums of label position s, in block order (the blocks whose range holds s)
+__global__ __launch_bounds__(256) void pred_sum_kernel(DevProblem p, const float *__restrict__ part,
+                                                       const int *__restrict__ rng, int ntb, int wstride, int H,
+                                                       int64_t sslots, float *__restrict__ d_pred) {
+    const int b = blockIdx.y;
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int s = (int)(e / H), h = (int)(e % H);
+    if (s > p.S[b]) return;
+    float t = 0.0f;
+    for (int k = 0; k < ntb; ++k) {
+        const int bx = b * ntb + k;
+        if (s >= rng[2 * bx] && s <= rng[2 * bx + 1]) t += part[((int64_t)bx * wstride + s) * H + h];
+    }
+    d_pred[((int64_t)b * sslots + s) * H + h] += t;
+}
+
+size_t joint_reduce_scratch_bytes(int B, int T_max, int S_max, int H) {
+    const int64_t ntb = (T_max + kReduceTT - 1) / kReduceTT;
+    return sizeof(float) * (size_t)B * ntb * (S_max + 1) * H + sizeof(int) * 2 * (size_t)B * ntb + 256;
+}
+
 
 // Sparse variant (development build, joint_reduce_sparse = 2; float atomics: not bitwise reproducible) (few live rows per frame, e.g. alignment-restricted training): the rows of a block of frames are
 // processed all at once (TPR threads per row) instead of frame by frame, so a workgroup does not wait one
@@ -919,7 +970,8 @@ __global__ __launch_bounds__(256) void joint_reduce_sparse_kernel(DevProblem p, 
 }
 
 hipError_t launch_joint_reduce(const DevProblem &p, const JointArgs &j, const int64_t *off, int T_max, int S_max,
-                               const unsigned short *dH, float *d_enc, float *d_pred, hipStream_t stream) {
+                               const unsigned short *dH, float *d_enc, float *d_pred, void *scratch,
+                               size_t scratch_bytes, hipStream_t stream) {
     const int ntb = (T_max + kReduceTT - 1) / kReduceTT;
     const int W = S_max + 1;
     // the row-parallel sparse kernel with float atomics: development A/B only (joint_reduce_sparse = 2)
@@ -933,7 +985,18 @@ hipError_t launch_joint_reduce(const DevProblem &p, const JointArgs &j, const in
             return;
         }
         const size_t lds = sizeof(float) * ((size_t)W * HS + 256 / (HS / 4) * HS);
-        joint_reduce_kernel<HS><<<p.B * (j.H / HS), 256, lds, stream>>>(p, j, off, dH, d_enc, d_pred);
+        if (scratch && scratch_bytes >= joint_reduce_scratch_bytes(p.B, T_max, S_max, j.H)) {
+            // blocks of kReduceTT frames, their d_pred sums added in block order by pred_sum_kernel
+            float *part = static_cast<float *>(scratch);
+            int *rng = reinterpret_cast<int *>(part + (size_t)p.B * ntb * W * j.H);
+            joint_reduce_kernel<HS><<<p.B * ntb * (j.H / HS), 256, lds, stream>>>(p, j, off, dH, d_enc, d_pred,
+                                                                                  kReduceTT, ntb, W, part, rng);
+            pred_sum_kernel<<<dim3((unsigned)(((int64_t)W * j.H + 255) / 256), (unsigned)p.B), 256, 0, stream>>>(
+                p, part, rng, ntb, W, j.H, j.pred_sb / j.H, d_pred);
+        } else {  // one block per utterance (no scratch)
+            joint_reduce_kernel<HS><<<p.B * (j.H / HS), 256, lds, stream>>>(p, j, off, dH, d_enc, d_pred, T_max, 1,
+                                                                            W, nullptr, nullptr);
+        }
     };
     if ((int64_t)p.B * ntb * (j.H / 4) > (1ll << 24)) return hipErrorInvalidValue;  // 32-bit dispatch size
     // LDS = W * HS + 4 KiB of fp32: about 30 KiB at the headline (several workgroups per CU), <= 64 KiB always
@@ -968,8 +1031,8 @@ static hipError_t launch_knw(const DevProblem &p, const JointArgs &j, size_t lds
 // and the label logit as a dot product.)
 template <int KS, int MF, bool BWD>
 static hipError_t launch_kt(const DevProblem &p, const JointArgs &j, hipStream_t stream) {
-    // the 16x16x32 backward keeps its dbias column sums and the per-wave chunk slots behind the bias
-    const size_t bias = sizeof(float) * (((p.V + 31) / 32 * 32) * (MF == 16 && BWD ? 2 : 1) + (MF == 16 && BWD ? 512 : 0));
+    // the 16x16x32 backward with dbias keeps one row of column sums per wave (8) behind the bias
+    const size_t bias = sizeof(float) * ((p.V + 31) / 32 * 32) * ((MF == 16 && BWD && j.dbias) ? 9 : 1);
     if (j.dbias && !(MF == 16 && BWD)) return hipErrorInvalidValue;
     const size_t tile = sizeof(unsigned short) * WTile<KS>::ELEMS;
     if (2 * tile + bias <= 160 * 1024) return launch_knw<KS, 2, 8, MF, BWD, 2>(p, j, 2 * tile + bias, stream);
@@ -993,9 +1056,12 @@ static hipError_t launch_kh(const DevProblem &p, const JointArgs &j, bool bwd, h
     return bwd ? launch_kb<KS, true>(p, j, stream) : launch_kb<KS, false>(p, j, stream);
 }
 
-size_t joint_min_lds_bytes(int H, int V) {  // the 16x16x32 backward (H <= 512) adds its dbias column sums + slots
-    return 2 * sizeof(unsigned short) * 32 * (size_t)H +
-           sizeof(float) * ((H <= 512 ? 2 : 1) * (((size_t)V + 31) / 32 * 32) + (H <= 512 ? 512 : 0));
+size_t joint_min_lds_bytes(int H, int V) {  // two weight tiles + the bias row
+    return 2 * sizeof(unsigned short) * 32 * (size_t)H + sizeof(float) * (((size_t)V + 31) / 32 * 32);
+}
+
+size_t joint_dbias_lds_bytes(int H, int V) {  // the 16x16x32 backward with dbias: + one column-sum row per wave
+    return joint_min_lds_bytes(H, V) + 8 * sizeof(float) * (((size_t)V + 31) / 32 * 32);
 }
 
 static hipError_t launch_joint(const DevProblem &p, const JointArgs &j, bool bwd, hipStream_t stream) {

@@ -98,6 +98,9 @@ class MrnntJointProblem(ctypes.Structure):
         ("max_shift", ctypes.c_int),
         ("hact_ld", ctypes.c_int64),
         ("dbias", ctypes.c_void_p),
+        # version 9
+        ("reduce_scratch", ctypes.c_void_p),
+        ("reduce_scratch_bytes", ctypes.c_size_t),
     ]
 
 
@@ -144,6 +147,7 @@ def _bind(path: str, dev: bool = False) -> ctypes.CDLL:
         "mrnnt_joint_live_rows": (i, [JP, vp, vp, vp]),
         "mrnnt_joint_backward": (i, [JP, vp, i64, vp, vp, vp, vp, vp, vp]),
         "mrnnt_joint_reduce": (i, [JP, vp, i64, vp, vp, vp, vp, vp]),
+        "mrnnt_joint_reduce_scratch_bytes": (i, [JP, ctypes.POINTER(sz)]),
         "mrnnt_last_error": (ctypes.c_char_p, []),
         "mrnnt_version": (i, []),
         "mrnnt_fill_zero": (i, [vp, sz, vp]),
@@ -157,8 +161,8 @@ def _bind(path: str, dev: bool = False) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.mrnnt_version() < 8:
-        raise ImportError(f"{path} is a stale build (ABI version {lib.mrnnt_version()} < 8); "
+    if lib.mrnnt_version() < 9:
+        raise ImportError(f"{path} is a stale build (ABI version {lib.mrnnt_version()} < 9); "
                           "rebuild with `make -C monotonic-rnnt_amd`")
     return lib
 

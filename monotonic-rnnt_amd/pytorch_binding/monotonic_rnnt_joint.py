@@ -139,10 +139,18 @@ class _JointPrepared:
             return G[:n], Hact[:n], bt[:n], bs[:n]
         return G[:n], Hact[:n]
 
-    def reduce(self, ws, dH, Hact, need_enc, need_pred):
-        """d_enc / d_pred (fp32) from dH = G weight over the live rows (mrnnt_joint_reduce)."""
+    def reduce(self, ws, dH, Hact, need_enc, need_pred, scratch=None):
+        """d_enc / d_pred (fp32) from dH = G weight over the live rows (mrnnt_joint_reduce). scratch: a dead device
+        buffer (G, once dH exists) for the blocked form; a fresh one is allocated when it is too small."""
         d_enc = torch.zeros(self.enc.shape, dtype=torch.float32, device=self.device)
         d_pred = torch.zeros(self.pred.shape, dtype=torch.float32, device=self.device)
+        need = ctypes.c_size_t(0)
+        _L.check(_L.load().mrnnt_joint_reduce_scratch_bytes(ctypes.byref(self.problem), ctypes.byref(need)),
+                 "joint_reduce_scratch_bytes")
+        if scratch is None or scratch.numel() * scratch.element_size() < need.value:
+            scratch = torch.empty(need.value, dtype=torch.uint8, device=self.device)
+        self.problem.reduce_scratch = scratch.data_ptr()
+        self.problem.reduce_scratch_bytes = scratch.numel() * scratch.element_size()
         with torch.cuda.device(self.device):
             _L.check(_L.load().mrnnt_joint_reduce(ctypes.byref(self.problem), _vp(ws), dH.shape[0], _vp(dH),
                                                   _vp(Hact), _vp(d_enc), _vp(d_pred), self.stream()),
@@ -157,10 +165,16 @@ _BIAS_SUM = os.environ.get("MRNNT_JOINT_BIAS_SUM") == "1"
 _DBIAS_MODE = os.environ.get("MRNNT_JOINT_DBIAS", "")
 
 
-def _dbias_in_pass(H):
+def _dbias_lds_fits(H, V):
+    """The gradient pass keeps one column-sum row per wave (8) beside two weight tiles and the bias row in the CU's
+    160 KiB of LDS (mrnnt_joint.hip joint_dbias_lds_bytes)."""
+    return 2 * 32 * H * 2 + 9 * 4 * ((V + 31) // 32 * 32) <= 160 * 1024
+
+
+def _dbias_in_pass(H, V):
     if _DBIAS_MODE == "column" and H in _HACT_LD:
         return False
-    if not _bwd_sums_columns(H):
+    if not _bwd_sums_columns(H) or not _dbias_lds_fits(H, V):
         return False
     return _DBIAS_MODE == "pass" or H >= 256
 
@@ -216,10 +230,11 @@ class MonotonicRNNTJointFunction(torch.autograd.Function):
         prep, ws = ctx.prep, ctx.saved_tensors[3]
         need_b = ctx.bias_dtype is not None and ctx.needs_input_grad[3]
         # dbias rides on the dweight GEMM (a ones column in Hact); MRNNT_JOINT_BIAS_SUM=1: a separate G.sum (A/B)
-        in_pass = need_b and not _BIAS_SUM and _dbias_in_pass(prep.H)
+        in_pass = need_b and not _BIAS_SUM and _dbias_in_pass(prep.H, prep.V)
         bias_col = need_b and ctx.needs_input_grad[2] and not _BIAS_SUM and prep.H in _HACT_LD and not in_pass
-        # the 16x16x32 gradient pass (H <= 512) sums G's columns itself: no separate pass over G
-        fused_b = need_b and not bias_col and not _BIAS_SUM and _bwd_sums_columns(prep.H)
+        # the 16x16x32 gradient pass (H <= 512, LDS permitting) sums G's columns itself: no separate pass over G
+        fused_b = (need_b and not bias_col and not _BIAS_SUM and _bwd_sums_columns(prep.H)
+                   and _dbias_lds_fits(prep.H, prep.V))
         db = torch.zeros(prep.V, dtype=torch.float32, device=prep.device) if fused_b else None
         G, Hact = prep.backward_rows(ws, grad_costs, bias_column=bias_col, dbias=db)
         d_enc = d_pred = d_w = d_b = None
@@ -235,7 +250,9 @@ class MonotonicRNNTJointFunction(torch.autograd.Function):
             d_b = G.sum(0, dtype=torch.float32).to(ctx.bias_dtype)
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
             dH = G @ prep.weight  # [n, H] bf16 (hipBLASLt)
-            d_enc, d_pred = prep.reduce(ws, dH, Hact, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+            # G is dead once dH exists (dweight / dbias came first): the reduce's scratch (stream-ordered after the GEMM)
+            d_enc, d_pred = prep.reduce(ws, dH, Hact, ctx.needs_input_grad[0], ctx.needs_input_grad[1], scratch=G)
+            del G
             d_enc = None if d_enc is None else d_enc.to(prep.enc.dtype)
             d_pred = None if d_pred is None else d_pred.to(prep.pred.dtype)
         return d_enc, d_pred, d_w, d_b, None, None, None, None, None, None
