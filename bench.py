@@ -64,6 +64,9 @@ def lengths_for(config, rank, world):
     if config == "c2":  # configs[1]
         B, T, S, V = 16, 200, 40, 256
         return np.full(B, T, np.int32), np.full(B, S, np.int32), V, "B=16,T=200,S=40,V=256 (configs[1])", "weak"
+    if config == "halo":  # (experiments) a chase-launch shape with the 4-wave halo recursion: S + 1 = 101 > 64
+        B, T, S, V = 16, 400, 100, 256
+        return np.full(B, T, np.int32), np.full(B, S, np.int32), V, "B=16,T=400,S=100,V=256 (4-wave chase)", "weak"
     if config == "c5":  # configs[4]: V = 10000, 64 utterances = 514.6 GB of acts: run as chunks
         B, T, S, V = 64, 1000, 200, 10000
         return (np.full(B, T, np.int32), np.full(B, S, np.int32), V,
@@ -103,7 +106,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="headline", choices=["headline", "c2", "ragged", "ragged64", "c5"])
+    ap.add_argument("--config", default="headline", choices=["headline", "c2", "ragged", "ragged64", "c5", "halo"])
     ap.add_argument("--cpu-sample", type=int, default=16, help="utterances in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="host threads for the CPU baseline (0 = this process's CPU share: affinity / cgroup quota)")
