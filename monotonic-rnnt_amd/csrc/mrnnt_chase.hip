@@ -140,14 +140,19 @@ struct Chase {
     __device__ __forceinline__ void gate(int f) {
         const int u = fwd ? f : T - 1 - f;
         if (u < rdy) return;
-        const uint32_t t0 = clock100();
+        uint32_t t0 = 0;
+        bool timing = false;  // (the clock is read only once a poll has failed: a frame found ready costs none)
         for (;;) {
             const int run = run_of(poll(u));
             if (run > 0) {
                 rdy = u + run;
                 return;
             }
-            if (clock100() - t0 >= budget) {
+            const uint32_t now = clock100();
+            if (!timing) {
+                t0 = now;
+                timing = true;
+            } else if (now - t0 >= budget) {
                 (*help)(f);
                 rdy = u + 1;
                 return;
