@@ -36,6 +36,7 @@
 //
 // Every lp value, every LSE and every store is the one the two-kernel path computes (the log-softmax bodies are
 // mrnnt_lsm.h's, the recursion steps mrnnt_dp.h's), so results are bit-identical to it.
+#include <algorithm>
 #include <type_traits>
 
 #include "mrnnt_dp.h"
@@ -47,6 +48,17 @@ extern "C" __device__ uint64_t mrnnt_llvm_dispatch_id() __asm("llvm.amdgcn.dispa
 
 #ifdef MRNNT_DEVTOOLS
 __device__ unsigned long long g_chase_helped;  // development build: columns a recursion wave computed itself
+// development build: per-workgroup timeline (s_memrealtime ticks) of the first kTraceWgs workgroups, 4 marks each --
+// recursion: start, lengths resolved, first frame in hand, walk done; producer: start, first slot, first flag, done
+constexpr int kTraceWgs = 4096;
+__device__ unsigned long long g_chase_trace[kTraceWgs * 4];
+#define CHASE_MARK(i)                                                                          \
+    do {                                                                                       \
+        if (threadIdx.x == 0 && blockIdx.x < (unsigned)kTraceWgs)                              \
+            g_chase_trace[blockIdx.x * 4 + (i)] = __builtin_amdgcn_s_memrealtime();            \
+    } while (0)
+#else
+#define CHASE_MARK(i) ((void)0)
 #endif
 
 // this launch's ready tag (scalar unit): a bijection of the dispatch id for a given epoch and queue
@@ -197,7 +209,7 @@ __device__ __forceinline__ void stage_loader(const DevProblem &p, const Utt &u, 
     for (;;) {
         const int i = issued + lane;
         const unsigned long long v = i < T ? load_wt(&flags[fwd ? i : T - 1 - i]) : want;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the poll and every earlier DMA have landed
+        wait_vmcnt0();  // the poll and every earlier DMA have landed
         lds_put(&st.loaded, issued);
         if (issued >= T) return;
         const unsigned long long miss = ~__ballot(v == want);
@@ -228,7 +240,10 @@ __device__ __forceinline__ void stage_loader(const DevProblem &p, const Utt &u, 
     }
 }
 
-// Wave 0: walk position u's lp row from the ring (its own row; the same value the direct pass loads), P frames ahead
+// Wave 0: walk position u's lp row from the ring (its own row; the same value the direct pass loads), P frames ahead.
+// The walk starts with an explicit vmcnt(0): the compiler's wait-count pass joins the other roles' paths into this
+// one (the kernel's control flow is structurised), takes the loader's LDS-DMAs for outstanding here, and would
+// otherwise put a vmcnt(0) -- a wait for the walk's own alpha / beta stores -- before every LDS access of the walk.
 template <int P>
 struct RingReader {
     StageLds &st;
@@ -255,10 +270,12 @@ __device__ __forceinline__ void alpha_staged(const DevProblem &p, const Utt &u, 
     const int T = u.T, S = u.S, W = S + 1;
     const bool own = lane < W;
     RingReader<P> rr(st);
+    wait_vmcnt0();  // (see RingReader)
     double a = (lane == 0) ? 0.0 : NEG_INF_D;
     Lp q[P];
 #pragma unroll
     for (int d = 0; d < P; ++d) q[d] = rr.read(min(d, T - 1));
+    CHASE_MARK(2);
     double *ap = p.alpha + u.r0;
     auto step = [&](int t, int d) {
         double y = dpp_shr1_bc(a + q[d].e);  // alpha(t-1, s-1) + lpe(t, s-1), from lane s-1
@@ -291,10 +308,12 @@ __device__ __forceinline__ void beta_staged(const DevProblem &p, const Utt &u, i
     const int T = u.T, S = u.S, W = S + 1;
     const bool own = lane < W;
     RingReader<P> rr(st);
+    wait_vmcnt0();  // (see RingReader)
     double bn = (lane == S) ? 0.0 : NEG_INF_D;  // beta(T, s)
     Lp q[P];
 #pragma unroll
     for (int d = 0; d < P; ++d) q[d] = rr.read(min(d, T - 1));
+    CHASE_MARK(2);
     double *bp = p.beta + u.r0 + (int64_t)(T - 1) * W;
     auto step = [&](int w, int d) {  // walk position w = frame T - 1 - w
         double carry = dpp_shl1_bc(bn);
@@ -330,6 +349,7 @@ __global__ __launch_bounds__(256) void chase_kernel(DevProblem p, ChaseArgs c, i
     __shared__ double xh[2][8][HL > 0 ? HL : 1];
     __shared__ typename std::conditional<STG && NW == 1, StageLds, NoStage>::type st;
     const int nrec = with_beta ? 2 * p.B : p.B;
+    CHASE_MARK(0);
     const unsigned long long tag = launch_tag(c.epoch);
     WaveLengths wl;
     if constexpr (DYN) wl = wave_lengths(p);
@@ -359,6 +379,7 @@ __global__ __launch_bounds__(256) void chase_kernel(DevProblem p, ChaseArgs c, i
         }
         const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
         const unsigned long long *flags = c.flags + u.c0;
+        CHASE_MARK(1);
         if constexpr (STG && NW == 1) {
             if (threadIdx.x == 0) {  // (LDS holds whatever the CU's previous workgroup left)
                 st.loaded = 0;
@@ -375,6 +396,7 @@ __global__ __launch_bounds__(256) void chase_kernel(DevProblem p, ChaseArgs c, i
                 beta_staged<4>(p, u, b, st);
             else
                 alpha_staged<4>(p, u, b, costs, st);
+            CHASE_MARK(3);
             return;
         }
         if (wave >= NW) return;  // one-wave direct recursion: the other waves of the workgroup have no work
@@ -413,6 +435,8 @@ __global__ __launch_bounds__(256) void chase_kernel(DevProblem p, ChaseArgs c, i
         tmax = __builtin_amdgcn_readfirstlane(tmax);
         slots = (with_beta ? (int64_t)(tmax + 1) / 2 : (int64_t)tmax) * per;
     }
+    CHASE_MARK(1);
+    bool first = true;
     for (int64_t si = (int64_t)blockIdx.x - nrec; si < slots; si += G) {
         const int kr = (int)(si / per);
         const int r = (int)(si - (int64_t)kr * per);
@@ -451,7 +475,10 @@ __global__ __launch_bounds__(256) void chase_kernel(DevProblem p, ChaseArgs c, i
         drain_stores();  // every wave: its write-through rows have landed
         __syncthreads();
         if (threadIdx.x == 0) store_wt(&c.flags[k.c], tag);
+        if (first) CHASE_MARK(2);
+        first = false;
     }
+    CHASE_MARK(3);
 }
 
 // The log-softmax body the chase launch carries for this problem (-1: none -- the two-kernel path runs). f32 acts,
@@ -510,6 +537,12 @@ hipError_t launch_chase(const DevProblem &p, const ChaseArgs &c, int elem, int S
 }
 
 #ifdef MRNNT_DEVTOOLS
+int chase_trace(unsigned long long *out, int n) {
+    n = std::min(n, kTraceWgs * 4);
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chase_trace), sizeof(unsigned long long) * n) != hipSuccess) return -1;
+    return n;
+}
+
 unsigned long long chase_helped(bool reset) {
     unsigned long long v = 0;
     if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_chase_helped), sizeof(v)) != hipSuccess) return ~0ull;

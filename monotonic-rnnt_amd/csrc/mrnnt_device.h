@@ -528,7 +528,16 @@ __device__ __forceinline__ void store_lp_wt(__amdgpu_buffer_rsrc_t r, unsigned v
 }
 
 // every store this wave issued has completed (the drain before a hand-off flag)
-__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// s_waitcnt vmcnt(0) through the builtin, which the compiler's wait-count pass sees: an inline-asm wait is opaque to
+// it, so it would go on counting the operations before it as outstanding -- an LDS-DMA among them makes it wait for
+// vmcnt(0) again before later LDS accesses, e.g. once per recursion step on the walk's global stores. (The empty asm
+// statements keep memory operations from moving across it.)
+__device__ __forceinline__ void wait_vmcnt0() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt = 0; expcnt, lgkmcnt unconstrained
+    asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void drain_stores() { wait_vmcnt0(); }
 
 template <class IO>
 __device__ __forceinline__ typename IO::V splat(float f) {

@@ -340,7 +340,7 @@ struct WTile16 {
     }
 };
 
-__device__ __forceinline__ void wait_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void wait_dma() { wait_vmcnt0(); }
 
 // wait until at most N vector-memory operations of this wave are outstanding (in-order completion): the
 // DMA of the chunk after next stays in flight across the barrier
