@@ -249,7 +249,9 @@ class MonotonicRNNTJointFunction(torch.autograd.Function):
         elif need_b and not bias_col:
             d_b = G.sum(0, dtype=torch.float32).to(ctx.bias_dtype)
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
-            dH = G @ prep.weight  # [n, H] bf16 (hipBLASLt)
+            # [n, H] bf16 (hipBLASLt), with W^T stored [H, V] (1 MB copy): hipBLASLt's kernel for that layout runs
+            # 3.9 vs 4.4 ms at H = 512 (profiles/r04/joint/gemm_probe.json)
+            dH = G @ prep.weight.t().contiguous().t()
             # G is dead once dH exists (dweight / dbias came first): the reduce's scratch (stream-ordered after the GEMM)
             d_enc, d_pred = prep.reduce(ws, dH, Hact, ctx.needs_input_grad[0], ctx.needs_input_grad[1], scratch=G)
             del G
