@@ -368,3 +368,33 @@ def test_chase_beside_a_kernel_holding_the_cus(op, dev):
         got = _run(op, a, lab, Tt, St)
         _assert_same(got, ref)
     torch.cuda.synchronize()
+
+
+def test_chase_two_streams_near_the_recursion_limit(op, dev):
+    """the spinning recursion workgroups of two concurrent chase launches, each at a batch near
+    chase_pays' limit (2B = 240 of 256 CUs), can hold the slots their producers need. The waves help themselves
+    after the wait budget, so both calls finish with the two-kernel path's bits."""
+    rng = np.random.default_rng(77)
+    B = 120
+    acts, labels, T, S = random_problem(rng, B, (90, 100), 30, 128, force={b: (100, 30) for b in range(0, B, 7)})
+    a, lab = torch.from_numpy(acts).to(dev), torch.from_numpy(labels).to(dev)
+    b = torch.flip(a, [1]).contiguous()
+    Tt, St = torch.from_numpy(T), torch.from_numpy(S)
+    with knobs(chase=0):
+        ra, rb = _run(op, a, lab, Tt, St), _run(op, b, lab, Tt, St)
+    n = _launches(lambda: _run(op, a, lab, Tt, St))
+    assert n["chase"] == 1, n
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for st in streams:
+        st.wait_stream(torch.cuda.current_stream())
+    outs = {}
+    for _ in range(3):
+        for key, x, st in (("a", a, streams[0]), ("b", b, streams[1])):
+            with torch.cuda.stream(st):
+                xx = x.detach().clone().requires_grad_(True)
+                c = op.monotonic_rnnt_loss(xx, lab, Tt, St)
+                c.sum().backward()
+                outs[key] = (c.detach(), xx.grad)
+    torch.cuda.synchronize()
+    _assert_same(outs["a"], ra)
+    _assert_same(outs["b"], rb)
