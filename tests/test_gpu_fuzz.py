@@ -2,7 +2,8 @@
 kernel variants switch on: V (vector width, chunking, FULL / ragged rows, V < 4, odd V), S+1 (single-wave /
 halo / per-step-barrier recursion, gradient segments of 256 rows), blank anywhere in [0, V), labels that may equal
 the blank, alignment restriction with random k, per-utterance gradient scales (negative and zero included),
-packed and padded layouts, f32 / bf16 / f16 acts; then the same generator through the other launch variants.
+packed and padded layouts, f32 / bf16 / f16 acts, host or device-resident lengths (round 4); then the same
+generator through the other launch variants.
 Tolerances as tests/test_gpu_parity.py (reduced precision: the grads tolerance adds one rounding of the acts type).
 The sweep found the stale-workspace bug pinned by test_gpu_parity.py::test_stale_workspace_contents_do_not_matter.
 """
@@ -73,8 +74,11 @@ def make_case(seed):
             align[b, fr[align[b, fr] == blank]] = (blank + 1) % V
     dtype = rng.choice(["f32"] * 6 + ["bf16", "f16"])
     padded = bool(rng.random() < 0.25)
+    # the reference's calling convention (lengths on the device, monotonic_rnnt.cu:85-88): planned from bounds and
+    # validated on the GPU, the chase launch included (drawn last: earlier fields keep their seeds' values)
+    dev_lengths = bool(rng.random() < 0.4)
     return dict(V=V, T=T, S=S, blank=blank, labels=labels, acts=acts, scale=scale, align=align, k=k,
-                dtype=str(dtype), padded=padded)
+                dtype=str(dtype), padded=padded, dev_lengths=dev_lengths)
 
 
 def pad(acts, T, S, pad_T, pad_S1):
@@ -189,7 +193,10 @@ def check_case(op, dev, c, cost_only_too=False):
     a = a.to(dev).requires_grad_(True)
     lab = torch.from_numpy(c["labels"]).to(dev)
     al = None if c["align"] is None else torch.from_numpy(c["align"]).to(dev)
-    costs = op.monotonic_rnnt_loss(a, lab, torch.from_numpy(T), torch.from_numpy(S), al, c["k"], c["blank"])
+    Tt, St = torch.from_numpy(T), torch.from_numpy(S)
+    if c.get("dev_lengths"):
+        Tt, St = Tt.to(dev), St.to(dev)
+    costs = op.monotonic_rnnt_loss(a, lab, Tt, St, al, c["k"], c["blank"])
     (costs * torch.from_numpy(c["scale"]).to(dev)).sum().backward()
     g = a.grad.float().cpu().numpy()
     if c["padded"]:
@@ -213,5 +220,5 @@ def check_case(op, dev, c, cost_only_too=False):
     tol = 1e-4 + rel * np.abs(gr[gfin])
     assert np.all(np.abs(g[gfin] - gr[gfin]) <= tol), np.abs(g[gfin] - gr[gfin]).max()
     if cost_only_too:  # the cost-only forward (no beta pass) gives the same costs bit for bit
-        c2 = op.monotonic_rnnt_loss(a.detach(), lab, torch.from_numpy(T), torch.from_numpy(S), al, c["k"], c["blank"])
+        c2 = op.monotonic_rnnt_loss(a.detach(), lab, Tt, St, al, c["k"], c["blank"])
         assert np.array_equal(c2.float().cpu().numpy().astype(np.float64), cc)
