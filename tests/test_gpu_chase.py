@@ -398,3 +398,24 @@ def test_chase_two_streams_near_the_recursion_limit(op, dev):
     torch.cuda.synchronize()
     _assert_same(outs["a"], ra)
     _assert_same(outs["b"], rb)
+
+
+@pytest.mark.parametrize("B", [64, 65])
+def test_chase_device_lengths_batch_limit(op, dev, B):
+    """Device lengths ride in one register per lane of every wave, so the chase launch takes them up to B = 64 and
+    B = 65 plans with a setup kernel and runs the two-kernel forward -- both with the two-kernel path's bits."""
+    rng = np.random.default_rng(600 + B)
+    acts, labels, T, S = random_problem(rng, B, (20, 40), 12, 64, force={0: (1, 0), 5: (40, 12)})
+    a, lab = torch.from_numpy(acts).to(dev), torch.from_numpy(labels[:, :max(1, int(S.max()))].copy()).to(dev)
+    Tt, St = torch.from_numpy(T), torch.from_numpy(S)
+    with knobs(chase=0):
+        ref = _run(op, a, lab, Tt, St)
+    Td, Sd = Tt.to(dev), St.to(dev)
+    n = _launches(lambda: _run(op, a, lab, Td, Sd))
+    got = _run(op, a, lab, Td, Sd)
+    _assert_same(got, ref)
+    if B <= 64:
+        assert n["chase"] == 1 and n["setup"] == 0, n
+    else:
+        assert n["chase"] == 0 and n["setup"] == 1, n
+    op.check_lengths()
