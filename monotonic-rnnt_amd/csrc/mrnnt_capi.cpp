@@ -1028,6 +1028,7 @@ int mrnnt_profile_read(double *total_ms, int64_t *launches, int n) {
 // development build: columns chase recursion waves computed themselves since the last reset (mrnnt_chase.hip)
 __attribute__((visibility("default"))) unsigned long long mrnnt_chase_helped(int reset) { return chase_helped(reset != 0); }
 __attribute__((visibility("default"))) int mrnnt_chase_trace(unsigned long long *out, int n) { return chase_trace(out, n); }
+__attribute__((visibility("default"))) int mrnnt_joint_trace(unsigned long long *out, int n) { return joint_trace(out, n); }
 
 // launch knobs: exported by the development build only (libmonotonic_rnnt_amd_dev.so, `make dev`)
 __attribute__((visibility("default"))) int mrnnt_tune(const char *key, int value) {

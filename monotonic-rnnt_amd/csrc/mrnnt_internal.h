@@ -252,6 +252,7 @@ inline int64_t chase_slots(int B, int T_max, int with_beta) {
 // development build: columns chase recursion waves computed themselves (since the last reset)
 unsigned long long chase_helped(bool reset);
 int chase_trace(unsigned long long *out, int n);  // development build: the chase launch timeline
+int joint_trace(unsigned long long *out, int n);  // development build: the fused joint forward's wave timeline
 hipError_t launch_chase(const DevProblem &p, const ChaseArgs &c, int elem, int S_max, int with_beta, int producers,
                         float *costs, hipStream_t stream);
 hipError_t launch_grad(const DevProblem &p, int elem, const float *scale, void *grads, int grid, hipStream_t stream);

@@ -18,12 +18,27 @@
 // D[vocab][row] = sum_k W[vocab][k] h[row][k]: the accumulator holds 16 vocabulary entries of ONE row per
 // lane (vocab = (i&3) + 8 (i>>2) + 4 (l>>5)), so the per-row online softmax is register-local and the two
 // lane halves merge once at the end.
+#include <algorithm>
 #include <type_traits>
 #include <utility>
 
 #include "mrnnt_device.h"
 
 namespace mrnnt {
+
+#ifdef MRNNT_DEVTOOLS
+// development build: the forward's per-wave timeline (s_memrealtime ticks) for waves 0 and 4 of the first
+// kJointTraceWgs workgroups, 5 marks each: start, bias staged, activations built, first chunk done, end
+constexpr int kJointTraceWgs = 4096;
+__device__ unsigned long long g_joint_trace[kJointTraceWgs * 10];
+#define JOINT_MARK(i)                                                                                         \
+    do {                                                                                                      \
+        if ((threadIdx.x & 255) == 0 && blockIdx.x < (unsigned)kJointTraceWgs)                                 \
+            g_joint_trace[blockIdx.x * 10 + (threadIdx.x >> 8) * 5 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define JOINT_MARK(i) ((void)0)
+#endif
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -446,14 +461,17 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
                                                                                              JointArgs j) {
     extern __shared__ __attribute__((aligned(16))) unsigned short wsh[];
     if ((int64_t)blockIdx.x * (32 * NW) >= list_len(j)) return;  // whole workgroup past a shorter list
+    JOINT_MARK(0);
     const int lane = threadIdx.x & 63, half = lane >> 5;
     const int64_t i = (int64_t)blockIdx.x * (32 * NW) + (threadIdx.x >> 6) * 32 + (lane & 31);
     const RowPos q = row_pos(p, j, i);
     const int V = p.V, blank = p.blank;
     const float *bias = load_bias<KS, NB>(j, V, wsh);
     __syncthreads();
+    JOINT_MARK(1);
     bf16x8 bfr[KS];
     build_act<KS, false>(j, q, half, i, bfr);
+    JOINT_MARK(2);
 
     const f2 l2e = {kLog2e, kLog2e};
     float m = NEG_INF_F, sum = 0.0f, zb = 0.0f, ze = 0.0f;
@@ -493,6 +511,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
                 fe = true;
             }
         }
+        if (c == 0) JOINT_MARK(3);
     });
     // merge the two lane halves (same row, disjoint vocabulary)
     const float m2 = __shfl_xor(m, 32), s2 = __shfl_xor(sum, 32);
@@ -508,7 +527,16 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
         p.den[q.row] = (float)den;
         p.lp[q.row] = Lp{(double)zb + den, (q.lab >= 0 ? (double)ze : (q.lab == -2 ? __builtin_nan("") : 0.0)) + den};
     }
+    JOINT_MARK(4);
 }
+
+#ifdef MRNNT_DEVTOOLS
+int joint_trace(unsigned long long *out, int n) {
+    n = std::min(n, kJointTraceWgs * 10);
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_joint_trace), sizeof(unsigned long long) * n) != hipSuccess) return -1;
+    return n;
+}
+#endif
 
 template <int KS, int NB, int NW, int RG>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2))) void joint_bwd_kernel(DevProblem p,

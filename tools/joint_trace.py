@@ -1,0 +1,48 @@
+"""Timeline of the fused joint forward (development build, g_joint_trace): waves 0 and 4 of the first 4096
+workgroups at H = 512 (tools/joint_bench.py's problem)."""
+import ctypes
+import json
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, "monotonic-rnnt_amd/pytorch_binding")
+import _mrnnt_lib as L  # noqa: E402
+
+L.select_dev()
+import monotonic_rnnt_joint as J  # noqa: E402
+
+dev = torch.device("cuda:0")
+g = torch.Generator(device=dev).manual_seed(0)
+B, T, S, V, H = 64, 1000, 200, 1024, 512
+enc = torch.randn(B, T, H, device=dev, generator=g).to(torch.bfloat16)
+pred = torch.randn(B, S + 1, H, device=dev, generator=g).to(torch.bfloat16)
+W = (torch.randn(V, H, device=dev, generator=g) * (2.0 / H ** 0.5)).to(torch.bfloat16)
+bias = (0.1 * torch.randn(V, device=dev, generator=g))
+labels = torch.from_numpy(np.random.default_rng(1).integers(1, V, (B, S)).astype(np.int32)).to(dev)
+Tl = torch.full((B,), T, dtype=torch.int32)
+Sl = torch.full((B,), S, dtype=torch.int32)
+lib = L.load_dev()
+out = []
+for it in range(3):
+    with torch.no_grad():
+        J.monotonic_rnnt_joint_loss(enc, pred, W, bias, labels, Tl, Sl)
+    torch.cuda.synchronize()
+    buf = (ctypes.c_ulonglong * (4096 * 10))()
+    n = lib.mrnnt_joint_trace(buf, 4096 * 10)
+    tr = np.frombuffer(buf, dtype=np.uint64)[:n].reshape(-1, 2, 5).astype(np.int64)
+    rel = (tr - tr[:, :, :1]) / 100.0  # us since each wave's start
+    life = rel[:, :, 4]
+    res = {
+        "wave_life_us_median": float(np.median(life)),
+        "bias_staged_us": float(np.median(rel[:, :, 1])),
+        "build_us": float(np.median(rel[:, :, 2] - rel[:, :, 1])),
+        "first_chunk_us": float(np.median(rel[:, :, 3] - rel[:, :, 2])),
+        "rest_chunks_us": float(np.median(rel[:, :, 4] - rel[:, :, 3])),
+        "build_frac": float(np.median((rel[:, :, 2] - rel[:, :, 1]) / life)),
+        "wave4_start_minus_wave0_us": float(np.median((tr[:, 1, 0] - tr[:, 0, 0]) / 100.0)),
+    }
+    out.append(res)
+    print(json.dumps(res), flush=True)
+json.dump(out, open(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/joint_trace.json", "w"), indent=1)
