@@ -27,14 +27,14 @@
 namespace mrnnt {
 
 #ifdef MRNNT_DEVTOOLS
-// development build: the forward's per-wave timeline (s_memrealtime ticks) for waves 0 and 4 of the first
+// development build: the forward's per-wave timeline (s_memrealtime ticks) for every wave (8) of the first
 // kJointTraceWgs workgroups, 5 marks each: start, bias staged, activations built, first chunk done, end
 constexpr int kJointTraceWgs = 4096;
-__device__ unsigned long long g_joint_trace[kJointTraceWgs * 10];
+__device__ unsigned long long g_joint_trace[kJointTraceWgs * 40];
 #define JOINT_MARK(i)                                                                                         \
     do {                                                                                                      \
-        if ((threadIdx.x & 255) == 0 && blockIdx.x < (unsigned)kJointTraceWgs)                                 \
-            g_joint_trace[blockIdx.x * 10 + (threadIdx.x >> 8) * 5 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+        if ((threadIdx.x & 63) == 0 && blockIdx.x < (unsigned)kJointTraceWgs && threadIdx.x < 512)            \
+            g_joint_trace[blockIdx.x * 40 + (threadIdx.x >> 6) * 5 + (i)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #else
 #define JOINT_MARK(i) ((void)0)
@@ -532,7 +532,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
 
 #ifdef MRNNT_DEVTOOLS
 int joint_trace(unsigned long long *out, int n) {
-    n = std::min(n, kJointTraceWgs * 10);
+    n = std::min(n, kJointTraceWgs * 40);
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_joint_trace), sizeof(unsigned long long) * n) != hipSuccess) return -1;
     return n;
 }

@@ -29,19 +29,21 @@ for it in range(3):
     with torch.no_grad():
         J.monotonic_rnnt_joint_loss(enc, pred, W, bias, labels, Tl, Sl)
     torch.cuda.synchronize()
-    buf = (ctypes.c_ulonglong * (4096 * 10))()
-    n = lib.mrnnt_joint_trace(buf, 4096 * 10)
-    tr = np.frombuffer(buf, dtype=np.uint64)[:n].reshape(-1, 2, 5).astype(np.int64)
-    rel = (tr - tr[:, :, :1]) / 100.0  # us since each wave's start
-    life = rel[:, :, 4]
+    buf = (ctypes.c_ulonglong * (4096 * 40))()
+    n = lib.mrnnt_joint_trace(buf, 4096 * 40)
+    tr = np.frombuffer(buf, dtype=np.uint64)[:n].reshape(-1, 8, 5).astype(np.int64)
+    t0 = tr[:, :, 0].min(axis=1, keepdims=True)
+    rel = (tr - t0[:, :, None]) / 100.0  # us since the workgroup's first wave started
+    build_end = rel[:, :, 2]
     res = {
-        "wave_life_us_median": float(np.median(life)),
-        "bias_staged_us": float(np.median(rel[:, :, 1])),
-        "build_us": float(np.median(rel[:, :, 2] - rel[:, :, 1])),
-        "first_chunk_us": float(np.median(rel[:, :, 3] - rel[:, :, 2])),
+        "tile_us_median": float(np.median(rel[:, :, 4].max(axis=1))),
+        "build_us_median": float(np.median(rel[:, :, 2] - rel[:, :, 1])),
+        "build_end_first_us": float(np.median(build_end.min(axis=1))),
+        "build_end_last_us": float(np.median(build_end.max(axis=1))),
+        "build_skew_us": float(np.median(build_end.max(axis=1) - build_end.min(axis=1))),
+        "first_chunk_done_after_last_build_us": float(np.median(rel[:, :, 3].min(axis=1) - build_end.max(axis=1))),
         "rest_chunks_us": float(np.median(rel[:, :, 4] - rel[:, :, 3])),
-        "build_frac": float(np.median((rel[:, :, 2] - rel[:, :, 1]) / life)),
-        "wave4_start_minus_wave0_us": float(np.median((tr[:, 1, 0] - tr[:, 0, 0]) / 100.0)),
+        "wave_start_spread_us": float(np.median(rel[:, :, 0].max(axis=1))),
     }
     out.append(res)
     print(json.dumps(res), flush=True)
