@@ -28,13 +28,14 @@ namespace mrnnt {
 
 #ifdef MRNNT_DEVTOOLS
 // development build: the forward's per-wave timeline (s_memrealtime ticks) for every wave (8) of the first
-// kJointTraceWgs workgroups, 5 marks each: start, bias staged, activations built, first chunk done, end
+// kJointTraceWgs workgroups, 8 marks each: start, bias staged, activations built, first chunk done, end, and inside
+// chunk 0: after the DMA wait, after the barrier, after the MFMAs
 constexpr int kJointTraceWgs = 4096;
-__device__ unsigned long long g_joint_trace[kJointTraceWgs * 40];
+__device__ unsigned long long g_joint_trace[kJointTraceWgs * 64];
 #define JOINT_MARK(i)                                                                                         \
     do {                                                                                                      \
         if ((threadIdx.x & 63) == 0 && blockIdx.x < (unsigned)kJointTraceWgs && threadIdx.x < 512)            \
-            g_joint_trace[blockIdx.x * 40 + (threadIdx.x >> 6) * 5 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+            g_joint_trace[blockIdx.x * 64 + (threadIdx.x >> 6) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #else
 #define JOINT_MARK(i) ((void)0)
@@ -430,9 +431,12 @@ __device__ __forceinline__ void chunk_loop_with(const JointArgs &j, int V, unsig
         } else {
             wait_dma();
         }
+        if (c == 0) JOINT_MARK(5);
         __builtin_amdgcn_s_barrier();
+        if (c == 0) JOINT_MARK(6);
         if (c + NB - 1 < nch) WT::template stage<NW>(j, V, c + NB - 1, wsh + ((c + NB - 1) % NB) * WT::ELEMS);
         const auto acc = mma(wsh + (c % NB) * WT::ELEMS);
+        if (c == 0) JOINT_MARK(7);
         epi(acc, c);
     }
 }
@@ -532,7 +536,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
 
 #ifdef MRNNT_DEVTOOLS
 int joint_trace(unsigned long long *out, int n) {
-    n = std::min(n, kJointTraceWgs * 40);
+    n = std::min(n, kJointTraceWgs * 64);
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_joint_trace), sizeof(unsigned long long) * n) != hipSuccess) return -1;
     return n;
 }

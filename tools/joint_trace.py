@@ -29,9 +29,9 @@ for it in range(3):
     with torch.no_grad():
         J.monotonic_rnnt_joint_loss(enc, pred, W, bias, labels, Tl, Sl)
     torch.cuda.synchronize()
-    buf = (ctypes.c_ulonglong * (4096 * 40))()
-    n = lib.mrnnt_joint_trace(buf, 4096 * 40)
-    tr = np.frombuffer(buf, dtype=np.uint64)[:n].reshape(-1, 8, 5).astype(np.int64)
+    buf = (ctypes.c_ulonglong * (4096 * 64))()
+    n = lib.mrnnt_joint_trace(buf, 4096 * 64)
+    tr = np.frombuffer(buf, dtype=np.uint64)[:n].reshape(-1, 8, 8).astype(np.int64)
     t0 = tr[:, :, 0].min(axis=1, keepdims=True)
     rel = (tr - t0[:, :, None]) / 100.0  # us since the workgroup's first wave started
     build_end = rel[:, :, 2]
@@ -44,6 +44,10 @@ for it in range(3):
         "first_chunk_done_after_last_build_us": float(np.median(rel[:, :, 3].min(axis=1) - build_end.max(axis=1))),
         "rest_chunks_us": float(np.median(rel[:, :, 4] - rel[:, :, 3])),
         "wave_start_spread_us": float(np.median(rel[:, :, 0].max(axis=1))),
+        "chunk0_wait_us": float(np.median(rel[:, :, 5] - rel[:, :, 2])),
+        "chunk0_barrier_us": float(np.median(rel[:, :, 6] - rel[:, :, 5])),
+        "chunk0_mma_us": float(np.median(rel[:, :, 7] - rel[:, :, 6])),
+        "chunk0_epilogue_us": float(np.median(rel[:, :, 3] - rel[:, :, 7])),
     }
     out.append(res)
     print(json.dumps(res), flush=True)
