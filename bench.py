@@ -422,9 +422,13 @@ def run(args, world):
     loss_val = float(loss_val.item())
     prof = prof_main
     el = coll(torch.tensor([elapsed], dtype=torch.float64, device=dev))
+    rank_elapsed = [float(el.item())]
     if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
+        g = [torch.zeros_like(el) for _ in range(world)]
+        dist.all_gather(g, el)
+        rank_elapsed = [float(x.item()) for x in g]
+    elapsed = max(rank_elapsed)
+    ar_us = allreduce_latency_us(dist, coll, torch, dev, world)
     total_utts = coll(torch.tensor([B], dtype=torch.int64, device=dev))
     if world > 1:
         dist.all_reduce(total_utts)
@@ -463,14 +467,17 @@ def run(args, world):
             ek = {"f32": "IoF32", "bf16": "IoBF16", "f16": "IoF16"}[args.acts_dtype]
             # the counter record belongs to this exact workload only: same config and acts dtype, and the same
             # live-row bytes per launch (an alignment band, a shard or chunking all change those)
-            # workload, measured with this very library build (its sha256)
+            # workload, measured on a library built from these very sources (source_sha256: csrc/ + include/ +
+            # Makefile + ROCm release; the build is path-independent) or this very binary (lib_sha256)
             if (pm.get("config") == args.config and pm.get("dtype") == args.acts_dtype
                     and pm.get("kernel", "").startswith(f"grad_staged_kernel<{ek}")
                     and pm.get("algorithmic_bytes_per_launch") == grad_bytes // n_chunks
-                    and pm.get("lib_sha256") == lib_sha256(L.LIB_PATH)):
+                    and (pm.get("source_sha256") == L.source_sha256()
+                         or pm.get("lib_sha256") == lib_sha256(L.LIB_PATH))):
                 traffic = pm.get("hbm_bytes_per_launch")
                 traffic_source = {"file": os.path.relpath(pmc_path, ROOT), "run": pm.get("source"),
-                                  "lib_sha256": pm.get("lib_sha256"), "measured_in_this_run": False}
+                                  "source_sha256": pm.get("source_sha256"), "lib_sha256": pm.get("lib_sha256"),
+                                  "measured_in_this_run": False}
         except Exception:
             traffic = None
 
@@ -531,6 +538,16 @@ def run(args, world):
                 "grad": {"avg_ms": round(g_avg, 4) if g_avg else None, "gbps": round(achieved, 1) if achieved else None},
             },
             "cpu_baseline": cpu,
+            # what the driver needs to compare N > 1 with N = 1: every rank's own step time (value uses the max),
+            # their spread, and the loss all-reduce's own latency (timed alone after the steps, max over ranks)
+            "ranks": {"n": world, "ms_per_step": [round(e * 1e3 / args.steps, 4) for e in rank_elapsed],
+                      "max_ms_per_step": round(max(rank_elapsed) * 1e3 / args.steps, 4),
+                      "min_ms_per_step": round(min(rank_elapsed) * 1e3 / args.steps, 4),
+                      "balance_min_over_max": round(min(rank_elapsed) / max(rank_elapsed), 4),
+                      "devices_distinct": len({(d["device"], d["pci_bus"], d["pci_device"])
+                                               for d in rank_devices}) == world,
+                      "allreduce_4byte_us": ar_us,
+                      "collective": "none" if world == 1 else ("gloo (rehearsal)" if gloo else "RCCL")},
             "lengths_ab": lengths_ab,
             "grads_placement": placement_log(),
             "tune": args.tune or None,
@@ -539,6 +556,25 @@ def run(args, world):
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def allreduce_latency_us(dist, coll, torch, dev, world, reps=50):
+    """Average latency of the step's one collective -- a 4-byte sum all-reduce -- each one completed before the next
+    (synchronised), max over ranks; None at world size 1."""
+    if world == 1:
+        return None
+    x = coll(torch.ones(1, dtype=torch.float32, device=dev))
+    for _ in range(5):
+        dist.all_reduce(x)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dist.all_reduce(x)
+        torch.cuda.synchronize()
+    t = coll(torch.tensor([(time.perf_counter() - t0) / reps * 1e6], dtype=torch.float64, device=dev))
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return round(float(t.item()), 2)
 
 
 def lib_sha256(path):

@@ -19,6 +19,9 @@
 // Differences:
 //  * restrict_to_alignment() records the alignment, and the band is built on the device at compute time instead of
 //    a host loop with blocking copies (:191-219);
+//  * every data member is an OUTPUT: min_allowed_s / max_allowed_s show the band of the last computation; the
+//    reference's computer reads the band from them (gpu_rnnt.h:103,149,196), this library does not -- a band written
+//    into them is ignored (the call is unrestricted unless restrict_to_alignment() was called) and overwritten;
 //  * the getters read the state of the last cost() / cost_and_grad() on this workspace (betas / ll_backward only
 //    after cost_and_grad, as in the reference, whose cost() skips the beta pass). Cells outside the lattice band
 //    read -inf (the reference leaves them unwritten), and denom_host() covers every row as the reference's reduce

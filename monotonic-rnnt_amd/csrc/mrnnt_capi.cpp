@@ -34,18 +34,8 @@ using namespace mrnnt;
 
 namespace {
 
-thread_local std::string g_last_error = "no error";
-
-RNNTStatus fail(RNNTStatus st, const std::string &msg) {
-    g_last_error = msg;
-    return st;
-}
-
-}  // namespace
-
-RNNTStatus mrnnt::set_error(RNNTStatus st, const std::string &msg) { return fail(st, msg); }
-
-namespace {
+// this thread's mrnnt_last_error() (the error state lives in mrnnt_entry.cpp)
+RNNTStatus fail(RNNTStatus st, const std::string &msg) { return mrnnt::set_error(st, msg); }
 
 RNNTStatus fail_hip(hipError_t e, const char *where) {
     return fail(RNNT_STATUS_EXECUTION_FAILED, std::string(where) + ": " + hipGetErrorString(e));
@@ -103,7 +93,10 @@ bool chase_shape_ok(const Plan &pl) {
     if (pl.align || pl.elem != ELEM_F32 || chase_body_shape(pl.V) < 0) return false;
     if (pl.S_max + 1 > 4 * 56 || pl.N * (int64_t)sizeof(Lp) >= ((int64_t)1 << 31)) return false;
     if (pl.dyn && pl.B > 64) return false;
-    if (2 * pl.B > cu_count_of_device()) return false;
+    // one recursion workgroup per utterance and direction: the cost-only forward needs B of them, the gradient call 2B
+    // (chase_pays decides per call). The flags are sized here, so the workspace size depends on the CU count of the
+    // device current when the plan is made (a problem of B > CUs utterances never takes the chase).
+    if (pl.B > cu_count_of_device()) return false;
     const double pass_s = (double)pl.N * pl.V * 4.0 / 6.0e12, recursion_s = mean_frames(pl) * 1.0e-7;
     return recursion_s >= 0.25 * pass_s;
 }
@@ -422,9 +415,7 @@ hipError_t timed(int id, hipStream_t s, F &&launch) {
 
 extern "C" {
 
-int mrnnt_version(void) { return MRNNT_VERSION; }
-
-const char *mrnnt_last_error(void) { return g_last_error.c_str(); }
+// mrnnt_version, mrnnt_last_error, mrnnt_lattice_bytes / mrnnt_lattice_host: mrnnt_entry.cpp (host-only)
 
 RNNTStatus mrnnt_workspace_size(const mrnnt_problem *p, size_t *bytes) {
     if (!bytes) return fail(RNNT_STATUS_INVALID_VALUE, "null size pointer");
@@ -432,36 +423,6 @@ RNNTStatus mrnnt_workspace_size(const mrnnt_problem *p, size_t *bytes) {
     const RNNTStatus st = make_plan(p, &pl);
     if (st != RNNT_STATUS_SUCCESS) return st;
     *bytes = pl.total;
-    return RNNT_STATUS_SUCCESS;
-}
-
-RNNTStatus mrnnt_lattice_bytes(const mrnnt_problem *p, size_t *bytes) {
-    // needs only B, T_host and S_host
-    if (!bytes || !p) return fail(RNNT_STATUS_INVALID_VALUE, "null argument");
-    if (p->B <= 0 || !p->T_host || !p->S_host) return fail(RNNT_STATUS_INVALID_VALUE, "B > 0 and host lengths required");
-    int64_t cols = 0;
-    for (int b = 0; b < p->B; ++b) {
-        if (p->T_host[b] <= 0 || p->S_host[b] < 0 || p->T_host[b] < p->S_host[b])
-            return fail(RNNT_STATUS_INVALID_VALUE, "invalid lengths at utterance " + std::to_string(b));
-        cols += p->T_host[b];
-    }
-    *bytes = sizeof(int64_t) * 2 * ((size_t)p->B + 1) + sizeof(int) * (size_t)cols;
-    return RNNT_STATUS_SUCCESS;
-}
-
-RNNTStatus mrnnt_lattice_host(const mrnnt_problem *p, void *host, size_t bytes) {
-    size_t need = 0;
-    const RNNTStatus st = mrnnt_lattice_bytes(p, &need);
-    if (st != RNNT_STATUS_SUCCESS) return st;
-    if (!host || bytes < need) return fail(RNNT_STATUS_INVALID_VALUE, "lattice buffer too small: need " + std::to_string(need));
-    int64_t *row = static_cast<int64_t *>(host), *col = row + p->B + 1;
-    int *col_b = reinterpret_cast<int *>(col + p->B + 1);
-    row[0] = col[0] = 0;
-    for (int b = 0; b < p->B; ++b) {
-        row[b + 1] = row[b] + (int64_t)p->T_host[b] * (p->S_host[b] + 1);
-        col[b + 1] = col[b] + p->T_host[b];
-        for (int64_t c = col[b]; c < col[b + 1]; ++c) col_b[c] = b;
-    }
     return RNNT_STATUS_SUCCESS;
 }
 
@@ -1522,18 +1483,9 @@ RNNTStatus GpuRNNTComputer<float>::cost(float *costs) {
     return manager_compute(workspace_manager_, blank_, stream_, costs, nullptr);
 }
 
-extern "C" RNNTStatus compute_rnnt_loss(RNNTWorkspaceManager &workspace_manager, RNNTOptions options, float *costs,
+// compute_rnnt_loss (mrnnt_entry.cpp) for loc = RNNT_GPU
+RNNTStatus mrnnt::gpu_compute_rnnt_loss(RNNTWorkspaceManager &workspace_manager, RNNTOptions options, float *costs,
                                         float *gradients) {
-    // src/rnnt_entrypoint.cpp:16-48 (a manager of the wrong kind is RNNT_STATUS_INVALID_VALUE here; the
-    // reference's reference-typed dynamic_cast throws std::bad_cast across the C boundary)
-    if (costs == nullptr) return fail(RNNT_STATUS_INVALID_VALUE, "costs is null");
-    if (options.loc == RNNT_CPU) {
-        auto *cm = dynamic_cast<CpuRNNTWorkspaceManager<float> *>(&workspace_manager);
-        if (!cm) return fail(RNNT_STATUS_INVALID_VALUE, "workspace manager is not a CpuRNNTWorkspaceManager<float>");
-        CpuRNNTComputer<float> computer(*cm, options.blank_label, options.num_threads);
-        return gradients != nullptr ? computer.cost_and_grad(costs, gradients) : computer.cost(costs);
-    }
-    if (options.loc != RNNT_GPU) return fail(RNNT_STATUS_INVALID_VALUE, "unknown compute location");
     auto *gm = dynamic_cast<GpuRNNTWorkspaceManager<float> *>(&workspace_manager);
     if (!gm) return fail(RNNT_STATUS_INVALID_VALUE, "workspace manager is not a GpuRNNTWorkspaceManager<float>");
     GpuRNNTComputer<float> computer(*gm, options.blank_label, options.stream);

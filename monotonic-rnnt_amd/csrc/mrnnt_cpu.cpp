@@ -47,14 +47,16 @@ static inline __attribute__((always_inline)) float vexp(float x) {
     constexpr float kMagic = 12582912.0f;  // 1.5 * 2^23: adding it rounds to an integer in the low bits
     const float xc = std::min(std::max(x, -87.0f), 88.7f);
     const float tq = xc * 1.44269504088896341f + kMagic;
-    const int n = __builtin_bit_cast(int, tq) - __builtin_bit_cast(int, kMagic);
+    // the integer part in unsigned arithmetic: NaN input makes tq NaN and n garbage (the result is replaced below),
+    // which in signed arithmetic was an overflow / negative left shift (UBSan, `make asan`)
+    const unsigned n = __builtin_bit_cast(unsigned, tq) - __builtin_bit_cast(unsigned, kMagic);
     const float fn = tq - kMagic;
     float r = xc - fn * 0.693145751953125f;
     r = r - fn * 1.428606765330187045e-06f;
     const float p =
         1.0f + r * (1.0f + r * (0.5f + r * (0.166666672f + r * (0.0416666418f + r * (0.00833345205f +
                                                                                      r * 0.00138888808f)))));
-    float res = p * __builtin_bit_cast(float, (n + 127) << 23);
+    float res = p * __builtin_bit_cast(float, (n + 127u) << 23);
     res = (x < -87.0f) ? 0.0f : res;
     res = (x > 88.7f) ? std::numeric_limits<float>::infinity() : res;
     return (x != x) ? x : res;

@@ -412,7 +412,9 @@ __device__ __forceinline__ float max3(float a, float b, float c) {
 // on every wave (0 forward, 4 backward; -1 = unknown): the wait before chunk c leaves the later DMAs and the
 // stores of the epilogues issued after chunk c's DMA in flight (vector memory completes in issue order).
 // (Staggering the two waves of a SIMD by one epilogue, and three buffers, both measured slower: registers.)
-template <int KS, int NB, int NW, class Mma, class Epi>
+// TRACE: stamp chunk 0 into the development build's forward timeline (the forward only: the backward kernels share
+// this loop and would overwrite the same slots).
+template <int KS, int NB, int NW, bool TRACE = false, class Mma, class Epi>
 __device__ __forceinline__ void chunk_loop_with(const JointArgs &j, int V, unsigned short *wsh, int S, Mma &&mma,
                                                 Epi &&epi) {
     using WT = WTile<KS>;
@@ -431,20 +433,20 @@ __device__ __forceinline__ void chunk_loop_with(const JointArgs &j, int V, unsig
         } else {
             wait_dma();
         }
-        if (c == 0) JOINT_MARK(5);
+        if (TRACE && c == 0) JOINT_MARK(5);
         __builtin_amdgcn_s_barrier();
-        if (c == 0) JOINT_MARK(6);
+        if (TRACE && c == 0) JOINT_MARK(6);
         if (c + NB - 1 < nch) WT::template stage<NW>(j, V, c + NB - 1, wsh + ((c + NB - 1) % NB) * WT::ELEMS);
         const auto acc = mma(wsh + (c % NB) * WT::ELEMS);
-        if (c == 0) JOINT_MARK(7);
+        if (TRACE && c == 0) JOINT_MARK(7);
         epi(acc, c);
     }
 }
 
-template <int KS, int NB, int NW, int RG, class Epi>
+template <int KS, int NB, int NW, int RG, bool TRACE = false, class Epi>
 __device__ __forceinline__ void chunk_loop(const JointArgs &j, int V, unsigned short *wsh, const bf16x8 (&bfr)[KS],
                                            int lane, int S, Epi &&epi) {
-    chunk_loop_with<KS, NB, NW>(j, V, wsh, S,
+    chunk_loop_with<KS, NB, NW, TRACE>(j, V, wsh, S,
                                 [&](const unsigned short *wb) { return WTile<KS>::template mma<RG>(wb, bfr, lane); },
                                 epi);
 }
@@ -480,7 +482,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const f2 l2e = {kLog2e, kLog2e};
     float m = NEG_INF_F, sum = 0.0f, zb = 0.0f, ze = 0.0f;
     bool fb = false, fe = false;
-    chunk_loop<KS, NB, NW, RG>(j, V, wsh, bfr, lane, 0, [&](const f32x16 &acc, int c) {
+    chunk_loop<KS, NB, NW, RG, true>(j, V, wsh, bfr, lane, 0, [&](const f32x16 &acc, int c) {
         f2 z[8];
         logits2(acc, bias, c, half, z);
         float cm = fmaxf(z[0].x, z[0].y);

@@ -22,7 +22,10 @@ import threading
 import torch  # noqa: F401
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "libmonotonic_rnnt_amd.so")
+# MRNNT_LIB_PATH: load another build of the library in place of the product (the host-only sanitizer build,
+# `make -C monotonic-rnnt_amd asan`, which has the CPU entry points only; tests/test_sanitizers.py)
+HOST_ONLY_PATH = os.environ.get("MRNNT_LIB_PATH") or None
+LIB_PATH = HOST_ONLY_PATH or os.path.join(PKG_DIR, "libmonotonic_rnnt_amd.so")
 DEV_PATH = os.path.join(PKG_DIR, "libmonotonic_rnnt_amd_dev.so")
 TOOLS_PATH = os.path.join(PKG_DIR, "libmrnnt_devtools.so")
 
@@ -160,7 +163,12 @@ def _bind(path: str, dev: bool = False) -> ctypes.CDLL:
         sig["mrnnt_chase_trace"] = (i, [ctypes.POINTER(ctypes.c_ulonglong), i])
         sig["mrnnt_joint_trace"] = (i, [ctypes.POINTER(ctypes.c_ulonglong), i])
     for name, (res, args) in sig.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None and path == HOST_ONLY_PATH and not name.startswith(("mrnnt_cpu", "mrnnt_lattice", "mrnnt_last",
+                                                                          "mrnnt_version")):
+            continue  # a host-only build: the GPU entry points are absent, and a call to one fails loudly
+        if fn is None:
+            raise ImportError(f"{path} does not export {name}")
         fn.restype = res
         fn.argtypes = args
     if lib.mrnnt_version() < 9:
@@ -257,6 +265,36 @@ def tune(key: str, value: int = -1) -> int:
     if not hasattr(lib, "mrnnt_tune") or lib.mrnnt_tune.restype is not ctypes.c_int:
         raise RuntimeError("launch knobs need the development build: `with _mrnnt_lib.use(_mrnnt_lib.load_dev()):`")
     return lib.mrnnt_tune(key.encode(), int(value))
+
+
+def library_sha256(path: str = LIB_PATH) -> str:
+    """sha256 of a built library file (test logs name the product build they ran on)."""
+    import hashlib
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()
+
+
+def source_sha256() -> str:
+    """sha256 over what the product library is built from -- csrc/, include/, the Makefile (names and bytes, sorted)
+    -- and the ROCm release the build uses. The Makefile's build is path-independent (-ffile-prefix-map, fixed
+    -cuid), so equal sources and toolchain give an equal library; a PMC record keyed by this hash stays valid across a
+    rebuild in another checkout (bench.py's roofline.traffic)."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    root = os.path.dirname(PKG_DIR)
+    files = sorted(glob.glob(os.path.join(PKG_DIR, "csrc", "*")) + glob.glob(os.path.join(root, "include", "*")) +
+                   [os.path.join(PKG_DIR, "Makefile")])
+    for f in files:
+        h.update(os.path.relpath(f, root).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    rocm = "/opt/rocm/.info/version"
+    h.update(b"rocm " + (open(rocm, "rb").read().strip() if os.path.exists(rocm) else b"unknown"))
+    return h.hexdigest()
 
 
 def profile_enable(on: bool = True) -> None:

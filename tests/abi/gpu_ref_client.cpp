@@ -133,4 +133,54 @@ int client_gpu_getters(const float *acts, const int *labels, int B, const int *T
         if (p) (void)hipFree(p);
     return bad;
 }
+
+// The band members are OUTPUT-only here (include/gpu_workspace_manager.h): a client that writes
+// its own band into wm.min_allowed_s / wm.max_allowed_s before cost() gets the unrestricted result (restrict_to_
+// alignment is the way to restrict), and after the call the members hold the band of that computation ([0, S_b]).
+// Returns the number of mismatches (0 = the pinned behaviour).
+int client_band_members_output_only(const float *acts, const int *labels, int B, const int *T, const int *S, int V,
+                                    int blank) {
+    int64_t N = 0;
+    int S_max = 0, T_max = 0;
+    for (int b = 0; b < B; ++b) {
+        N += (int64_t)T[b] * (S[b] + 1);
+        S_max = std::max(S_max, S[b]);
+        T_max = std::max(T_max, T[b]);
+    }
+    float *d_acts = to_gpu(acts, (size_t)N * V);
+    int *d_labels = to_gpu(labels, (size_t)B * S_max);
+    int *d_T = to_gpu(T, (size_t)B), *d_S = to_gpu(S, (size_t)B);
+    int bad = 0;
+    hipStream_t stream;
+    (void)hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
+    std::vector<float> plain(B), written(B);
+    {
+        GpuRNNTWorkspaceManager<float> wm(d_acts, d_labels, B, d_T, d_S, V);
+        bad += wm.create_workspace() != RNNT_STATUS_SUCCESS;
+        GpuRNNTComputer<float> computer(wm, blank, stream);
+        bad += computer.cost(plain.data()) != RNNT_STATUS_SUCCESS;
+        wm.free_workspace();
+    }
+    {
+        GpuRNNTWorkspaceManager<float> wm(d_acts, d_labels, B, d_T, d_S, V);
+        bad += wm.create_workspace() != RNNT_STATUS_SUCCESS;
+        // a band of one label position per frame (min = max = 0): under the reference's computer this would leave
+        // only the path that emits nothing, and an infinite cost wherever S_b > 0
+        const std::vector<int> zero((size_t)B * T_max, 0);
+        bad += hipMemcpy(wm.min_allowed_s, zero.data(), zero.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess;
+        bad += hipMemcpy(wm.max_allowed_s, zero.data(), zero.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess;
+        GpuRNNTComputer<float> computer(wm, blank, stream);
+        bad += computer.cost(written.data()) != RNNT_STATUS_SUCCESS;
+        bad += same(plain, written);  // the write was not an input
+        std::vector<int> emx((size_t)B * T_max);
+        for (int b = 0; b < B; ++b) std::fill_n(emx.begin() + (size_t)b * T_max, T_max, S[b]);
+        bad += same(from_gpu(wm.min_allowed_s, zero.size()), zero);  // overwritten with this computation's band
+        bad += same(from_gpu(wm.max_allowed_s, emx.size()), emx);
+        wm.free_workspace();
+    }
+    (void)hipStreamDestroy(stream);
+    for (void *p : {(void *)d_acts, (void *)d_labels, (void *)d_T, (void *)d_S})
+        if (p) (void)hipFree(p);
+    return bad;
+}
 }

@@ -71,6 +71,12 @@ CASES = {
     "many_columns_b8": (8, 8, (600, 800), 6, 16, torch.float32, "packed", False),
     "steal_b80": (10, 80, (60, 90), 5, 16, torch.float32, "packed", False),  # > 64 utterances: setup kernel + stealing
     "long_labels_halo": (9, 2, (300, 320), 250, 8, torch.float32, "packed", False),
+    # 9 <= B <= 64 on shapes the chase launch does not take: the lengths planned inside the log-softmax launch with
+    # every lane of a wave holding an utterance (lane 63 = utterance 63), the headline's own kernels
+    "fused_b64_v1024": (13, 64, (90, 110), 20, 1024, torch.float32, "packed", False),
+    "fused_b64_v512": (14, 64, (60, 100), 40, 512, torch.float32, "packed", False),
+    "fused_b64_bf16_v256": (15, 64, (150, 250), 60, 256, torch.bfloat16, "packed", False),
+    "fused_b33_v1024": (16, 33, (40, 120), 30, 1024, torch.float32, "packed", False),
 }
 
 
@@ -81,12 +87,12 @@ def test_device_lengths_bit_identical_to_host_lengths(op, dev, name, separate_se
     (development build, dyn_fused = 0): the separate setup kernel for every case."""
     if separate_setup:
         with knobs(dyn_fused=0):
-            _bit_identical(op, dev, name)
+            _bit_identical(op, dev, name, True)
     else:
-        _bit_identical(op, dev, name)
+        _bit_identical(op, dev, name, False)
 
 
-def _bit_identical(op, dev, name):
+def _bit_identical(op, dev, name, separate_setup):
     seed, B, Tr, Smax, V, dt, layout, aligned = CASES[name]
     rng = np.random.default_rng(seed)
     acts, labels, T, S = random_problem(rng, B, Tr, Smax, V)
@@ -105,7 +111,18 @@ def _bit_identical(op, dev, name):
     k = 2 if aligned else 0
     scale = torch.linspace(0.5, 2.0, B, device=dev)
     c_host, g_host = _run(op, acts_t, lab, _t(T), _t(S), al, k, scale=scale)
-    c_dev, g_dev = _run(op, acts_t, lab, _t(T, dev), _t(S, dev), al, k, scale=scale)
+    if name.startswith("fused_"):
+        import _mrnnt_lib as L
+        L.profile_enable(True)
+        try:
+            c_dev, g_dev = _run(op, acts_t, lab, _t(T, dev), _t(S, dev), al, k, scale=scale)
+            prof = L.profile_read()
+        finally:
+            L.profile_enable(False)
+        assert prof["chase"][1] == 0 and prof["log_softmax"][1] == 1, prof
+        assert prof["setup"][1] == (1 if separate_setup else 0), prof
+    else:
+        c_dev, g_dev = _run(op, acts_t, lab, _t(T, dev), _t(S, dev), al, k, scale=scale)
     assert torch.equal(c_host, c_dev)
     assert torch.equal(g_host.view(torch.int16 if dt != torch.float32 else torch.int32),
                        g_dev.view(torch.int16 if dt != torch.float32 else torch.int32))

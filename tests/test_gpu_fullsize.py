@@ -21,8 +21,29 @@ pytestmark = [pytest.mark.gpu, pytest.mark.slow]
 B, T, S, V = 64, 1000, 200, 1024
 
 
+def _loss_and_grad(op, acts, labels, Tt, St):
+    acts.requires_grad_(True)
+    costs = op.monotonic_rnnt_loss(acts, labels, Tt, St, blank_label=0)
+    costs.sum().backward()
+    torch.cuda.synchronize()
+    grads = acts.grad
+    acts.grad = None
+    acts.requires_grad_(False)
+    return costs.detach(), grads
+
+
+def _equal_in_chunks(a, b, rows=1 << 20):
+    """torch.equal of two [N, V] tensors bit for bit (int32 views: -0.0 != 0.0, NaN payloads compared), chunk by chunk
+    so no full-size temporary is made."""
+    ai, bi = a.view(torch.int32), b.view(torch.int32)
+    return all(torch.equal(ai[r: r + rows], bi[r: r + rows]) for r in range(0, a.shape[0], rows))
+
+
 @pytest.fixture(scope="module")
 def headline():
+    """The headline batch run the way bench.py times it -- lengths on the device (the reference's convention,
+    monotonic_rnnt.cu:85-88), which plans the lattice inside the log-softmax launch at B = 64 (one utterance per lane of
+    every wave, lane 63 included) -- and again with host lengths; every test below reads the device-lengths result."""
     import _mrnnt_lib as L
     import monotonic_rnnt_op as op
 
@@ -35,16 +56,35 @@ def headline():
     labels = torch.from_numpy(labels_np).to(dev)
     Tt = torch.full((B,), T, dtype=torch.int32)
     St = torch.full((B,), S, dtype=torch.int32)
-    acts.requires_grad_(True)
-    costs = op.monotonic_rnnt_loss(acts, labels, Tt, St, blank_label=0)
-    costs.sum().backward()
-    torch.cuda.synchronize()
-    grads = acts.grad
-    acts.requires_grad_(False)
-    yield dict(acts=acts, grads=grads, costs=costs.detach().cpu().numpy().astype(np.float64), labels=labels_np,
-               rows_per=rows_per)
+    L.profile_enable(True)
+    try:
+        costs, grads = _loss_and_grad(op, acts, labels, Tt.to(dev), St.to(dev))
+        prof = L.profile_read()
+    finally:
+        L.profile_enable(False)
+    costs_h, grads_h = _loss_and_grad(op, acts, labels, Tt, St)
+    same = dict(costs=torch.equal(costs.view(torch.int32), costs_h.view(torch.int32)),
+                grads=_equal_in_chunks(grads, grads_h))
+    del grads_h
+    torch.cuda.empty_cache()
+    yield dict(acts=acts, grads=grads, costs=costs.cpu().numpy().astype(np.float64), labels=labels_np,
+               rows_per=rows_per, prof=prof, host_lengths_same=same, library=L.library_sha256())
     del acts, grads
     torch.cuda.empty_cache()
+
+
+def test_device_lengths_take_the_fused_planning_launch(headline):
+    """The benched convention at the benched size: no setup kernel (the lengths are planned inside the log-softmax
+    launch), one log-softmax, one recursion, one gradient pass."""
+    prof = headline["prof"]
+    print(f"library sha256 {headline['library']}")
+    assert prof["setup"][1] == 0 and prof["chase"][1] == 0, prof
+    assert prof["log_softmax"][1] == 1 and prof["alpha_beta"][1] == 1 and prof["grad"][1] == 1, prof
+
+
+def test_device_lengths_bit_identical_to_host_lengths(headline):
+    """Costs and all 13.2 G gradient elements of the device-lengths run equal the host-lengths run bit for bit."""
+    assert headline["host_lengths_same"] == dict(costs=True, grads=True), headline["host_lengths_same"]
 
 
 def test_costs_finite(headline):

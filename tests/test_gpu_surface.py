@@ -391,6 +391,17 @@ def test_bench_eight_rank_rehearsal():
     assert c2["n_gpus"] == 8 and c2["config"]["global_batch"] == 128 and c2["scaling"] == "weak"
     assert sorted(d["rank"] for d in c2["config"]["rank_devices"]) == list(range(8))
     assert {d["local_rank"] for d in c2["config"]["rank_devices"]} == set(range(8))
+    # the keys the driver compares N > 1 with N = 1 by: every rank's step time, max / min, the
+    # all-reduce's own latency; value is computed from the max over ranks
+    rk = c2["ranks"]
+    assert rk["n"] == 8 and len(rk["ms_per_step"]) == 8 and all(t > 0 for t in rk["ms_per_step"])
+    assert rk["max_ms_per_step"] == max(rk["ms_per_step"]) == c2["ms_per_step"]
+    assert rk["min_ms_per_step"] == min(rk["ms_per_step"]) and 0 < rk["balance_min_over_max"] <= 1
+    assert rk["allreduce_4byte_us"] > 0 and rk["collective"] == "gloo (rehearsal)"
+    assert rk["devices_distinct"] is False  # 8 gloo ranks share this one GPU; under RCCL bench.py requires distinct
+    assert abs(c2["value"] - 128 * 2 / (c2["ms_per_step"] * 2e-3)) <= 1e-3 * c2["value"]
+    one_c2 = _bench(["--config", "c2", "--steps", "2", "--warmup", "1", "--no-cpu"], 400)
+    assert one_c2["ranks"]["n"] == 1 and one_c2["ranks"]["allreduce_4byte_us"] is None
     one = _bench(["--config", "ragged", "--steps", "1", "--warmup", "0", "--no-cpu", "--hbm-budget-gb", "30"], 400)
     eight = _bench(["--gpus", "8", "--dist-backend", "gloo", "--config", "ragged", "--steps", "1", "--warmup", "0",
                     "--no-cpu", "--hbm-budget-gb", "8"], 600)

@@ -25,8 +25,11 @@ IDS = [os.path.basename(p)[:-4] for p in FIXTURES]
 
 
 def _build(src, out, compiler):
-    cmd = [compiler, "-O2", "-std=c++17", "-fPIC", "-shared", "-I", INC, os.path.join(ROOT, "tests", "abi", src),
-           "-L", PKG, "-lmonotonic_rnnt_amd", "-Wl,-rpath," + PKG, "-o", out]
+    lib = os.environ.get("MRNNT_LIB_PATH")  # the host-only sanitizer build (tests/test_sanitizers.py)
+    link = ([lib, "-Wl,-rpath," + os.path.dirname(lib)] + os.environ.get("MRNNT_SAN_FLAGS", "").split() if lib else
+            ["-L", PKG, "-lmonotonic_rnnt_amd", "-Wl,-rpath," + PKG])
+    cmd = [compiler, "-O2", "-std=c++17", "-fPIC", "-shared", "-I", INC, os.path.join(ROOT, "tests", "abi", src)] + \
+        link + ["-o", out]
     if compiler.endswith("hipcc"):
         cmd.insert(1, "--offload-arch=gfx950")
     subprocess.run(cmd, check=True)
@@ -149,3 +152,19 @@ def test_gpu_manager_getters_match_golden(gpu_client, path):
                 emx[b, t] = m[min(T[b], t + 1 + k)]
     np.testing.assert_array_equal(mn.reshape(B, Tm), emn)
     np.testing.assert_array_equal(mx.reshape(B, Tm), emx)
+
+
+@pytest.mark.gpu
+def test_gpu_manager_band_members_are_output_only(gpu_client):
+    """the band members are an output of the last computation, not an input (include/
+    gpu_workspace_manager.h). A band written into them before cost() is ignored -- the costs equal a
+    plain call's -- and the members hold [0, S_b] afterwards."""
+    fx = dict(np.load(next(p for p in FIXTURES if os.path.basename(p) == "multibatch.npz")))
+    lab, _ = _tight(fx)
+    acts = np.ascontiguousarray(fx["acts"], np.float32)
+    T = np.ascontiguousarray(fx["T"], np.int32)
+    S = np.ascontiguousarray(fx["S"], np.int32)
+    assert S.max() > 0
+    bad = gpu_client.client_band_members_output_only(_p(acts), _p(lab), len(T), _p(T), _p(S), acts.shape[1],
+                                                     int(fx["blank"]))
+    assert bad == 0

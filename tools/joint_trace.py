@@ -1,5 +1,7 @@
 """Timeline of the fused joint forward (development build, g_joint_trace): waves 0 and 4 of the first 4096
-workgroups at H = 512 (tools/joint_bench.py's problem)."""
+workgroups at H = 512 (tools/joint_bench.py's problem). Only the forward kernel stamps (the chunk-0 marks included:
+the backward kernels share the chunk loop but not its TRACE flag), so a read after a training step still shows the
+last forward alone."""
 import ctypes
 import json
 import sys

@@ -63,7 +63,8 @@ def main():
             "occ_skip", "col_scatter", "col_xcd", "dp_halo"} | {k for v in variants for k in v if k not in SPECIAL}
     DEFAULTS = {k: L.tune(k) for k in sorted(keys)}
     bad = [k for k, v in DEFAULTS.items() if v < 0]
-    assert not bad, f"unknown knobs {bad}"
+    if bad:  # a knob the development build does not know (e.g. a removed one) fails loudly, never silently skipped
+        raise SystemExit(f"kbench: unknown knobs {bad}")
     dev = torch.device("cuda:0")
     keep = []
     if args.fragment_gb > 0:
@@ -134,7 +135,8 @@ def main():
                     o = int(val) * 256
                     grads_holder["t"] = grads_store[o: o + rows * V].view(rows, V)
                     continue
-                assert L.tune(k, val) >= 0, k
+                if L.tune(k, val) < 0:
+                    raise SystemExit(f"kbench: unknown knob {k}")
             if "grads_offset_kb" not in v:
                 grads_holder["t"] = grads_list[gb_i][: rows * V].view(rows, V)
             L.profile_enable(True)
@@ -144,8 +146,8 @@ def main():
             c = costs.cpu().numpy()
             if ref_costs is None:
                 ref_costs = c
-            if not v.get("chase_probe"):  # (a chase probe leaves the costs unset)
-                assert np.allclose(c, ref_costs, rtol=1e-6), "variant changed the costs"
+            if not np.allclose(c, ref_costs, rtol=1e-6):
+                raise SystemExit(f"kbench: variant {v} changed the costs")
             if r == 0:
                 continue  # warm-up round
             for k in times[i]:

@@ -19,6 +19,7 @@ import argparse
 import csv
 import json
 import os
+import sys
 import shutil
 from collections import defaultdict
 
@@ -48,6 +49,12 @@ def counters(d, counter):
             if row["Counter_Name"] == counter:
                 per[row["Kernel_Name"]].append(float(row["Counter_Value"]))
     return per
+
+
+def source_sha256():
+    sys.path.insert(0, os.path.join(ROOT, "monotonic-rnnt_amd", "pytorch_binding"))
+    import _mrnnt_lib
+    return _mrnnt_lib.source_sha256()
 
 
 def lib_sha256():
@@ -119,8 +126,10 @@ def main():
         "bench_hip_event_avg_ms": {"grad": bench["kernels"]["grad"]["avg_ms"],
                                    "log_softmax": bench["kernels"]["log_softmax"]["avg_ms"]},
         "correction": "FETCH_SIZE(KiB)*1024*2 (gfx950 half-count of 16-B/lane streaming reads) + WRITE_SIZE(KiB)*1024",
-        # the library build the counters were measured on: bench.py uses this record only for that very build
+        # what the counters were measured on: bench.py uses this record for a library built from these very sources
+        # (source_sha256, path-independent build) or for this very binary (lib_sha256)
         "lib_sha256": lib_sha256(),
+        "source_sha256": source_sha256(),
         "source": f"profiles/{a.tag}/pmc_per_launch{sfx}.json (rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, "
                   f"python3 bench.py --config {a.config} --acts-dtype {a.dtype} --steps 3 --warmup 1 --no-cpu)",
     }
