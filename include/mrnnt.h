@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MRNNT_VERSION 9
+#define MRNNT_VERSION 10
 
 /* acts / grads element types */
 #define MRNNT_F32 0
@@ -231,9 +231,18 @@ RNNTStatus mrnnt_joint_backward(const mrnnt_joint_problem *p, void *workspace, i
                                 const float *grad_scale, void *G, void *Hact, int64_t *bt_idx, int64_t *bs_idx,
                                 hipStream_t stream);
 
+/* (version 10) After mrnnt_joint_backward: dpre = (G weight) * (1 - Hact^2), bf16 [n_live, H], on hand-written MFMA
+ * tiles (mrnnt_joint_gemm.hip): the dH GEMM with the tanh derivative in its epilogue. weight_t is the weight
+ * transposed, bf16 [H, V] row-major; Hact as mrnnt_joint_backward wrote it (row stride p->hact_ld, 0 = H). Needs
+ * H = 256 or 512 and V a multiple of 8 (RNNT_STATUS_INVALID_VALUE otherwise: use a library GEMM for dH and
+ * mrnnt_joint_reduce with Hact). Pass dpre to mrnnt_joint_reduce with Hact = NULL. */
+RNNTStatus mrnnt_joint_dpre(const mrnnt_joint_problem *p, int64_t n_live, const void *G, const void *weight_t,
+                            const void *Hact, void *dpre, hipStream_t stream);
+
 /* After mrnnt_joint_backward, with dH = G weight (bf16 [n_live, H], e.g. a library GEMM): accumulate
  * dpre = dH * (1 - Hact^2) into d_enc (fp32, enc's [B, enc_stride/H, H] shape; rows (b, t < T_b) are
  * overwritten) and d_pred (fp32, pred's shape; added to: zero it first). Zero d_enc's padding rows yourself.
+ * Hact = NULL (version 10): dH already holds dpre (mrnnt_joint_dpre) and is summed as it is.
  * Every sum has a fixed order (bitwise reproducible). p->reduce_scratch (version 9) lets it run on blocks of frames
  * whose d_pred sums are then added in block order; see mrnnt_joint_reduce_scratch_bytes. */
 RNNTStatus mrnnt_joint_reduce(const mrnnt_joint_problem *p, void *workspace, int64_t n_live, const void *dH,
@@ -253,7 +262,8 @@ int mrnnt_version(void);
  * enable=1 starts recording (clearing previous records). mrnnt_profile_read synchronises the
  * recorded events and returns per-kernel totals in ms and launch counts for
  *   [0] band, [1] log-softmax row reduce, [2] alpha/beta DP, [3] logit gradient, [4] setup,
- *   [5] joint forward, [6] joint backward, [7] joint reduce. */
+ *   [5] joint forward, [6] joint backward, [7] joint reduce, [8] chase launch (log-softmax + alpha/beta),
+ *   [9] joint dpre GEMM (version 10). */
 void mrnnt_profile_enable(int enable);
 int mrnnt_profile_read(double *total_ms, int64_t *launches, int n);
 

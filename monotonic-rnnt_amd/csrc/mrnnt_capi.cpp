@@ -912,8 +912,8 @@ RNNTStatus mrnnt_joint_reduce(const mrnnt_joint_problem *jp, void *ws, int64_t n
     if ((st = check_joint_pointers(jp)) != RNNT_STATUS_SUCCESS) return st;
     if (!ws || !d_enc || !d_pred) return fail(RNNT_STATUS_INVALID_VALUE, "workspace / d_enc / d_pred is null");
     if (n_live < 0 || n_live > jl.n_inband) return fail(RNNT_STATUS_INVALID_VALUE, "n_live outside [0, in-band rows]");
-    if (n_live > 0 && (!dH || !Hact || (reinterpret_cast<uintptr_t>(dH) & 7) || (reinterpret_cast<uintptr_t>(Hact) & 7)))
-        return fail(RNNT_STATUS_INVALID_VALUE, "dH / Hact null or not 8-byte aligned");
+    if (n_live > 0 && (!dH || (reinterpret_cast<uintptr_t>(dH) & 7) || (reinterpret_cast<uintptr_t>(Hact) & 7)))
+        return fail(RNNT_STATUS_INVALID_VALUE, "dH null or dH / Hact not 8-byte aligned");
     const mrnnt_problem p = base_problem(jp);
     DevProblem d = make_dev(&p, jl.base, ws);
     JointArgs j = joint_args(jp, jl, ws, n_live);
@@ -924,6 +924,30 @@ RNNTStatus mrnnt_joint_reduce(const mrnnt_joint_problem *jp, void *ws, int64_t n
                                    d_enc, d_pred, jp->reduce_scratch, jp->reduce_scratch_bytes, stream);
     });
     if (e != hipSuccess) return fail_hip(e, "joint reduce kernel");
+    return RNNT_STATUS_SUCCESS;
+}
+
+RNNTStatus mrnnt_joint_dpre(const mrnnt_joint_problem *jp, int64_t n_live, const void *G, const void *weight_t,
+                            const void *Hact, void *dpre, hipStream_t stream) {
+    JointPlan jl;
+    RNNTStatus st = make_joint_plan(jp, &jl);
+    if (st != RNNT_STATUS_SUCCESS) return st;
+    if (jp->H != 256 && jp->H != 512)
+        return fail(RNNT_STATUS_INVALID_VALUE, "mrnnt_joint_dpre: H must be 256 or 512 (use a library GEMM)");
+    if (jp->V % 8) return fail(RNNT_STATUS_INVALID_VALUE, "mrnnt_joint_dpre: V must be a multiple of 8");
+    if (n_live < 0 || n_live > jl.n_inband) return fail(RNNT_STATUS_INVALID_VALUE, "n_live outside [0, in-band rows]");
+    const int64_t ld = jp->hact_ld ? jp->hact_ld : jp->H;
+    if (ld < jp->H || ld % 4) return fail(RNNT_STATUS_INVALID_VALUE, "hact_ld must be >= H and a multiple of 4");
+    if (n_live == 0) return RNNT_STATUS_SUCCESS;
+    for (const void *q : {G, weight_t, Hact, static_cast<const void *>(dpre)})
+        if (!q || (reinterpret_cast<uintptr_t>(q) & 15))
+            return fail(RNNT_STATUS_INVALID_VALUE, "mrnnt_joint_dpre: G / weight_t / Hact / dpre null or not 16-byte aligned");
+    const hipError_t e = timed(K_JOINT_DPRE, stream, [&] {
+        return launch_joint_dpre(static_cast<const unsigned short *>(G), static_cast<const unsigned short *>(weight_t),
+                                 static_cast<const unsigned short *>(Hact), ld, static_cast<unsigned short *>(dpre),
+                                 n_live, jp->V, jp->H, stream);
+    });
+    if (e != hipSuccess) return fail_hip(e, "joint dpre kernel");
     return RNNT_STATUS_SUCCESS;
 }
 
@@ -1003,6 +1027,7 @@ __attribute__((visibility("default"))) int mrnnt_tune(const char *key, int value
     else if (!std::strcmp(key, "dp_halo")) slot = &t.dp_halo;
     else if (!std::strcmp(key, "dp_lean")) slot = &t.dp_lean;
     else if (!std::strcmp(key, "joint_reduce_sparse")) slot = &t.joint_reduce_sparse;
+    else if (!std::strcmp(key, "joint_dpre_nw")) slot = &t.joint_dpre_nw;
     else if (!std::strcmp(key, "softmax_grid_per_cu")) slot = &t.softmax_grid_per_cu;
     else if (!std::strcmp(key, "grad_grid_per_cu")) slot = &t.grad_grid_per_cu;
     else if (!std::strcmp(key, "grid_per_cu")) {  // both streaming kernels

@@ -180,8 +180,9 @@ constexpr int kRing = 16;  // lp frames in the LDS ring (1 KiB each: 16 KiB, whi
 
 struct StageLds {
     Lp ring[kRing][64];
-    int loaded;    // walk positions [0, loaded) are in the ring (the loader wave)
-    int consumed;  // walk positions [0, consumed) have been read by the recursion wave
+    int loaded;        // walk positions [0, loaded) are in the ring (the loader wave)
+    int consumed[64];  // [0]: walk positions [0, consumed) have been read by the recursion wave (every lane of it
+                       // stores its own word, so the store needs no lane-0 branch)
 };
 struct NoStage {};
 
@@ -228,7 +229,7 @@ __device__ __forceinline__ void stage_loader(const DevProblem &p, const Utt &u, 
             }
         }
         if (ready > issued) waiting = false;
-        const int room = lds_get(&st.consumed) + kRing;
+        const int room = lds_get(&st.consumed[0]) + kRing;
         const int end = min(min(ready, room), T);
         for (; issued < end; ++issued) {
             const int t = fwd ? issued : T - 1 - issued;
@@ -257,46 +258,62 @@ struct RingReader {
         asm volatile("" ::: "memory");
         return st.ring[u % kRing][threadIdx.x & 63];
     }
-    __device__ __forceinline__ void done(int u) {  // walk position u's slot may be refilled
-        if ((threadIdx.x & 63) == 0) lds_put(&st.consumed, u + 1);
+    __device__ __forceinline__ void done(int u) {  // walk positions [0, u] may be refilled (once per block of P)
+        lds_put(&st.consumed[threadIdx.x & 63], u + 1);
     }
 };
 
-// the steps of alpha_pass_halo / beta_pass_halo at NW = 1, HL = 0, lean (the same operations, so the same bits)
+// The walk's alpha / beta stores through a buffer resource over the utterance's rows: lanes past S get an offset
+// outside the resource and the hardware drops their store -- no exec-mask branch around every step's store.
+struct RowStore {
+    __amdgpu_buffer_rsrc_t rs;
+    unsigned voff;
+    __device__ __forceinline__ RowStore(double *rows, int64_t n, int lane, int W)
+        : rs(__builtin_amdgcn_make_buffer_rsrc(static_cast<void *>(rows), (short)0, (int)(n * (int64_t)sizeof(double)),
+                                               0x00020000)),
+          voff(lane < W ? (unsigned)lane * 8u : 0x80000000u) {}
+    __device__ __forceinline__ void put(double v, unsigned soff) const {
+        typedef unsigned u2 __attribute__((ext_vector_type(2)));
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), rs, voff, soff, 0);
+    }
+};
+
+// The steps of alpha_pass_halo / beta_pass_halo at NW = 1, HL = 0, lean (the same operations, so the same bits),
+// laid out for a one-wave chain: blocks of P steps with no branch inside (the ring read of each step clamps its frame
+// instead of testing it, the stores are buffer stores, consumption is published once per block).
 template <int P>
 __device__ __forceinline__ void alpha_staged(const DevProblem &p, const Utt &u, int b, float *__restrict__ costs,
                                              StageLds &st) {
     const int lane = threadIdx.x & 63;
     const int T = u.T, S = u.S, W = S + 1;
-    const bool own = lane < W;
     RingReader<P> rr(st);
     wait_vmcnt0();  // (see RingReader)
+    const RowStore out(p.alpha + u.r0, (int64_t)T * W, lane, W);
     double a = (lane == 0) ? 0.0 : NEG_INF_D;
     Lp q[P];
 #pragma unroll
     for (int d = 0; d < P; ++d) q[d] = rr.read(min(d, T - 1));
     CHASE_MARK(2);
-    double *ap = p.alpha + u.r0;
+    unsigned soff = 0;
     auto step = [&](int t, int d) {
-        double y = dpp_shr1_bc(a + q[d].e);  // alpha(t-1, s-1) + lpe(t, s-1), from lane s-1
-        if (lane == 0) y = NEG_INF_D;
+        const double y = dpp_shr1_ninf(a + q[d].e);  // alpha(t-1, s-1) + lpe(t, s-1), from lane s-1 (lane 0: -inf)
         a = lse2(a + q[d].b, y);
-        if (own) ap[lane] = a;
-        ap += W;
-        rr.done(t);
-        if (t + P < T) q[d] = rr.read(t + P);
+        out.put(a, soff);
+        soff += (unsigned)W * 8u;
+        q[d] = rr.read(min(t + P, T - 1));
     };
     int t0 = 0;
     for (; t0 + P <= T; t0 += P) {
 #pragma unroll
         for (int d = 0; d < P; ++d) step(t0 + d, d);
+        rr.done(t0 + P - 1);
     }
 #pragma unroll
     for (int d = 0; d < P; ++d) {
         if (t0 + d >= T) break;
         step(t0 + d, d);
     }
-    if (own && lane == S) {
+    if (lane == S) {
         p.ll[b] = a;
         if (costs) costs[b] = (float)(-a);
     }
@@ -306,28 +323,27 @@ template <int P>
 __device__ __forceinline__ void beta_staged(const DevProblem &p, const Utt &u, int b, StageLds &st) {
     const int lane = threadIdx.x & 63;
     const int T = u.T, S = u.S, W = S + 1;
-    const bool own = lane < W;
     RingReader<P> rr(st);
     wait_vmcnt0();  // (see RingReader)
+    const RowStore out(p.beta + u.r0, (int64_t)T * W, lane, W);
     double bn = (lane == S) ? 0.0 : NEG_INF_D;  // beta(T, s)
     Lp q[P];
 #pragma unroll
     for (int d = 0; d < P; ++d) q[d] = rr.read(min(d, T - 1));
     CHASE_MARK(2);
-    double *bp = p.beta + u.r0 + (int64_t)(T - 1) * W;
+    unsigned soff = (unsigned)(T - 1) * (unsigned)W * 8u;
     auto step = [&](int w, int d) {  // walk position w = frame T - 1 - w
-        double carry = dpp_shl1_bc(bn);
-        if (lane == 63) carry = NEG_INF_D;
+        const double carry = dpp_shl1_ninf(bn);  // beta(t+1, s+1), from lane s+1 (lane 63: -inf)
         bn = lse2(bn + q[d].b, carry + q[d].e);
-        if (own) bp[lane] = bn;
-        bp -= W;
-        rr.done(w);
-        if (w + P < T) q[d] = rr.read(w + P);
+        out.put(bn, soff);
+        soff -= (unsigned)W * 8u;
+        q[d] = rr.read(min(w + P, T - 1));
     };
     int w0 = 0;
     for (; w0 + P <= T; w0 += P) {
 #pragma unroll
         for (int d = 0; d < P; ++d) step(w0 + d, d);
+        rr.done(w0 + P - 1);
     }
 #pragma unroll
     for (int d = 0; d < P; ++d) {
@@ -383,7 +399,7 @@ __global__ __launch_bounds__(256) void chase_kernel(DevProblem p, ChaseArgs c, i
         if constexpr (STG && NW == 1) {
             if (threadIdx.x == 0) {  // (LDS holds whatever the CU's previous workgroup left)
                 st.loaded = 0;
-                st.consumed = 0;
+                st.consumed[0] = 0;
             }
             __syncthreads();
             if (wave >= 2) return;

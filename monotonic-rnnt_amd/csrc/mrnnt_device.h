@@ -27,8 +27,16 @@ __device__ __forceinline__ float fast_log2(float x) { return __builtin_amdgcn_lo
 // correction (in [0, ln 2]) uses the fp32 hardware exp2/log2 plus the classic log1p rounding correction
 // (~1e-7 absolute per step). One -inf input gives d = -inf, e = 0, r = m exactly; both -inf is the only
 // NaN case and is patched to -inf.
+__device__ __forceinline__ double max_f64(double x, double y) {
+    // v_max_f64 without the canonicalising max fmax() emits for an operand the compiler cannot prove canonical (a DPP
+    // result): the same value for every non-NaN input, one instruction fewer per recursion step
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+    return r;
+}
+
 __device__ __forceinline__ double lse2(double x, double y) {
-    const double m = fmax(x, y);
+    const double m = max_f64(x, y);
     const float d = (float)(-fabs(x - y));
     const float e = fast_exp2(d * kLog2e);
     const float u = 1.0f + e;

@@ -33,6 +33,20 @@ __device__ __forceinline__ double dpp_shl1_bc(double v) {
     return __hiloint2double(hi, lo);
 }
 
+// Shifts that bring -inf into the lane without a source (alpha: lane 0, beta: lane 63): the low word of -inf is 0
+// (bound_ctrl), its high word is the DPP move's old value -- one move per half and no select after it on the chain.
+__device__ __forceinline__ double dpp_shr1_ninf(double v) {
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x138, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_update_dpp((int)0xFFF00000u, __double2hiint(v), 0x138, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ double dpp_shl1_ninf(double v) {
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x130, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_update_dpp((int)0xFFF00000u, __double2hiint(v), 0x130, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+
 // One utterance's lattice as a recursion pass walks it: lengths and the offsets of its first row and column. The
 // recursion kernels read them from the lattice arrays; the chase launch under device-resident lengths takes them from
 // the lengths every wave holds in registers (wave_lengths), before the arrays are published.

@@ -108,6 +108,9 @@ hipError_t launch_joint_reduce(const DevProblem &p, const JointArgs &j, const in
                                size_t scratch_bytes, hipStream_t stream);
 // scratch of the blocked d_enc / d_pred reduce (per-block d_pred sums and label ranges)
 size_t joint_reduce_scratch_bytes(int B, int T_max, int S_max, int H);
+// dpre = (G W) * (1 - Hact^2) on MFMA (mrnnt_joint_gemm.hip); H in {256, 512}, V % 8 == 0
+hipError_t launch_joint_dpre(const unsigned short *G, const unsigned short *Wt, const unsigned short *Hact,
+                             int64_t hact_ld, unsigned short *dpre, int64_t n, int V, int H, hipStream_t stream);
 hipError_t launch_zero(void *ptr, size_t bytes, hipStream_t stream);
 // dbias: the fixed-order sum of the backward's per-workgroup column sums (scratch: joint_dbias_part_bytes)
 size_t joint_dbias_part_bytes(int64_t n_max, int V);
@@ -154,6 +157,9 @@ struct Tuning {
     int chase_stage = 1;          // one-wave chase recursion: lp frames staged in LDS by a loader wave (0: direct
                                   // gated loads; development build)
     int chase_delay_us = 0;       // development probe: every chase producer workgroup starts this late
+    int joint_dpre_nw = 0;        // joint dpre GEMM (mrnnt_joint_gemm.hip): 0 -> G loaded straight into registers, W^T
+                                  // through LDS (8 waves, 32 rows x 256 h each); development build: both operands
+                                  // through LDS with 8 (two per SIMD, 128 h x 64 rows each) or 4 waves (128 x 128)
     int col_xcd = 0;              // XCD-chunked column order (visit_col, col_mul < 0; overrides col_scatter): bit 0
                                   // log-softmax, bit 1 gradient
 };
@@ -182,7 +188,7 @@ inline bool nt_acts_loads(const DevProblem &p, int elem_bytes) {
 
 // Kernel-family ids for the profiling counters (mrnnt_profile_read order).
 enum KernelId { K_BAND = 0, K_SOFTMAX = 1, K_DP = 2, K_GRAD = 3, K_SETUP = 4, K_JOINT_FWD = 5, K_JOINT_BWD = 6,
-                K_JOINT_RED = 7, K_CHASE = 8, K_COUNT = 9 };
+                K_JOINT_RED = 7, K_CHASE = 8, K_JOINT_DPRE = 9, K_COUNT = 10 };
 
 // lp (may be null): zero its 64 pad entries either side of [0, n)
 hipError_t launch_setup(const int *T, const int *S, int B, int64_t *row_off, int64_t *col_off, int *col_b,

@@ -814,7 +814,8 @@ hipError_t launch_joint_dbias_sum(const JointArgs &j, int V, hipStream_t stream)
 
 constexpr int kReduceTT = 64;  // frames per workgroup (blocked form, and the sparse variant)
 
-template <int HS>
+// PRE: dH already holds dpre = dH * (1 - Hact^2) (mrnnt_joint_dpre's epilogue); Hact is not read
+template <int HS, bool PRE>
 __global__ __launch_bounds__(256) void joint_reduce_kernel(DevProblem p, JointArgs j, const int64_t *__restrict__ off,
                                                            const unsigned short *__restrict__ dH,
                                                            float *__restrict__ d_enc, float *__restrict__ d_pred,
@@ -872,10 +873,15 @@ __global__ __launch_bounds__(256) void joint_reduce_kernel(DevProblem p, JointAr
         for (int64_t r = r0 + rsub; r < r1; r += RP) {
             const int s = j.ls[r];
             const uint2 dv = *reinterpret_cast<const uint2 *>(dH + r * H + h0 + hl);
-            const uint2 hv = *reinterpret_cast<const uint2 *>(j.Hact + r * j.hact_ld + h0 + hl);
-            const float h_0 = bf16_lo(hv.x), h_1 = bf16_hi(hv.x), h_2 = bf16_lo(hv.y), h_3 = bf16_hi(hv.y);
-            const float v0 = bf16_lo(dv.x) * (1.0f - h_0 * h_0), v1 = bf16_hi(dv.x) * (1.0f - h_1 * h_1);
-            const float v2 = bf16_lo(dv.y) * (1.0f - h_2 * h_2), v3 = bf16_hi(dv.y) * (1.0f - h_3 * h_3);
+            float v0 = bf16_lo(dv.x), v1 = bf16_hi(dv.x), v2 = bf16_lo(dv.y), v3 = bf16_hi(dv.y);
+            if constexpr (!PRE) {
+                const uint2 hv = *reinterpret_cast<const uint2 *>(j.Hact + r * j.hact_ld + h0 + hl);
+                const float h_0 = bf16_lo(hv.x), h_1 = bf16_hi(hv.x), h_2 = bf16_lo(hv.y), h_3 = bf16_hi(hv.y);
+                v0 *= 1.0f - h_0 * h_0;
+                v1 *= 1.0f - h_1 * h_1;
+                v2 *= 1.0f - h_2 * h_2;
+                v3 *= 1.0f - h_3 * h_3;
+            }
             e0 += v0;
             e1 += v1;
             e2 += v2;
@@ -1008,10 +1014,12 @@ hipError_t launch_joint_reduce(const DevProblem &p, const JointArgs &j, const in
                                size_t scratch_bytes, hipStream_t stream) {
     const int ntb = (T_max + kReduceTT - 1) / kReduceTT;
     const int W = S_max + 1;
-    // the row-parallel sparse kernel with float atomics: development A/B only (joint_reduce_sparse = 2)
-    const bool sparse = kVariants && tuning().joint_reduce_sparse == 2;
+    // the row-parallel sparse kernel with float atomics: development A/B only (joint_reduce_sparse = 2; dH + Hact)
+    const bool pre = j.Hact == nullptr;  // dH holds dpre (mrnnt_joint_dpre)
+    const bool sparse = kVariants && tuning().joint_reduce_sparse == 2 && !pre;
     auto go = [&](auto hs_tag) {
         constexpr int HS = decltype(hs_tag)::value;
+        auto kern = pre ? joint_reduce_kernel<HS, true> : joint_reduce_kernel<HS, false>;
         if (sparse) {
             const size_t lds = sizeof(float) * ((size_t)W * HS + (size_t)kReduceTT * HS);
             joint_reduce_sparse_kernel<HS><<<p.B * ntb * (j.H / HS), 256, lds, stream>>>(p, j, off, dH, d_enc,
@@ -1023,13 +1031,12 @@ hipError_t launch_joint_reduce(const DevProblem &p, const JointArgs &j, const in
             // blocks of kReduceTT frames, their d_pred sums added in block order by pred_sum_kernel
             float *part = static_cast<float *>(scratch);
             int *rng = reinterpret_cast<int *>(part + (size_t)p.B * ntb * W * j.H);
-            joint_reduce_kernel<HS><<<p.B * ntb * (j.H / HS), 256, lds, stream>>>(p, j, off, dH, d_enc, d_pred,
-                                                                                  kReduceTT, ntb, W, part, rng);
+            kern<<<p.B * ntb * (j.H / HS), 256, lds, stream>>>(p, j, off, dH, d_enc, d_pred, kReduceTT, ntb, W, part,
+                                                                rng);
             pred_sum_kernel<<<dim3((unsigned)(((int64_t)W * j.H + 255) / 256), (unsigned)p.B), 256, 0, stream>>>(
                 p, part, rng, ntb, W, j.H, j.pred_sb / j.H, d_pred);
         } else {  // one block per utterance (no scratch)
-            joint_reduce_kernel<HS><<<p.B * (j.H / HS), 256, lds, stream>>>(p, j, off, dH, d_enc, d_pred, T_max, 1,
-                                                                            W, nullptr, nullptr);
+            kern<<<p.B * (j.H / HS), 256, lds, stream>>>(p, j, off, dH, d_enc, d_pred, T_max, 1, W, nullptr, nullptr);
         }
     };
     if ((int64_t)p.B * ntb * (j.H / 4) > (1ll << 24)) return hipErrorInvalidValue;  // 32-bit dispatch size

@@ -1,0 +1,345 @@
+// mrnnt_joint_gemm.hip -- the fused joint network's backward GEMMs on hand-written MFMA tiles:
+//
+//   dpre[r, h] = (sum_v G[r, v] W[v, h]) * (1 - Hact[r, h]^2)      r < n_live, h < H          (joint_dpre_kernel)
+//
+// i.e. dH = G W (the gradient of the joint activations) with the tanh derivative applied in the epilogue, so the
+// d_enc / d_pred reduce reads one [n, H] tensor instead of dH and Hact (mrnnt_joint_reduce with Hact = NULL). G is
+// the bf16 logit gradient of the live rows (mrnnt_joint_backward), W the [V, H] weight, given transposed ([H, V],
+// k = v contiguous in both operands).
+//
+// Tile: a workgroup of 4 waves (one per SIMD, 512 registers each) owns 256 rows x 256 hidden units; wave w computes
+// 128 h x 128 r as 4 x 4 v_mfma_f32_32x32x16_bf16 tiles (256 accumulator registers): A = W^T rows (h), B = G rows (r),
+// so the accumulator of a lane holds 16 hidden units of ONE row -- four runs of 4 consecutive h, one 8-byte Hact
+// load and one 8-byte dpre store each. K (= V) streams through LDS in chunks of 32 by LDS-DMA (buffer_load ... lds:
+// no staging registers), 4 stages deep, each stage one [256][32] image of G and one of W^T with the 16-byte piece p of
+// row r stored at piece p ^ ((r >> 2) & 3): the 16 lanes of each ds_read_b128 group land on 16 distinct bank quads.
+// The two h-halves of a row tile (H = 512) run as blocks b and b + 8 -- on the same XCD, dispatched together -- so
+// the second reads G from that XCD's L2.
+#include "mrnnt_device.h"
+
+namespace mrnnt {
+
+typedef __bf16 gbf16x8 __attribute__((ext_vector_type(8)));
+typedef float gf32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kGT = 256;          // rows and hidden units per workgroup tile
+constexpr int kGKC = 32;          // k per LDS stage
+constexpr int kGStages = 4;       // LDS stages (3 chunks of DMA in flight beside the MFMAs)
+constexpr int kGImage = kGT * kGKC * 2;              // bytes of one [256][32] bf16 image (16 KiB)
+constexpr int kGStageBytes = 2 * kGImage;            // G image + W^T image
+
+__device__ __forceinline__ float bf16_lo_f(unsigned u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float bf16_hi_f(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
+
+__device__ __forceinline__ int gimg_off(int r, int p) { return r * 64 + ((p ^ ((r >> 2) & 3)) << 4); }
+
+// one LDS-DMA piece: 16 bytes per lane from the buffer into LDS at dst + 16 lane (a plain __device__ function: the
+// address-space cast in a kernel template's body makes clang drop the template's host-side instantiation)
+__device__ __forceinline__ void gemm_dma(__amdgpu_buffer_rsrc_t rs, unsigned char *dst, unsigned voff, unsigned soff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)dst, 16, voff, soff, 0, 0);
+}
+
+// wait until at most N vector-memory operations of this wave are outstanding (issue order = completion order)
+template <int N>
+__device__ __forceinline__ void gemm_wait_vm() {
+    static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+// NW = 8: two waves per SIMD (256 registers each), wave w computes 128 h (w & 1) x 64 rows (w >> 1) -- one wave's
+// LDS-DMA issue and epilogue run beside the other's MFMAs; NW = 4: one wave per SIMD, 128 h x 128 rows (development
+// build). The fragments, their k order and every accumulation are the same in both: bit-identical results.
+template <int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4, NW / 4))) void joint_dpre_kernel(
+    const unsigned short *__restrict__ G, const unsigned short *__restrict__ Wt, const unsigned short *__restrict__ Hact,
+    int64_t hact_ld, unsigned short *__restrict__ dpre, int64_t n, int V, int H) {
+    constexpr int RT = 4 * 4 / NW;             // 32-row tiles per wave (4 or 2)
+    constexpr int DPI = kGImage / 1024 / NW;   // LDS-DMA wave-instructions per image per wave (4 or 2)
+    extern __shared__ __attribute__((aligned(16))) unsigned char glds[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // XCD-aware tile order: blocks are dispatched round-robin over the 8 XCDs, so b and b + 8 share an XCD
+    const int nh = H / kGT;
+    const int64_t b = blockIdx.x;
+    const int64_t xcd = b & 7, j = b >> 3;
+    const int hh = (int)(j % nh);
+    const int64_t rt = (j / nh) * 8 + xcd;
+    const int64_t r0 = rt * kGT;
+    if (r0 >= n) return;
+    const int h0 = hh * kGT;
+    const int rows = (int)min<int64_t>(kGT, n - r0);
+    // buffer resources over this tile's rows of G (rows past n read as zero) and of W^T
+    const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<unsigned short *>(G) + r0 * V, (short)0, rows * V * 2, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<unsigned short *>(Wt) + (int64_t)h0 * V, (short)0, kGT * V * 2, 0x00020000);
+    unsigned voff[DPI];
+#pragma unroll
+    for (int i = 0; i < DPI; ++i) {
+        const int row = 16 * (DPI * wave + i) + (lane >> 2);
+        const int p = (lane & 3) ^ ((row >> 2) & 3);
+        voff[i] = (unsigned)(row * V + 8 * p) * 2u;
+    }
+    const int nch = (V + kGKC - 1) / kGKC;
+    auto stage = [&](int c) {
+        unsigned char *s = glds + (c % kGStages) * kGStageBytes;
+#pragma unroll
+        for (int i = 0; i < DPI; ++i) {
+            gemm_dma(rg, s + 1024 * (DPI * wave + i), voff[i], (unsigned)(c * kGKC * 2));
+            gemm_dma(rw, s + kGImage + 1024 * (DPI * wave + i), voff[i], (unsigned)(c * kGKC * 2));
+        }
+    };
+#pragma unroll
+    for (int c = 0; c < kGStages - 1; ++c)
+        if (c < nch) stage(c);
+
+    const int wh = wave & 1, wr = wave >> 1;  // this wave: h 128 wh .. +128, rows 32 RT wr .. +32 RT of the tile
+    const int l32 = lane & 31, half = lane >> 5;
+    gf32x16 acc[4][RT];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int q = 0; q < RT; ++q)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[a][q][e] = 0.0f;
+
+    for (int c = 0; c < nch; ++c) {
+        // chunk c landed for this wave (its later chunks' DMA stays in flight), then for every wave
+        constexpr int kPer = 2 * DPI;
+        if (c + 2 < nch) gemm_wait_vm<2 * kPer>();
+        else if (c + 1 < nch) gemm_wait_vm<kPer>();
+        else gemm_wait_vm<0>();
+        __syncthreads();
+        if (c + kGStages - 1 < nch) stage(c + kGStages - 1);  // into the stage every wave finished with at c - 1
+        const unsigned char *s = glds + (c % kGStages) * kGStageBytes;
+        const unsigned char *gi = s, *wi = s + kGImage;
+        const bool tail = (c + 1) * kGKC > V;  // k past V in this chunk: those fragments are zeroed (both operands)
+#pragma unroll
+        for (int ks = 0; ks < kGKC / 16; ++ks) {
+            const int p = 2 * ks + half;
+            gbf16x8 fa[4], fb[RT];
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                fa[t] = *reinterpret_cast<const gbf16x8 *>(wi + gimg_off(128 * wh + 32 * t + l32, p));
+#pragma unroll
+            for (int t = 0; t < RT; ++t)
+                fb[t] = *reinterpret_cast<const gbf16x8 *>(gi + gimg_off(32 * RT * wr + 32 * t + l32, p));
+            if (tail && c * kGKC + 8 * p >= V) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) fa[t] = (gbf16x8){};
+#pragma unroll
+                for (int t = 0; t < RT; ++t) fb[t] = (gbf16x8){};
+            }
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int q = 0; q < RT; ++q)
+                    acc[a][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a], fb[q], acc[a][q], 0, 0, 0);
+        }
+    }
+
+    // epilogue: lane (l32, half) holds row r = r0 + 32 RT wr + 32 q + l32 and, in register 4 g + e of tile (a, q),
+    // hidden unit h = h0 + 128 wh + 32 a + 8 g + 4 half + e
+#pragma unroll
+    for (int q = 0; q < RT; ++q) {
+        const int rr = 32 * RT * wr + 32 * q + l32;
+        if (rr >= rows) continue;
+        const int64_t r = r0 + rr;
+        const unsigned short *hrow = Hact + r * hact_ld;
+        unsigned short *orow = dpre + r * H;
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int h = h0 + 128 * wh + 32 * a + 8 * g + 4 * half;
+                const uint2 hv = *reinterpret_cast<const uint2 *>(hrow + h);
+                const float h0v = bf16_lo_f(hv.x), h1v = bf16_hi_f(hv.x), h2v = bf16_lo_f(hv.y), h3v = bf16_hi_f(hv.y);
+                const float d0 = acc[a][q][4 * g] * (1.0f - h0v * h0v), d1 = acc[a][q][4 * g + 1] * (1.0f - h1v * h1v);
+                const float d2 = acc[a][q][4 * g + 2] * (1.0f - h2v * h2v), d3 = acc[a][q][4 * g + 3] * (1.0f - h3v * h3v);
+                *reinterpret_cast<uint2 *>(orow + h) = make_uint2(IoBF16::pack2(d0, d1), IoBF16::pack2(d2, d3));
+            }
+    }
+}
+
+// The default form (joint_dpre_nw = 0): only W^T goes through LDS; each wave owns 32 rows x all 256 hidden units of
+// the tile (8 x 1 tiles, 128 accumulator registers) and loads its rows of G straight into the B operand with 16-byte
+// global loads -- every G element reaches the CU once, and the LDS-DMA per MFMA is half the staged forms' (the DMA
+// issue, not the MFMA, set their pace). K runs in chunks of 64 with the k order permuted inside a chunk (step ks,
+// lane half hf, element e <-> k = 32 hf + 8 ks + e; A and B agree, so the products summed are the same): a lane's four
+// G fragments of a chunk are 64 contiguous bytes, a whole 128-byte line per row between the two lane halves.
+constexpr int kDKC = 64;                      // k per chunk
+constexpr int kDStages = 4;                   // W^T stages of [256][64] bf16 (32 KiB each)
+constexpr int kDImage = kGT * kDKC * 2;
+
+__device__ __forceinline__ int dimg_off(int r, int p) { return r * 128 + ((p ^ ((r >> 1) & 7)) << 4); }
+
+// TAILV: V is not a multiple of 64 -- fragments of k >= V are zeroed in both operands (a per-lane select in every
+// chunk); V % 64 == 0 compiles without it. The chunk loop runs in pairs so the two G register sets alternate without
+// copies, and every A-fragment read is one base address per k-step plus the tile's immediate offset (the swizzle of
+// row 32 a + l32 depends on l32 alone).
+template <bool TAILV>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void joint_dpre_direct_kernel(
+    const unsigned short *__restrict__ G, const unsigned short *__restrict__ Wt, const unsigned short *__restrict__ Hact,
+    int64_t hact_ld, unsigned short *__restrict__ dpre, int64_t n, int V, int H) {
+    constexpr int NW = 8;
+    constexpr int DPI = kDImage / 1024 / NW;  // LDS-DMA wave-instructions per W^T chunk per wave (4)
+    extern __shared__ __attribute__((aligned(16))) unsigned char glds[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nh = H / kGT;
+    const int64_t b = blockIdx.x;
+    const int64_t xcd = b & 7, j = b >> 3;
+    const int hh = (int)(j % nh);
+    const int64_t rt = (j / nh) * 8 + xcd;
+    const int64_t r0 = rt * kGT;
+    if (r0 >= n) return;
+    const int h0 = hh * kGT;
+    const int l32 = lane & 31, hf = lane >> 5;
+    // this lane's row of G: rows past n read as zero (buffer bounds); 32-bit offsets within the resource
+    const int rr = 32 * wave + l32;
+    const int rows = (int)min<int64_t>(kGT, n - r0);
+    const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<unsigned short *>(G) + r0 * V, (short)0, rows * V * 2, 0x00020000);
+    const unsigned gvoff = (unsigned)(rr * V + 32 * hf) * 2u;
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<unsigned short *>(Wt) + (int64_t)h0 * V, (short)0, kGT * V * 2, 0x00020000);
+    unsigned wvoff[DPI];
+#pragma unroll
+    for (int i = 0; i < DPI; ++i) {
+        const int row = 8 * (DPI * wave + i) + (lane >> 3);
+        const int p = (lane & 7) ^ ((row >> 1) & 7);
+        wvoff[i] = (unsigned)(row * V + 8 * p) * 2u;
+    }
+    // A fragment of tile a, k-step ks: image row 32 a + l32, piece 4 hf + ks -> aoff[ks] + 4096 a
+    int aoff[4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) aoff[ks] = l32 * 128 + (((4 * hf + ks) ^ ((l32 >> 1) & 7)) << 4);
+    const int nch = (V + kDKC - 1) / kDKC;
+    auto stage = [&](int c) {
+        unsigned char *s = glds + (c % kDStages) * kDImage;
+#pragma unroll
+        for (int i = 0; i < DPI; ++i) gemm_dma(rw, s + 1024 * (DPI * wave + i), wvoff[i], (unsigned)(c * kDKC * 2));
+    };
+    auto gload = [&](int c, gbf16x8 (&f)[4]) {
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+            f[ks] = __builtin_bit_cast(gbf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                                    rg, gvoff + 16u * ks, (unsigned)(c * kDKC * 2), 0));
+    };
+#pragma unroll
+    for (int c = 0; c < kDStages - 1; ++c)
+        if (c < nch) stage(c);
+    gbf16x8 g0[4], g1[4];
+    gload(0, g0);
+    if (1 < nch) gload(1, g1);
+    gf32x16 acc[8];
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[a][e] = 0.0f;
+
+    // one chunk: wait for its W^T and G (in-order completion: iteration i issues W^T chunk i + 3, then G chunk i + 2,
+    // so after G chunk c come W^T chunk c + 2 and G chunk c + 1, 4 ops each), barrier, refill, 32 MFMAs
+    auto chunk = [&](int c, gbf16x8 (&gc)[4]) {
+        static_assert(DPI == 4 && kDStages == 4, "the wait counts assume 4 DMA ops per chunk and 4 stages");
+        if (c == 0) {
+            if (nch > 1) gemm_wait_vm<4>();
+            else gemm_wait_vm<0>();
+        } else if (c + 2 < nch) {
+            gemm_wait_vm<8>();
+        } else if (c + 1 < nch) {
+            gemm_wait_vm<4>();
+        } else {
+            gemm_wait_vm<0>();
+        }
+        __syncthreads();
+        if (c + kDStages - 1 < nch) stage(c + kDStages - 1);
+        const unsigned char *wi = glds + (c % kDStages) * kDImage;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            gbf16x8 fb = gc[ks];
+            gbf16x8 fa[8];
+#pragma unroll
+            for (int a = 0; a < 8; ++a) fa[a] = *reinterpret_cast<const gbf16x8 *>(wi + aoff[ks] + 4096 * a);
+            if constexpr (TAILV) {
+                if (c * kDKC + 32 * hf + 8 * ks >= V) {  // k = 64 c + 32 hf + 8 ks + [0, 8)
+                    fb = (gbf16x8){};
+#pragma unroll
+                    for (int a = 0; a < 8; ++a) fa[a] = (gbf16x8){};
+                }
+            }
+#pragma unroll
+            for (int a = 0; a < 8; ++a) acc[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a], fb, acc[a], 0, 0, 0);
+        }
+    };
+    int c = 0;
+    for (; c + 1 < nch; c += 2) {
+        chunk(c, g0);
+        if (c + 2 < nch) gload(c + 2, g0);
+        chunk(c + 1, g1);
+        if (c + 3 < nch) gload(c + 3, g1);
+    }
+    if (c < nch) chunk(c, g0);
+
+    // epilogue: lane (l32, hf) holds row r0 + 32 wave + l32 and, in register 4 g + e of tile a, hidden unit
+    // h = h0 + 32 a + 8 g + 4 hf + e
+    if (rr >= rows) return;
+    const int64_t r = r0 + rr;
+    const unsigned short *hrow = Hact + r * hact_ld;
+    unsigned short *orow = dpre + r * H;
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int h = h0 + 32 * a + 8 * g + 4 * hf;
+            const uint2 hv = *reinterpret_cast<const uint2 *>(hrow + h);
+            const float h0v = bf16_lo_f(hv.x), h1v = bf16_hi_f(hv.x), h2v = bf16_lo_f(hv.y), h3v = bf16_hi_f(hv.y);
+            const float d0 = acc[a][4 * g] * (1.0f - h0v * h0v), d1 = acc[a][4 * g + 1] * (1.0f - h1v * h1v);
+            const float d2 = acc[a][4 * g + 2] * (1.0f - h2v * h2v), d3 = acc[a][4 * g + 3] * (1.0f - h3v * h3v);
+            *reinterpret_cast<uint2 *>(orow + h) = make_uint2(IoBF16::pack2(d0, d1), IoBF16::pack2(d2, d3));
+        }
+}
+
+template <int NW>
+static hipError_t launch_dpre_nw(const unsigned short *G, const unsigned short *Wt, const unsigned short *Hact,
+                                 int64_t hact_ld, unsigned short *dpre, int64_t n, int V, int H, int64_t blocks,
+                                 size_t lds, hipStream_t stream) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(joint_dpre_kernel<NW>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    joint_dpre_kernel<NW><<<(unsigned)blocks, 64 * NW, lds, stream>>>(G, Wt, Hact, hact_ld, dpre, n, V, H);
+    return hipGetLastError();
+}
+
+template <bool TAILV>
+static hipError_t launch_dpre_direct(const unsigned short *G, const unsigned short *Wt, const unsigned short *Hact,
+                                     int64_t hact_ld, unsigned short *dpre, int64_t n, int V, int H, int64_t blocks,
+                                     hipStream_t stream) {
+    const size_t lds = (size_t)kDStages * kDImage;
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(joint_dpre_direct_kernel<TAILV>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    joint_dpre_direct_kernel<TAILV><<<(unsigned)blocks, 512, lds, stream>>>(G, Wt, Hact, hact_ld, dpre, n, V, H);
+    return hipGetLastError();
+}
+
+// dpre over the live rows; H in {256, 512}, V a multiple of 8 (16-byte rows), n_live < 2^31 / (2 V) per tile of 256
+hipError_t launch_joint_dpre(const unsigned short *G, const unsigned short *Wt, const unsigned short *Hact,
+                             int64_t hact_ld, unsigned short *dpre, int64_t n, int V, int H, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    if ((H != 256 && H != 512) || V % 8 || (int64_t)kGT * V * 2 >= ((int64_t)1 << 31) || hact_ld < H)
+        return hipErrorInvalidValue;
+    const int nh = H / kGT;
+    const int64_t rtiles = (n + kGT - 1) / kGT;
+    const int64_t blocks = ((rtiles + 7) / 8) * 8 * nh;  // (row tile, h-half) pairs in XCD order; extras exit
+    if (blocks > 0x7fffffff / 512) return hipErrorInvalidValue;
+    const size_t lds = (size_t)kGStages * kGStageBytes;
+    if constexpr (kVariants) {
+        if (tuning().joint_dpre_nw == 4) return launch_dpre_nw<4>(G, Wt, Hact, hact_ld, dpre, n, V, H, blocks, lds, stream);
+        if (tuning().joint_dpre_nw == 8) return launch_dpre_nw<8>(G, Wt, Hact, hact_ld, dpre, n, V, H, blocks, lds, stream);
+    }
+    return V % kDKC ? launch_dpre_direct<true>(G, Wt, Hact, hact_ld, dpre, n, V, H, blocks, stream)
+                    : launch_dpre_direct<false>(G, Wt, Hact, hact_ld, dpre, n, V, H, blocks, stream);
+}
+
+}  // namespace mrnnt

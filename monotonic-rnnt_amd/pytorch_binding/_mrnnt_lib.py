@@ -43,7 +43,8 @@ MRNNT_BF16 = 1
 MRNNT_F16 = 2
 
 # kernel-family order of mrnnt_profile_read
-KERNELS = ("band", "log_softmax", "alpha_beta", "grad", "setup", "joint_fwd", "joint_bwd", "joint_reduce", "chase")
+KERNELS = ("band", "log_softmax", "alpha_beta", "grad", "setup", "joint_fwd", "joint_bwd", "joint_reduce", "chase",
+           "joint_dpre")
 
 
 class MrnntProblem(ctypes.Structure):
@@ -151,6 +152,7 @@ def _bind(path: str, dev: bool = False) -> ctypes.CDLL:
         "mrnnt_joint_backward": (i, [JP, vp, i64, vp, vp, vp, vp, vp, vp]),
         "mrnnt_joint_reduce": (i, [JP, vp, i64, vp, vp, vp, vp, vp]),
         "mrnnt_joint_reduce_scratch_bytes": (i, [JP, ctypes.POINTER(sz)]),
+        "mrnnt_joint_dpre": (i, [JP, i64, vp, vp, vp, vp, vp]),
         "mrnnt_last_error": (ctypes.c_char_p, []),
         "mrnnt_version": (i, []),
         "mrnnt_fill_zero": (i, [vp, sz, vp]),
@@ -171,8 +173,8 @@ def _bind(path: str, dev: bool = False) -> ctypes.CDLL:
             raise ImportError(f"{path} does not export {name}")
         fn.restype = res
         fn.argtypes = args
-    if lib.mrnnt_version() < 9:
-        raise ImportError(f"{path} is a stale build (ABI version {lib.mrnnt_version()} < 9); "
+    if lib.mrnnt_version() < 10:
+        raise ImportError(f"{path} is a stale build (ABI version {lib.mrnnt_version()} < 10); "
                           "rebuild with `make -C monotonic-rnnt_amd`")
     return lib
 

@@ -11,8 +11,9 @@ without materialising them: the HIP kernels of `mrnnt_joint.hip` form each tile 
 inside the gradient pass. Backward returns gradients for enc, pred, weight and bias: the fused kernel writes
 the logit gradient G and the activations tanh(enc + pred) of the live rows (bf16); dweight = G^T Hact (split-K
 batched GEMM, fp32 out; Hact carries a ones column when dbias is needed, so dbias = sum G comes out of the same
-GEMM) and dH = G weight are plain library GEMMs over those rows (hipBLASLt through torch), and mrnnt_joint_reduce folds dpre = dH (1 - Hact^2) into denc (sum over s) and dpred
-(sum over t) in one pass.
+GEMM) is a library GEMM over those rows (hipBLASLt through torch); dpre = (G weight) (1 - Hact^2) is one
+hand-written MFMA pass (mrnnt_joint_dpre; H = 256 / 512 -- other widths take dH from hipBLASLt and multiply in the
+reduce), and mrnnt_joint_reduce folds dpre into denc (sum over s) and dpred (sum over t) in one pass.
 
 Shapes: enc [B, T_slots >= max T, H], pred [B, S_slots >= max S + 1, H], weight [V, H] (torch.nn.Linear
 layout), bias [V] or None; H in {128, 256, 384, 512, 640}. Inputs of other floating dtypes are cast to bf16
@@ -139,9 +140,20 @@ class _JointPrepared:
             return G[:n], Hact[:n], bt[:n], bs[:n]
         return G[:n], Hact[:n]
 
+    def dpre(self, G, Hact):
+        """dpre = (G weight) * (1 - Hact^2), bf16 [n, H], on the library's hand-written MFMA tiles (mrnnt_joint_dpre)."""
+        n = G.shape[0]
+        wt = self.weight.t().contiguous()  # [H, V]: k = v contiguous, as G's rows (1 MB at H = 512, V = 1024)
+        out = torch.empty(max(1, n), self.H, dtype=torch.bfloat16, device=self.device)
+        with torch.cuda.device(self.device):
+            _L.check(_L.load().mrnnt_joint_dpre(ctypes.byref(self.problem), n, _vp(G), _vp(wt), _vp(Hact), _vp(out),
+                                                self.stream()), "mrnnt_joint_dpre")
+        return out[:n]
+
     def reduce(self, ws, dH, Hact, need_enc, need_pred, scratch=None):
-        """d_enc / d_pred (fp32) from dH = G weight over the live rows (mrnnt_joint_reduce). scratch: a dead device
-        buffer (G, once dH exists) for the blocked form; a fresh one is allocated when it is too small."""
+        """d_enc / d_pred (fp32) from dH = G weight over the live rows (mrnnt_joint_reduce); Hact None: dH is already
+        dpre (mrnnt_joint_dpre). scratch: a dead device buffer (G, once dH exists) for the blocked form; a fresh one is
+        allocated when it is too small."""
         d_enc = torch.zeros(self.enc.shape, dtype=torch.float32, device=self.device)
         d_pred = torch.zeros(self.pred.shape, dtype=torch.float32, device=self.device)
         need = ctypes.c_size_t(0)
@@ -159,6 +171,14 @@ class _JointPrepared:
 
 
 _BIAS_SUM = os.environ.get("MRNNT_JOINT_BIAS_SUM") == "1"
+# dH: a library GEMM (hipBLASLt) and the reduce's own multiply by default; MRNNT_JOINT_DH=mfma takes the library's
+# hand-written MFMA kernel with the tanh derivative fused (mrnnt_joint_dpre: H = 256 / 512, V % 8 == 0) -- opt-in
+# while it is slower than the GEMM it replaces (6.1 vs 3.8 ms at H = 512, the reduce 2.7 -> 2.1 ms)
+_DH_BLAS = os.environ.get("MRNNT_JOINT_DH", "blas") != "mfma"
+
+
+def _dpre_ok(H, V):
+    return not _DH_BLAS and H in (256, 512) and V % 8 == 0
 # dbias source per H: the 16x16x32 gradient pass sums G's columns at H = 256, 384, 512 (measured faster than the
 # ones column at 256 / 384, profiles/r03/joint/dbias/); the ones column stays at H = 128 (the pass's column sums cost
 # more there) and H = 640 (32x32x16 gradient pass). MRNNT_JOINT_DBIAS=pass / column forces one (A/B).
@@ -249,11 +269,15 @@ class MonotonicRNNTJointFunction(torch.autograd.Function):
         elif need_b and not bias_col:
             d_b = G.sum(0, dtype=torch.float32).to(ctx.bias_dtype)
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
-            # [n, H] bf16 (hipBLASLt), with W^T stored [H, V] (1 MB copy): hipBLASLt's kernel for that layout runs
-            # 3.9 vs 4.4 ms at H = 512 (profiles/r04/joint/gemm_probe.json)
-            dH = G @ prep.weight.t().contiguous().t()
+            if _dpre_ok(H, prep.V):
+                # dpre = (G W) * (1 - Hact^2) in one hand-written MFMA pass; the reduce then reads it alone
+                dH, h_in = prep.dpre(G, Hact), None
+            else:
+                # [n, H] bf16 (hipBLASLt), with W^T stored [H, V] (1 MB copy): hipBLASLt's kernel for that layout runs
+                # 3.9 vs 4.4 ms at H = 512 (profiles/r04/joint/gemm_probe.json)
+                dH, h_in = G @ prep.weight.t().contiguous().t(), Hact
             # G is dead once dH exists (dweight / dbias came first): the reduce's scratch (stream-ordered after the GEMM)
-            d_enc, d_pred = prep.reduce(ws, dH, Hact, ctx.needs_input_grad[0], ctx.needs_input_grad[1], scratch=G)
+            d_enc, d_pred = prep.reduce(ws, dH, h_in, ctx.needs_input_grad[0], ctx.needs_input_grad[1], scratch=G)
             del G
             d_enc = None if d_enc is None else d_enc.to(prep.enc.dtype)
             d_pred = None if d_pred is None else d_pred.to(prep.pred.dtype)

@@ -42,7 +42,9 @@ def c4_shard(request):
     acts = torch.empty((nrows, V), dtype=torch.float32, device=dev)
     L.synth_acts(acts.data_ptr(), r0 * V, nrows * V, 8, 1, torch.cuda.current_stream().cuda_stream)
     costs = torch.empty(hi - lo, dtype=torch.float32)
-    T, S = torch.from_numpy(Tg[lo:hi]), torch.from_numpy(Sg[lo:hi])
+    # lengths on the device, as bench.py --config ragged passes them (the reference's convention; B = 256 > 64: the
+    # setup-kernel planning with the log-softmax's work stealing)
+    T, S = torch.from_numpy(Tg[lo:hi]).to(dev), torch.from_numpy(Sg[lo:hi]).to(dev)
     lab = torch.from_numpy(np.ascontiguousarray(labels[lo:hi])).to(dev)
     assert op.monotonic_rnnt_cpp.gpu_monotonic_rnnt(acts, lab, T, S, costs, acts, 0) == 0
     torch.cuda.synchronize()
@@ -97,5 +99,7 @@ def test_config_c4_all_costs_match_oracle(c4_shard):
         del host
         worst = max(worst, float(np.max(np.abs(c[b0 - lo: b1 - lo] - cr) / np.abs(cr))))
         print(f"utterances [{b0}, {b1}): worst rel err so far {worst:.3e}", flush=True)  # progress for long runs
-    print(f"configs[3] utterances [{lo}, {hi}): costs max rel err {worst:.3e}")
+    import _mrnnt_lib as L
+    print(f"configs[3] utterances [{lo}, {hi}): costs max rel err {worst:.3e} (device lengths; library sha256 "
+          f"{L.library_sha256()})")
     assert worst <= 1e-4

@@ -34,7 +34,9 @@ def test_config_c5_whole_batch_in_place_chunks():
                      torch.cuda.current_stream().cuda_stream)
         costs = torch.empty(CHUNK, dtype=torch.float32)
         lab = torch.from_numpy(np.ascontiguousarray(labels[b0: b0 + CHUNK])).to(dev)
-        Tt, St = torch.full((CHUNK,), T, dtype=torch.int32), torch.full((CHUNK,), S, dtype=torch.int32)
+        # lengths on the device, as bench.py --config c5 passes them (planned inside the log-softmax launch)
+        Tt = torch.full((CHUNK,), T, dtype=torch.int32, device=dev)
+        St = torch.full((CHUNK,), S, dtype=torch.int32, device=dev)
         assert op.monotonic_rnnt_cpp.gpu_monotonic_rnnt(acts, lab, Tt, St, costs, acts, 0) == 0
         for a in range(0, acts.shape[0], 1 << 18):
             worst_rs = max(worst_rs, acts[a: a + (1 << 18)].sum(dim=1, dtype=torch.float64).abs().max().item())
@@ -53,5 +55,5 @@ def test_config_c5_whole_batch_in_place_chunks():
         worst_c = max(worst_c, abs(costs_all[b] - cr[0]) / abs(cr[0]))
         print(f"utterance {b}: cost {costs_all[b]:.6f} oracle {cr[0]:.6f}; worst rel err so far {worst_c:.3e}",
               flush=True)
-    print(f"configs[4] all 64 costs: max rel err {worst_c:.3e}")
+    print(f"configs[4] all 64 costs: max rel err {worst_c:.3e} (device lengths; library sha256 {L.library_sha256()})")
     assert worst_c <= 1e-4

@@ -274,3 +274,44 @@ def test_joint_tile_variants_vs_host(dev, H, V, blank, tile):
     close(db, db_r, name="d_bias")
     for b in range(len(T)):
         assert torch.all(de[b, T[b]:] == 0) and torch.all(dp[b, S[b] + 1:] == 0)
+
+
+@pytest.mark.parametrize("H,V,ld", [(512, 1024, 512), (256, 1000, 256), (512, 1000, 520), (256, 1024, 288)])
+def test_joint_dpre_kernel_vs_torch(jop, dev, H, V, ld):
+    """mrnnt_joint_dpre (hand-written MFMA GEMM, mrnnt_joint_gemm.hip) against torch on the same bf16 operands:
+    dpre = (G W) * (1 - Hact^2) over 3,000 rows (11+ row tiles, the last partial), V with and without a partial last
+    k-chunk, Hact with a wider row stride. Tolerance: the bf16 rounding of the output (2^-8 relative) plus fp32
+    accumulation-order noise, stated as |d - ref| <= 2^-7 |ref| + 1e-3 max|ref|."""
+    enc, pred, w, _, labels, T, S = make_case(7, 4, (150, 200), 60, H, V)
+    prep = jop._JointPrepared(enc.to(dev), pred.to(dev), w.to(dev), None, torch.from_numpy(labels).to(dev),
+                              torch.from_numpy(T), torch.from_numpy(S), 0)
+    n = 3000
+    g = torch.Generator(device=dev).manual_seed(H + V + ld)
+    G = (torch.randn(n, V, device=dev, generator=g) * 1e-2).to(torch.bfloat16)
+    Hw = torch.tanh(torch.randn(n, ld, device=dev, generator=g)).to(torch.bfloat16)
+    prep.problem.hact_ld = ld
+    out = prep.dpre(G, Hw)
+    torch.cuda.synchronize()
+    h = Hw[:, :H].float()
+    ref = (G.float() @ prep.weight.float()) * (1.0 - h * h)
+    err = (out.float() - ref).abs()
+    lim = 2.0 ** -7 * ref.abs() + 1e-3 * ref.abs().max()
+    assert bool((err <= lim).all()), (err.max().item(), ref.abs().max().item())
+    # bit-for-bit repeatable
+    assert torch.equal(prep.dpre(G, Hw), out)
+
+
+def test_joint_dpre_path_matches_library_gemm_path(jop, dev, monkeypatch):
+    """The backward through mrnnt_joint_dpre + the reduce on dpre equals the hipBLASLt dH + reduce-with-Hact path
+    within the bf16 rounding of dH / dpre (both against the same fp64 host reference: test above; here path vs path)."""
+    enc, pred, w, bias, labels, T, S = make_case(11, 3, (40, 70), 20, 512, 256)
+    outs = []
+    for blas in (False, True):
+        monkeypatch.setattr(jop, "_DH_BLAS", blas)
+        outs.append(run_joint(jop, dev, enc, pred, w, bias, labels, T, S, scale=[1.0, 0.5, -1.0]))
+    (c0, de0, dp0, dw0, db0), (c1, de1, dp1, dw1, db1) = outs
+    assert np.array_equal(c0, c1)
+    assert torch.equal(dw0, dw1) and torch.equal(db0, db1)  # dW / dbias do not depend on the dH path
+    for x, y, name in ((de0, de1, "d_enc"), (dp0, dp1, "d_pred")):
+        err = (x.float() - y.float()).abs().max().item()
+        assert err <= 1e-2 * y.float().abs().max().item() + 1e-6, (name, err)

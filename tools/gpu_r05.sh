@@ -1,0 +1,40 @@
+# Round-5 GPU steps, chained with && (each under its own time limit); MODE picks the set.
+#   full  : every gpu-marked test, smoke(), the default bench line, configs[1] graph bench
+#   c2    : configs[1] HIP-graph bench + rocprofv3 kernel stats of it
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/${TAG:-r05}
+mkdir -p $O
+cd $R
+case ${MODE:-full} in
+full)
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rs --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 && \
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && \
+  timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err && \
+  timeout -k 10 300 python bench.py --config c2 --graph --steps 2000 --warmup 200 > $O/bench_c2_graph.json 2> $O/bench_c2_graph.err
+  rc=$?; echo rc=$rc; tail -n 3 $O/pytest_gpu.log; cat $O/smoke.log $O/bench.json $O/bench_c2_graph.json; exit $rc ;;
+joint)
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_joint.py -x -v -rs --timeout 300 --timeout-method thread > $O/pytest_joint.log 2>&1 && \
+  timeout -k 10 300 python tools/joint_bench.py --no-unfused --steps 5 > $O/joint_h512.json 2> $O/joint_h512.err && \
+  MRNNT_JOINT_DH=mfma timeout -k 10 300 python tools/joint_bench.py --no-unfused --steps 5 > $O/joint_h512_mfma.json 2> $O/joint_h512_mfma.err
+  rc=$?; echo rc=$rc; tail -n 3 $O/pytest_joint.log; cat $O/joint_h512.json $O/joint_h512_mfma.json; exit $rc ;;
+dpre)
+  timeout -k 10 300 python tools/dpre_bench.py > $O/dpre_bench.json 2> $O/dpre_bench.err && \
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_joint.py -x -q --timeout 300 --timeout-method thread -k dpre > $O/pytest_dpre.log 2>&1
+  rc=$?; echo rc=$rc; cat $O/dpre_bench.json; tail -n 2 $O/pytest_dpre.log; exit $rc ;;
+dprepmc)
+  cd /tmp && export TMPDIR=/tmp
+  J="$R/tools/dpre_bench.py --reps 2 --variants [{\"joint_dpre_nw\":0}]"
+  timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES --output-format csv -d $O/pmc_sq -- python3 $J > $O/pmc_sq.json 2> $O/pmc_sq.err && \
+  timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_VALU_MFMA_COEXEC_CYCLES SQ_INSTS_SALU SQ_INST_CYCLES_VMEM SQ_WAVES --output-format csv -d $O/pmc_sq2 -- python3 $J > $O/pmc_sq2.json 2> $O/pmc_sq2.err && \
+  timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d $O/pmc_grbm -- python3 $J > $O/pmc_grbm.json 2> $O/pmc_grbm.err && \
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -- python3 $J > $O/pmc_fetch.json 2> $O/pmc_fetch.err && \
+  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -- python3 $J > $O/pmc_write.json 2> $O/pmc_write.err && \
+  python3 $R/tools/pmc_kernel.py $O/pmc_sq $O/pmc_sq2 $O/pmc_grbm $O/pmc_fetch $O/pmc_write --match dpre --match Cijk > $O/pmc_dpre.txt
+  rc=$?; echo rc=$rc; cat $O/pmc_dpre.txt; exit $rc ;;
+c2)
+  timeout -k 10 300 python bench.py --config c2 --graph --steps 2000 --warmup 200 > $O/bench_c2_graph.json 2> $O/bench_c2_graph.err && \
+  cd /tmp && export TMPDIR=/tmp && \
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/c2_stats -o run --output-format csv -- python3 $R/bench.py --config c2 --graph --steps 2000 --warmup 200 --no-cpu --no-lengths-ab > $O/bench_c2_graph_prof.json 2> $O/bench_c2_graph_prof.err
+  rc=$?; echo rc=$rc; cat $O/bench_c2_graph.json; exit $rc ;;
+esac

@@ -114,7 +114,9 @@ def main():
         "ms_per_step": round(dt * 1e3, 3), "utt_per_s": round(B / dt, 1),
         "forward_rows": n_band, "live_rows": n_live, "live_frac": round(n_live / n_band, 4),
         "kernels_ms": {"joint_fwd": round(ms("joint_fwd"), 3), "alpha_beta": round(ms("alpha_beta"), 3),
-                       "joint_bwd": round(ms("joint_bwd"), 3), "joint_reduce": round(ms("joint_reduce"), 3)},
+                       "joint_bwd": round(ms("joint_bwd"), 3), "joint_reduce": round(ms("joint_reduce"), 3),
+                       "joint_dpre": round(ms("joint_dpre"), 3)},
+        "joint_dpre_tflops": round(f_bwd * H / H / (ms("joint_dpre") * 1e-3) / 1e12, 1) if pr["joint_dpre"][1] else None,
         "joint_fwd_tflops": round(f_fwd / (ms("joint_fwd") * 1e-3) / 1e12, 1),
         "joint_bwd_tflops": round(f_bwd / (ms("joint_bwd") * 1e-3) / 1e12, 1),
         "peak_tflops": PEAK_TFLOPS,
