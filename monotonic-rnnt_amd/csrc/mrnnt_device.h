@@ -41,7 +41,9 @@ __device__ __forceinline__ double lse2(double x, double y) {
     const float e = fast_exp2(d * kLog2e);
     const float u = 1.0f + e;
     const float corr = ((u - 1.0f) - e) * __builtin_amdgcn_rcpf(u);
-    const float c = fast_log2(u) * kLn2 - corr;
+    // an explicit fma: left to contraction, one kernel fused log2(u) * ln2 - corr and another (whose SLP pass packed
+    // the multiply with its neighbour's) did not, and the walks' results differed in the last bits
+    const float c = fmaf(fast_log2(u), kLn2, -corr);
     const double r = m + (double)c;
     return (m == NEG_INF_D) ? NEG_INF_D : r;
 }

@@ -157,9 +157,12 @@ struct Tuning {
     int chase_stage = 1;          // one-wave chase recursion: lp frames staged in LDS by a loader wave (0: direct
                                   // gated loads; development build)
     int chase_delay_us = 0;       // development probe: every chase producer workgroup starts this late
-    int joint_dpre_nw = 0;        // joint dpre GEMM (mrnnt_joint_gemm.hip): 0 -> G loaded straight into registers, W^T
-                                  // through LDS (8 waves, 32 rows x 256 h each); development build: both operands
-                                  // through LDS with 8 (two per SIMD, 128 h x 64 rows each) or 4 waves (128 x 128)
+    int joint_reduce_hact = 1;    // joint reduce: 1 reads Hact; 0 (development build) recomputes the activation from
+                                  // enc / pred (the gradient pass's bits; measured slower, mrnnt_joint.hip)
+    int joint_dpre_nw = 0;        // joint dpre GEMM (mrnnt_joint_gemm.hip): 0 -> persistent, G loaded straight into
+                                  // registers, W^T through LDS (8 waves, 32 rows x 256 h each); development build: 1 the
+                                  // same tile one workgroup per tile; both operands through LDS with 8 (two per SIMD,
+                                  // 128 h x 64 rows each) or 4 waves (128 x 128)
     int col_xcd = 0;              // XCD-chunked column order (visit_col, col_mul < 0; overrides col_scatter): bit 0
                                   // log-softmax, bit 1 gradient
 };

@@ -814,8 +814,17 @@ hipError_t launch_joint_dbias_sum(const JointArgs &j, int V, hipStream_t stream)
 
 constexpr int kReduceTT = 64;  // frames per workgroup (blocked form, and the sparse variant)
 
-// PRE: dH already holds dpre = dH * (1 - Hact^2) (mrnnt_joint_dpre's epilogue); Hact is not read
-template <int HS, bool PRE>
+// SRC: where the tanh derivative's activation comes from.
+//   kRedHact (default): read from Hact;
+//   kRedTanh (development build, joint_reduce_hact = 0): recomputed, h = bf16(fast_tanh2(enc + pred)) exactly as the
+//     gradient pass built it (same function and operands: the stored Hact's bits, test_joint_reduce_recomputed_
+//     activation_is_bit_identical) -- enc[b, t] once per frame, the pred slice staged in LDS, so the reduce streams dH
+//     alone (4 GB at H = 512 instead of 8). Measured slower, 2.71 -> 4.26 ms: the frame loop is latency-bound, and the
+//     staged slice costs occupancy (three workgroups per CU instead of five) -- the bytes were not its limit;
+//   kRedPre: dH already holds dpre = dH * (1 - Hact^2) (mrnnt_joint_dpre's epilogue).
+constexpr int kRedTanh = 0, kRedHact = 1, kRedPre = 2;
+
+template <int HS, int SRC>
 __global__ __launch_bounds__(256) void joint_reduce_kernel(DevProblem p, JointArgs j, const int64_t *__restrict__ off,
                                                            const unsigned short *__restrict__ dH,
                                                            float *__restrict__ d_enc, float *__restrict__ d_pred,
@@ -823,7 +832,7 @@ __global__ __launch_bounds__(256) void joint_reduce_kernel(DevProblem p, JointAr
                                                            int *__restrict__ rng) {
     constexpr int TPR = HS / 4;     // threads per row slice
     constexpr int RP = 256 / TPR;   // rows in parallel
-    extern __shared__ float lds[];  // acc[(S_b+1) * HS] then red[RP][HS]
+    extern __shared__ float lds[];  // acc[(S_b+1) * HS], red[RP][HS], then (kRedTanh) pred slice [S_b+1][HS] bf16
     const int H = j.H;
     const int nh = H / HS;
     // the h-slices of one block of frames are consecutive workgroups: they read the same rows (L2 reuse)
@@ -865,18 +874,39 @@ __global__ __launch_bounds__(256) void joint_reduce_kernel(DevProblem p, JointAr
     __syncthreads();
     const int s_lo = srange[0], s_hi = srange[1];
     for (int i = s_lo * HS + tid; i < (s_hi + 1) * HS; i += 256) acc[i] = 0.0f;
+    // kRedTanh: pred[b, s, h0 .. h0 + HS) for the touched s, 8 bytes per thread and row
+    unsigned short *pl = reinterpret_cast<unsigned short *>(red + RP * HS);
+    if constexpr (SRC == kRedTanh) {
+        for (int i = s_lo * TPR + tid; i < (s_hi + 1) * TPR; i += 256) {
+            const int ss = i / TPR, hq = (i % TPR) * 4;
+            *reinterpret_cast<uint2 *>(pl + ss * HS + hq) =
+                *reinterpret_cast<const uint2 *>(j.pred + (int64_t)b * j.pred_sb + (int64_t)ss * H + h0 + hq);
+        }
+    }
     __syncthreads();
     for (int t = t0; t < t1; ++t) {
         const int64_t col = p.col_off[b] + t;
         const int64_t r0 = off[col], r1 = off[col + 1];
         float e0 = 0.0f, e1 = 0.0f, e2 = 0.0f, e3 = 0.0f;
+        uint2 ev = make_uint2(0u, 0u);
+        if constexpr (SRC == kRedTanh)
+            if (r1 > r0) ev = *reinterpret_cast<const uint2 *>(j.enc + (int64_t)b * j.enc_sb + (int64_t)t * H + h0 + hl);
         for (int64_t r = r0 + rsub; r < r1; r += RP) {
             const int s = j.ls[r];
             const uint2 dv = *reinterpret_cast<const uint2 *>(dH + r * H + h0 + hl);
             float v0 = bf16_lo(dv.x), v1 = bf16_hi(dv.x), v2 = bf16_lo(dv.y), v3 = bf16_hi(dv.y);
-            if constexpr (!PRE) {
-                const uint2 hv = *reinterpret_cast<const uint2 *>(j.Hact + r * j.hact_ld + h0 + hl);
-                const float h_0 = bf16_lo(hv.x), h_1 = bf16_hi(hv.x), h_2 = bf16_lo(hv.y), h_3 = bf16_hi(hv.y);
+            if constexpr (SRC != kRedPre) {
+                float h_0, h_1, h_2, h_3;
+                if constexpr (SRC == kRedHact) {
+                    const uint2 hv = *reinterpret_cast<const uint2 *>(j.Hact + r * j.hact_ld + h0 + hl);
+                    h_0 = bf16_lo(hv.x), h_1 = bf16_hi(hv.x), h_2 = bf16_lo(hv.y), h_3 = bf16_hi(hv.y);
+                } else {  // build_row's activation, bit for bit
+                    const uint2 pv = *reinterpret_cast<const uint2 *>(pl + s * HS + hl);
+                    const f2 ya = fast_tanh2((f2){bf16_lo(ev.x), bf16_hi(ev.x)} + (f2){bf16_lo(pv.x), bf16_hi(pv.x)});
+                    const f2 yb = fast_tanh2((f2){bf16_lo(ev.y), bf16_hi(ev.y)} + (f2){bf16_lo(pv.y), bf16_hi(pv.y)});
+                    h_0 = (float)(__bf16)ya.x, h_1 = (float)(__bf16)ya.y, h_2 = (float)(__bf16)yb.x;
+                    h_3 = (float)(__bf16)yb.y;
+                }
                 v0 *= 1.0f - h_0 * h_0;
                 v1 *= 1.0f - h_1 * h_1;
                 v2 *= 1.0f - h_2 * h_2;
@@ -1017,16 +1047,23 @@ hipError_t launch_joint_reduce(const DevProblem &p, const JointArgs &j, const in
     // the row-parallel sparse kernel with float atomics: development A/B only (joint_reduce_sparse = 2; dH + Hact)
     const bool pre = j.Hact == nullptr;  // dH holds dpre (mrnnt_joint_dpre)
     const bool sparse = kVariants && tuning().joint_reduce_sparse == 2 && !pre;
+    const bool tanh_src = kVariants && tuning().joint_reduce_hact == 0 && !pre;
     auto go = [&](auto hs_tag) {
         constexpr int HS = decltype(hs_tag)::value;
-        auto kern = pre ? joint_reduce_kernel<HS, true> : joint_reduce_kernel<HS, false>;
+        auto kern = pre ? joint_reduce_kernel<HS, kRedPre>
+                        : (tanh_src ? joint_reduce_kernel<HS, kRedTanh> : joint_reduce_kernel<HS, kRedHact>);
         if (sparse) {
             const size_t lds = sizeof(float) * ((size_t)W * HS + (size_t)kReduceTT * HS);
             joint_reduce_sparse_kernel<HS><<<p.B * ntb * (j.H / HS), 256, lds, stream>>>(p, j, off, dH, d_enc,
                                                                                           d_pred, ntb);
             return;
         }
-        const size_t lds = sizeof(float) * ((size_t)W * HS + 256 / (HS / 4) * HS);
+        // (+ the staged pred slice, bf16 [W][HS], of the recomputing form: up to 88 KiB)
+        const size_t lds = sizeof(float) * ((size_t)W * HS + 256 / (HS / 4) * HS) +
+                           (tanh_src ? sizeof(unsigned short) * W * HS : 0);
+        if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+            return;  // (the launch below then fails and reports)
         if (scratch && scratch_bytes >= joint_reduce_scratch_bytes(p.B, T_max, S_max, j.H)) {
             // blocks of kReduceTT frames, their d_pred sums added in block order by pred_sum_kernel
             float *part = static_cast<float *>(scratch);
@@ -1040,7 +1077,7 @@ hipError_t launch_joint_reduce(const DevProblem &p, const JointArgs &j, const in
         }
     };
     if ((int64_t)p.B * ntb * (j.H / 4) > (1ll << 24)) return hipErrorInvalidValue;  // 32-bit dispatch size
-    // LDS = W * HS + 4 KiB of fp32: about 30 KiB at the headline (several workgroups per CU), <= 64 KiB always
+    // LDS = W * HS fp32 + 4 KiB + W * HS bf16: about 43 KiB at the headline (three workgroups per CU), <= 88 KiB
     if (W <= 448) go(std::integral_constant<int, 32>());
     else if (W <= 896) go(std::integral_constant<int, 16>());
     else if (W <= 1792) go(std::integral_constant<int, 8>());

@@ -15,6 +15,8 @@
 // row r stored at piece p ^ ((r >> 2) & 3): the 16 lanes of each ds_read_b128 group land on 16 distinct bank quads.
 // The two h-halves of a row tile (H = 512) run as blocks b and b + 8 -- on the same XCD, dispatched together -- so
 // the second reads G from that XCD's L2.
+#include <algorithm>
+
 #include "mrnnt_device.h"
 
 namespace mrnnt {
@@ -173,6 +175,37 @@ constexpr int kDImage = kGT * kDKC * 2;
 
 __device__ __forceinline__ int dimg_off(int r, int p) { return r * 128 + ((p ^ ((r >> 1) & 7)) << 4); }
 
+// One chunk of 64 k of the direct / persistent forms: 4 k-steps x 8 MFMAs. The A fragments of k-step ks + 1 are read
+// from LDS before the MFMAs of ks are issued (two fragment sets, sched_barrier-fenced): left to itself the compiler
+// reuses two fragment registers and waits out an LDS round trip every second MFMA.
+template <bool TAILV>
+__device__ __forceinline__ void dchunk_mma(const unsigned char *wi, const int (&aoff)[4], const gbf16x8 (&gc)[4],
+                                           gf32x16 (&acc)[8], int k0, int hf, int V) {
+    gbf16x8 fa[2][8];
+#pragma unroll
+    for (int a = 0; a < 8; ++a) fa[0][a] = *reinterpret_cast<const gbf16x8 *>(wi + aoff[0] + 4096 * a);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+        if (ks + 1 < 4) {
+#pragma unroll
+            for (int a = 0; a < 8; ++a)
+                fa[(ks + 1) & 1][a] = *reinterpret_cast<const gbf16x8 *>(wi + aoff[ks + 1] + 4096 * a);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        gbf16x8 fb = gc[ks];
+        if constexpr (TAILV) {
+            if (k0 + 32 * hf + 8 * ks >= V) {  // k = k0 + 32 hf + 8 ks + [0, 8)
+                fb = (gbf16x8){};
+#pragma unroll
+                for (int a = 0; a < 8; ++a) fa[ks & 1][a] = (gbf16x8){};
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < 8; ++a) acc[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks & 1][a], fb, acc[a], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 // TAILV: V is not a multiple of 64 -- fragments of k >= V are zeroed in both operands (a per-lane select in every
 // chunk); V % 64 == 0 compiles without it. The chunk loop runs in pairs so the two G register sets alternate without
 // copies, and every A-fragment read is one base address per k-step plus the tile's immediate offset (the swizzle of
@@ -254,23 +287,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         }
         __syncthreads();
         if (c + kDStages - 1 < nch) stage(c + kDStages - 1);
-        const unsigned char *wi = glds + (c % kDStages) * kDImage;
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-            gbf16x8 fb = gc[ks];
-            gbf16x8 fa[8];
-#pragma unroll
-            for (int a = 0; a < 8; ++a) fa[a] = *reinterpret_cast<const gbf16x8 *>(wi + aoff[ks] + 4096 * a);
-            if constexpr (TAILV) {
-                if (c * kDKC + 32 * hf + 8 * ks >= V) {  // k = 64 c + 32 hf + 8 ks + [0, 8)
-                    fb = (gbf16x8){};
-#pragma unroll
-                    for (int a = 0; a < 8; ++a) fa[a] = (gbf16x8){};
-                }
-            }
-#pragma unroll
-            for (int a = 0; a < 8; ++a) acc[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a], fb, acc[a], 0, 0, 0);
-        }
+        dchunk_mma<TAILV>(glds + (c % kDStages) * kDImage, aoff, gc, acc, c * kDKC, hf, V);
     };
     int c = 0;
     for (; c + 1 < nch; c += 2) {
@@ -311,6 +328,162 @@ static hipError_t launch_dpre_nw(const unsigned short *G, const unsigned short *
     return hipGetLastError();
 }
 
+// The persistent form (default, joint_dpre_nw = 0): the direct form's tile, one workgroup per CU walking tiles
+// b, b + G, ... (G = grid size, a multiple of 8, so the XCD pairing holds), with the W^T DMA and the G loads running
+// on across tile boundaries -- the next tile's first chunks are in flight while this one's epilogue runs, and no
+// workgroup start, prologue or drained pipeline separates the tiles.
+template <bool TAILV>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void joint_dpre_persist_kernel(
+    const unsigned short *__restrict__ G, const unsigned short *__restrict__ Wt, const unsigned short *__restrict__ Hact,
+    int64_t hact_ld, unsigned short *__restrict__ dpre, int64_t n, int V, int H, int64_t slots) {
+    constexpr int NW = 8;
+    constexpr int DPI = kDImage / 1024 / NW;  // LDS-DMA wave-instructions per W^T chunk per wave (4)
+    constexpr int kEpi = 64;                  // vector-memory ops of one epilogue per wave (32 Hact loads, 32 stores)
+    extern __shared__ __attribute__((aligned(16))) unsigned char glds[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int l32 = lane & 31, hf = lane >> 5;
+    const int nh = H / kGT;
+    const int64_t rtiles = (n + kGT - 1) / kGT;
+    const int64_t gsz = gridDim.x;
+    // slot t -> (row tile, h-half): rt = 8 (t / (8 nh)) + t % 8, hh = (t / 8) % nh; only the last group of 8 row tiles
+    // can hold invalid slots, so this workgroup's valid slots are a prefix of b, b + G, ...
+    auto tile_rt = [&](int64_t t) { return ((t >> 3) / nh) * 8 + (t & 7); };
+    int ntile = 0;
+    for (int64_t t = blockIdx.x; t < slots && tile_rt(t) < rtiles; t += gsz) ++ntile;
+    if (ntile == 0) return;
+    const int nch = (V + kDKC - 1) / kDKC;
+    const int nq = ntile * nch;  // < 2^31: ntile <= slots / G, nch <= V / 64
+    struct Tile {
+        int64_t r0;
+        int h0, rows;
+    };
+    auto tile = [&](int k) {
+        const int64_t t = blockIdx.x + (int64_t)k * gsz;
+        Tile x;
+        x.r0 = tile_rt(t) * kGT;
+        x.h0 = (int)((t >> 3) % nh) * kGT;
+        x.rows = (int)min<int64_t>(kGT, n - x.r0);
+        return x;
+    };
+    const int rr = 32 * wave + l32;  // this lane's row of a tile
+    const unsigned gvoff = (unsigned)(rr * V + 32 * hf) * 2u;
+    unsigned wvoff[DPI];
+#pragma unroll
+    for (int i = 0; i < DPI; ++i) {
+        const int row = 8 * (DPI * wave + i) + (lane >> 3);
+        const int p = (lane & 7) ^ ((row >> 1) & 7);
+        wvoff[i] = (unsigned)(row * V + 8 * p) * 2u;
+    }
+    int aoff[4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) aoff[ks] = l32 * 128 + (((4 * hf + ks) ^ ((l32 >> 1) & 7)) << 4);
+    // stream positions q = k nch + c (tile k of this workgroup, chunk c)
+    auto stage = [&](int q) {
+        if (q >= nq) return;
+        const int k = q / nch, c = q - k * nch;
+        const Tile x = tile(k);
+        const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<unsigned short *>(Wt) + (int64_t)x.h0 * V, (short)0, kGT * V * 2, 0x00020000);
+        unsigned char *s = glds + (q % kDStages) * kDImage;
+#pragma unroll
+        for (int i = 0; i < DPI; ++i) gemm_dma(rw, s + 1024 * (DPI * wave + i), wvoff[i], (unsigned)(c * kDKC * 2));
+    };
+    auto gload = [&](int q, gbf16x8 (&f)[4]) {
+        if (q >= nq) return;
+        const int k = q / nch, c = q - k * nch;
+        const Tile x = tile(k);
+        const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<unsigned short *>(G) + x.r0 * V, (short)0, x.rows * V * 2, 0x00020000);
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+            f[ks] = __builtin_bit_cast(gbf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                                    rg, gvoff + 16u * ks, (unsigned)(c * kDKC * 2), 0));
+    };
+    auto is_last_full = [&](int q) {  // q ends a tile whose 256 rows are all valid (its epilogue issued kEpi ops)
+        if (q < 0) return false;
+        const int k = q / nch;
+        return q - k * nch == nch - 1 && tile(k).rows == kGT;
+    };
+#pragma unroll
+    for (int q = 0; q < kDStages - 1; ++q) stage(q);
+    gbf16x8 g0[4], g1[4];
+    gload(0, g0);
+    gload(1, g1);
+    gf32x16 acc[8];
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[a][e] = 0.0f;
+
+    // position q: wait for its W^T and G (in-order completion; after G(q), issued at the end of position q - 2, come
+    // position q - 1's W^T(q + 2), epilogue and G(q + 1): wait for the largest supported count not above that),
+    // barrier, W^T(q + 3), 32 MFMAs, the epilogue at a tile's last chunk; the caller then loads G(q + 2)
+    auto step = [&](int q, gbf16x8 (&gc)[4]) {
+        int after = 0;
+        if (q >= 1) after += (q + 2 < nq ? DPI : 0) + (q + 1 < nq ? 4 : 0) + (is_last_full(q - 1) ? kEpi : 0);
+        else after += (1 < nq ? 4 : 0);  // the prologue: G(1) after G(0)
+        if (after >= 63) gemm_wait_vm<63>();
+        else if (after >= 8) gemm_wait_vm<8>();
+        else if (after >= 4) gemm_wait_vm<4>();
+        else gemm_wait_vm<0>();
+        __syncthreads();
+        stage(q + kDStages - 1);
+        const int k = q / nch, c = q - k * nch;
+        dchunk_mma<TAILV>(glds + (q % kDStages) * kDImage, aoff, gc, acc, c * kDKC, hf, V);
+        if (c == nch - 1) {
+            const Tile x = tile(k);
+            if (rr < x.rows) {
+                const int64_t r = x.r0 + rr;
+                const unsigned short *hrow = Hact + r * hact_ld;
+                unsigned short *orow = dpre + r * H;
+#pragma unroll
+                for (int a = 0; a < 8; ++a)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const int h = x.h0 + 32 * a + 8 * g + 4 * hf;
+                        const uint2 hv = *reinterpret_cast<const uint2 *>(hrow + h);
+                        const float h0v = bf16_lo_f(hv.x), h1v = bf16_hi_f(hv.x);
+                        const float h2v = bf16_lo_f(hv.y), h3v = bf16_hi_f(hv.y);
+                        const float d0 = acc[a][4 * g] * (1.0f - h0v * h0v), d1 = acc[a][4 * g + 1] * (1.0f - h1v * h1v);
+                        const float d2 = acc[a][4 * g + 2] * (1.0f - h2v * h2v);
+                        const float d3 = acc[a][4 * g + 3] * (1.0f - h3v * h3v);
+                        *reinterpret_cast<uint2 *>(orow + h) = make_uint2(IoBF16::pack2(d0, d1), IoBF16::pack2(d2, d3));
+                    }
+            }
+#pragma unroll
+            for (int a = 0; a < 8; ++a)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) acc[a][e] = 0.0f;
+        }
+    };
+    int q = 0;
+    for (; q + 1 < nq; q += 2) {
+        step(q, g0);
+        gload(q + 2, g0);
+        step(q + 1, g1);
+        gload(q + 3, g1);
+    }
+    if (q < nq) step(q, g0);
+}
+
+template <bool TAILV>
+static hipError_t launch_dpre_persist(const unsigned short *G, const unsigned short *Wt, const unsigned short *Hact,
+                                      int64_t hact_ld, unsigned short *dpre, int64_t n, int V, int H, int64_t slots,
+                                      hipStream_t stream) {
+    const size_t lds = (size_t)kDStages * kDImage;
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(joint_dpre_persist_kernel<TAILV>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || cus <= 0)
+        cus = 256;
+    const int64_t grid = std::min<int64_t>(slots, (int64_t)(cus + 7) / 8 * 8);  // a multiple of 8: the XCD pairing
+    joint_dpre_persist_kernel<TAILV><<<(unsigned)grid, 512, lds, stream>>>(G, Wt, Hact, hact_ld, dpre, n, V, H, slots);
+    return hipGetLastError();
+}
+
 template <bool TAILV>
 static hipError_t launch_dpre_direct(const unsigned short *G, const unsigned short *Wt, const unsigned short *Hact,
                                      int64_t hact_ld, unsigned short *dpre, int64_t n, int V, int H, int64_t blocks,
@@ -338,8 +511,13 @@ hipError_t launch_joint_dpre(const unsigned short *G, const unsigned short *Wt, 
         if (tuning().joint_dpre_nw == 4) return launch_dpre_nw<4>(G, Wt, Hact, hact_ld, dpre, n, V, H, blocks, lds, stream);
         if (tuning().joint_dpre_nw == 8) return launch_dpre_nw<8>(G, Wt, Hact, hact_ld, dpre, n, V, H, blocks, lds, stream);
     }
-    return V % kDKC ? launch_dpre_direct<true>(G, Wt, Hact, hact_ld, dpre, n, V, H, blocks, stream)
-                    : launch_dpre_direct<false>(G, Wt, Hact, hact_ld, dpre, n, V, H, blocks, stream);
+    if constexpr (kVariants) {
+        if (tuning().joint_dpre_nw == 1)
+            return V % kDKC ? launch_dpre_direct<true>(G, Wt, Hact, hact_ld, dpre, n, V, H, blocks, stream)
+                            : launch_dpre_direct<false>(G, Wt, Hact, hact_ld, dpre, n, V, H, blocks, stream);
+    }
+    return V % kDKC ? launch_dpre_persist<true>(G, Wt, Hact, hact_ld, dpre, n, V, H, blocks, stream)
+                    : launch_dpre_persist<false>(G, Wt, Hact, hact_ld, dpre, n, V, H, blocks, stream);
 }
 
 }  // namespace mrnnt

@@ -315,3 +315,15 @@ def test_joint_dpre_path_matches_library_gemm_path(jop, dev, monkeypatch):
     for x, y, name in ((de0, de1, "d_enc"), (dp0, dp1, "d_pred")):
         err = (x.float() - y.float()).abs().max().item()
         assert err <= 1e-2 * y.float().abs().max().item() + 1e-6, (name, err)
+
+
+@pytest.mark.parametrize("H,V", [(512, 256), (256, 1000), (128, 64), (640, 130)])
+def test_joint_reduce_recomputed_activation_is_bit_identical(jop, dev, H, V):
+    """The reduce recomputes tanh(enc + pred) with the gradient pass's own function instead of reading Hact (halving
+    its bytes): d_enc / d_pred equal the Hact-reading form (development build, joint_reduce_hact = 1) bit for bit."""
+    enc, pred, w, bias, labels, T, S = make_case(H + 3 * V, 3, (30, 60), 20, H, V)
+    with knobs(joint_reduce_hact=0):
+        _, de0, dp0, dw0, _ = run_joint(jop, dev, enc, pred, w, bias, labels, T, S)
+    with knobs(joint_reduce_hact=1):
+        _, de1, dp1, dw1, _ = run_joint(jop, dev, enc, pred, w, bias, labels, T, S)
+    assert torch.equal(de0, de1) and torch.equal(dp0, dp1) and torch.equal(dw0, dw1)

@@ -32,6 +32,9 @@ dprepmc)
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -- python3 $J > $O/pmc_write.json 2> $O/pmc_write.err && \
   python3 $R/tools/pmc_kernel.py $O/pmc_sq $O/pmc_sq2 $O/pmc_grbm $O/pmc_fetch $O/pmc_write --match dpre --match Cijk > $O/pmc_dpre.txt
   rc=$?; echo rc=$rc; cat $O/pmc_dpre.txt; exit $rc ;;
+dbg)
+  timeout -k 10 300 python tools/debug/chase_state_diff.py > $O/chase_state_diff.txt 2>&1
+  rc=$?; echo rc=$rc; cat $O/chase_state_diff.txt | tail -40; exit $rc ;;
 c2)
   timeout -k 10 300 python bench.py --config c2 --graph --steps 2000 --warmup 200 > $O/bench_c2_graph.json 2> $O/bench_c2_graph.err && \
   cd /tmp && export TMPDIR=/tmp && \
