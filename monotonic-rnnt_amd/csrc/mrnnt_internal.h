@@ -96,6 +96,8 @@ struct JointArgs {
     float *dbias;                // [V] fp32: the backward adds sum_i G[i] into it (16x16x32 backward only), or nullptr
     float *dbias_part;           // with dbias: the backward's per-workgroup column sums, then the segment sums
                                  // (joint_dbias_part_bytes), summed in order by launch_joint_dbias_sum
+    int probe;                   // development build, forward timing probe (results wrong): bit 0 every row's
+                                 // activation reads pred row s = 0, bit 1 enc row t = 0 (0 otherwise)
 };
 
 // Row lists over the lattice: mode 0 = every in-band row, mode 1 = live rows (needs alpha/beta/ll).
@@ -159,6 +161,7 @@ struct Tuning {
     int chase_delay_us = 0;       // development probe: every chase producer workgroup starts this late
     int joint_reduce_hact = 1;    // joint reduce: 1 reads Hact; 0 (development build) recomputes the activation from
                                   // enc / pred (the gradient pass's bits; measured slower, mrnnt_joint.hip)
+    int joint_probe = 0;          // development probe: JointArgs::probe of the joint forward (results wrong)
     int joint_dpre_nw = 0;        // joint dpre GEMM (mrnnt_joint_gemm.hip): 0 -> persistent, G loaded straight into
                                   // registers, W^T through LDS (8 waves, 32 rows x 256 h each); development build: 1 the
                                   // same tile one workgroup per tile; both operands through LDS with 8 (two per SIMD,

@@ -220,8 +220,9 @@ template <int NK, int KSTEP, bool STORE>
 __device__ __forceinline__ void build_row(const JointArgs &j, const RowPos &q, int k0, int64_t i, bf16x8 *bfr) {
     constexpr int H = NK * KSTEP;
     const bool v = q.valid;
-    const unsigned short *er = j.enc + (v ? (int64_t)q.b * j.enc_sb + (int64_t)q.t * H : 0) + k0;
-    const unsigned short *pr = j.pred + (v ? (int64_t)q.b * j.pred_sb + (int64_t)q.s * H : 0) + k0;
+    const int t_ld = (kVariants && (j.probe & 2)) ? 0 : q.t, s_ld = (kVariants && (j.probe & 1)) ? 0 : q.s;
+    const unsigned short *er = j.enc + (v ? (int64_t)q.b * j.enc_sb + (int64_t)t_ld * H : 0) + k0;
+    const unsigned short *pr = j.pred + (v ? (int64_t)q.b * j.pred_sb + (int64_t)s_ld * H : 0) + k0;
     const float keep = v ? 1.0f : 0.0f;
 #pragma unroll
     for (int ks = 0; ks < NK; ++ks) {
@@ -1155,6 +1156,11 @@ static hipError_t launch_joint(const DevProblem &p, const JointArgs &j, bool bwd
 }
 
 hipError_t launch_joint_forward(const DevProblem &p, const JointArgs &j, hipStream_t stream) {
+    if (kVariants && tuning().joint_probe) {
+        JointArgs jp = j;
+        jp.probe = tuning().joint_probe;
+        return launch_joint(p, jp, false, stream);
+    }
     return launch_joint(p, j, false, stream);
 }
 

@@ -18,6 +18,21 @@ joint)
   timeout -k 10 300 python tools/joint_bench.py --no-unfused --steps 5 > $O/joint_h512.json 2> $O/joint_h512.err && \
   MRNNT_JOINT_DH=mfma timeout -k 10 300 python tools/joint_bench.py --no-unfused --steps 5 > $O/joint_h512_mfma.json 2> $O/joint_h512_mfma.err
   rc=$?; echo rc=$rc; tail -n 3 $O/pytest_joint.log; cat $O/joint_h512.json $O/joint_h512_mfma.json; exit $rc ;;
+reduce)
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_joint.py -x -v -rs --timeout 300 --timeout-method thread > $O/pytest_joint.log 2>&1 && \
+  timeout -k 10 300 python tools/joint_bench.py --no-unfused --steps 5 > $O/joint_h512.json 2> $O/joint_h512.err && \
+  timeout -k 10 300 python tools/joint_bench.py --no-unfused --steps 5 --tune joint_reduce_pf=1 > $O/joint_h512_pf1.json 2> $O/joint_h512_pf1.err
+  rc=$?; echo rc=$rc; tail -n 3 $O/pytest_joint.log; cat $O/joint_h512.json $O/joint_h512_pf1.json; exit $rc ;;
+redab)
+  [ -n "$AB" ] || AB='[{"joint_reduce_pf":1},{"joint_reduce_pf":4},{"joint_reduce_pf":4,"joint_reduce_xcd":1},{"joint_reduce_pf":1,"joint_reduce_xcd":1}]'
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_joint.py -x -q --timeout 300 --timeout-method thread > $O/pytest_joint.log 2>&1 && \
+  timeout -k 10 400 python tools/joint_bench.py --no-unfused --steps 3 --ab "$AB" > $O/joint_ab.json 2> $O/joint_ab.err && \
+  cd /tmp && export TMPDIR=/tmp && \
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_red_fetch -- python3 $R/tools/joint_bench.py --no-unfused --steps 1 --warmup 1 --tune joint_reduce_xcd=0 > $O/pmc_red_fetch.json 2> $O/pmc_red_fetch.err && \
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_red_fetch_xcd -- python3 $R/tools/joint_bench.py --no-unfused --steps 1 --warmup 1 --tune joint_reduce_xcd=1 > $O/pmc_red_fetch_xcd.json 2> $O/pmc_red_fetch_xcd.err && \
+  python3 $R/tools/pmc_kernel.py $O/pmc_red_fetch --match reduce --match joint_fwd > $O/pmc_red_fetch.txt && \
+  python3 $R/tools/pmc_kernel.py $O/pmc_red_fetch_xcd --match reduce --match joint_fwd > $O/pmc_red_fetch_xcd.txt
+  rc=$?; echo rc=$rc; tail -n 2 $O/pytest_joint.log; cat $O/joint_ab.json; cat $O/pmc_red_fetch.txt $O/pmc_red_fetch_xcd.txt; exit $rc ;;
 dpre)
   timeout -k 10 300 python tools/dpre_bench.py > $O/dpre_bench.json 2> $O/dpre_bench.err && \
   timeout -k 10 300 python -u -m pytest tests/test_gpu_joint.py -x -q --timeout 300 --timeout-method thread -k dpre > $O/pytest_dpre.log 2>&1
@@ -35,6 +50,9 @@ dprepmc)
 dbg)
   timeout -k 10 300 python tools/debug/chase_state_diff.py > $O/chase_state_diff.txt 2>&1
   rc=$?; echo rc=$rc; cat $O/chase_state_diff.txt | tail -40; exit $rc ;;
+ctrace)
+  timeout -k 10 300 python tools/chase_trace.py $O/chase_trace.json > $O/chase_trace.txt 2>&1
+  rc=$?; echo rc=$rc; cat $O/chase_trace.txt | tail -5; exit $rc ;;
 c2)
   timeout -k 10 300 python bench.py --config c2 --graph --steps 2000 --warmup 200 > $O/bench_c2_graph.json 2> $O/bench_c2_graph.err && \
   cd /tmp && export TMPDIR=/tmp && \

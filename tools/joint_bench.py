@@ -37,12 +37,16 @@ def main():
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE")
     ap.add_argument("--align-k", type=int, default=None,
                     help="alignment-restricted loss (max_distance_from_alignment = K) on bench.py's synthetic alignment")
+    ap.add_argument("--ab", default=None, metavar="JSON",
+                    help="list of knob dicts: after the main line, interleaved rounds of one fused step per variant "
+                         "(per-kernel library timings, median over --ab-rounds)")
+    ap.add_argument("--ab-rounds", type=int, default=7)
     a = ap.parse_args()
     import _mrnnt_lib as L
     import monotonic_rnnt_joint as J
     import monotonic_rnnt_op as op
 
-    if a.tune:
+    if a.tune or a.ab:
         L.select_dev()  # launch knobs live in the development build
     for kv in a.tune:
         k, v = kv.split("=")
@@ -131,6 +135,29 @@ def main():
         out["speedup"] = round(dt_u / dt, 3)
         out["max_rel_cost_diff"] = float(((c_f.double() - c_u.double()).abs() / c_u.double().abs().clamp(min=1))
                                          .max().item())
+    if a.ab:
+        variants = json.loads(a.ab)
+        saved = [{k: L.tune(k) for k in v} for v in variants]
+        runs = [dict() for _ in variants]
+        for r in range(a.ab_rounds):
+            for vi, v in enumerate(variants):
+                for k, x in v.items():
+                    assert L.tune(k, int(x)) >= 0, k
+                fused()
+                torch.cuda.synchronize()
+                L.profile_enable(True)
+                fused()
+                torch.cuda.synchronize()
+                pr = L.profile_read()
+                L.profile_enable(False)
+                for k in ("joint_fwd", "joint_bwd", "joint_reduce", "joint_dpre"):
+                    if pr[k][1]:
+                        runs[vi].setdefault(k, []).append(pr[k][0] / pr[k][1])
+                for k, x in saved[vi].items():
+                    L.tune(k, x)
+        out["ab"] = [{"knobs": v, "median_ms": {k: round(float(np.median(x)), 4) for k, x in runs[vi].items()},
+                      "min_ms": {k: round(float(np.min(x)), 4) for k, x in runs[vi].items()}}
+                     for vi, v in enumerate(variants)]
     print(json.dumps(out), flush=True)
 
 
