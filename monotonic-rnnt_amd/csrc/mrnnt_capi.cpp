@@ -498,6 +498,7 @@ RNNTStatus mrnnt_forward(const mrnnt_problem *p, void *ws, size_t ws_bytes, floa
         ca.budget = (uint32_t)std::min<int64_t>((int64_t)std::max(0, tuning().chase_wait_us) * 100, UINT32_MAX / 2);
         ca.delay = kVariants ? (uint32_t)std::max(0, tuning().chase_delay_us) * 100u : 0u;
         ca.stage = kVariants ? tuning().chase_stage : 1;
+        ca.probe = kVariants ? tuning().chase_probe : 0;
         const int nrec = with_beta ? 2 * pl.B : pl.B;
         const int producers = (int)std::min<int64_t>(streaming_grid(slot_bound, tuning().chase_grid_per_cu),
                                                      ((int64_t)1 << 22) - nrec);
@@ -1043,6 +1044,7 @@ __attribute__((visibility("default"))) int mrnnt_tune(const char *key, int value
     else if (!std::strcmp(key, "chase_wait_us")) slot = &t.chase_wait_us;
     else if (!std::strcmp(key, "chase_stage")) slot = &t.chase_stage;
     else if (!std::strcmp(key, "chase_delay_us")) slot = &t.chase_delay_us;
+    else if (!std::strcmp(key, "chase_probe")) slot = &t.chase_probe;
     else if (!std::strcmp(key, "chase_grid_per_cu")) slot = &t.chase_grid_per_cu;
     else if (!std::strcmp(key, "nt_load")) slot = &t.nt_load;
     else if (!std::strcmp(key, "occ_skip")) slot = &t.occ_skip;

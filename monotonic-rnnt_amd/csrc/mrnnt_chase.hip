@@ -283,7 +283,7 @@ struct RowStore {
 // instead of testing it, the stores are buffer stores, consumption is published once per block).
 template <int P>
 __device__ __forceinline__ void alpha_staged(const DevProblem &p, const Utt &u, int b, float *__restrict__ costs,
-                                             StageLds &st) {
+                                             StageLds &st, int probe = 0) {
     const int lane = threadIdx.x & 63;
     const int T = u.T, S = u.S, W = S + 1;
     RingReader<P> rr(st);
@@ -297,10 +297,13 @@ __device__ __forceinline__ void alpha_staged(const DevProblem &p, const Utt &u, 
     unsigned soff = 0;
     auto step = [&](int t, int d) {
         const double y = dpp_shr1_ninf(a + q[d].e);  // alpha(t-1, s-1) + lpe(t, s-1), from lane s-1 (lane 0: -inf)
-        a = lse2(a + q[d].b, y);
-        out.put(a, soff);
+        if (kVariants && (probe & 2))
+            a = max_f64(a + q[d].b, y);
+        else
+            a = lse2(a + q[d].b, y);
+        if (!kVariants || !(probe & 1)) out.put(a, soff);
         soff += (unsigned)W * 8u;
-        q[d] = rr.read(min(t + P, T - 1));
+        if (!kVariants || !(probe & 4)) q[d] = rr.read(min(t + P, T - 1));
     };
     int t0 = 0;
     for (; t0 + P <= T; t0 += P) {
@@ -320,7 +323,7 @@ __device__ __forceinline__ void alpha_staged(const DevProblem &p, const Utt &u, 
 }
 
 template <int P>
-__device__ __forceinline__ void beta_staged(const DevProblem &p, const Utt &u, int b, StageLds &st) {
+__device__ __forceinline__ void beta_staged(const DevProblem &p, const Utt &u, int b, StageLds &st, int probe = 0) {
     const int lane = threadIdx.x & 63;
     const int T = u.T, S = u.S, W = S + 1;
     RingReader<P> rr(st);
@@ -334,10 +337,13 @@ __device__ __forceinline__ void beta_staged(const DevProblem &p, const Utt &u, i
     unsigned soff = (unsigned)(T - 1) * (unsigned)W * 8u;
     auto step = [&](int w, int d) {  // walk position w = frame T - 1 - w
         const double carry = dpp_shl1_ninf(bn);  // beta(t+1, s+1), from lane s+1 (lane 63: -inf)
-        bn = lse2(bn + q[d].b, carry + q[d].e);
-        out.put(bn, soff);
+        if (kVariants && (probe & 2))
+            bn = max_f64(bn + q[d].b, carry + q[d].e);
+        else
+            bn = lse2(bn + q[d].b, carry + q[d].e);
+        if (!kVariants || !(probe & 1)) out.put(bn, soff);
         soff -= (unsigned)W * 8u;
-        q[d] = rr.read(min(w + P, T - 1));
+        if (!kVariants || !(probe & 4)) q[d] = rr.read(min(w + P, T - 1));
     };
     int w0 = 0;
     for (; w0 + P <= T; w0 += P) {
@@ -409,9 +415,9 @@ __global__ __launch_bounds__(256) void chase_kernel(DevProblem p, ChaseArgs c, i
                 return;
             }
             if (bwd)
-                beta_staged<4>(p, u, b, st);
+                beta_staged<4>(p, u, b, st, kVariants ? c.probe : 0);
             else
-                alpha_staged<4>(p, u, b, costs, st);
+                alpha_staged<4>(p, u, b, costs, st, kVariants ? c.probe : 0);
             CHASE_MARK(3);
             return;
         }

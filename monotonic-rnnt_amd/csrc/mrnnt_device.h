@@ -24,9 +24,10 @@ __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_ex
 __device__ __forceinline__ float fast_log2(float x) { return __builtin_amdgcn_logf(x); }   // v_log_f32
 
 // log(e^x + e^y) with fp64 state (rnnt_helper.h:16-30 semantics): m + log1p(exp(-|x - y|)). The bounded
-// correction (in [0, ln 2]) uses the fp32 hardware exp2/log2 plus the classic log1p rounding correction
-// (~1e-7 absolute per step). One -inf input gives d = -inf, e = 0, r = m exactly; both -inf is the only
-// NaN case and is patched to -inf.
+// correction (in [0, ln 2]) is log2(1 + e) * ln 2 on the fp32 hardware exp2/log2: <= ~1e-7 absolute per step (the
+// rounding of 1 + e to fp32, 6e-8, plus v_log_f32's). The classic log1p rounding fix (((u - 1) - e) / u) halved that
+// but put three more dependent operations on the one-wave recursion's chain. One -inf input gives
+// d = -inf, e = 0, r = m exactly; both -inf is the only NaN case and is patched to -inf.
 __device__ __forceinline__ double max_f64(double x, double y) {
     // v_max_f64 without the canonicalising max fmax() emits for an operand the compiler cannot prove canonical (a DPP
     // result): the same value for every non-NaN input, one instruction fewer per recursion step
@@ -39,11 +40,7 @@ __device__ __forceinline__ double lse2(double x, double y) {
     const double m = max_f64(x, y);
     const float d = (float)(-fabs(x - y));
     const float e = fast_exp2(d * kLog2e);
-    const float u = 1.0f + e;
-    const float corr = ((u - 1.0f) - e) * __builtin_amdgcn_rcpf(u);
-    // an explicit fma: left to contraction, one kernel fused log2(u) * ln2 - corr and another (whose SLP pass packed
-    // the multiply with its neighbour's) did not, and the walks' results differed in the last bits
-    const float c = fmaf(fast_log2(u), kLn2, -corr);
+    const float c = fast_log2(1.0f + e) * kLn2;
     const double r = m + (double)c;
     return (m == NEG_INF_D) ? NEG_INF_D : r;
 }

@@ -159,6 +159,7 @@ struct Tuning {
     int chase_stage = 1;          // one-wave chase recursion: lp frames staged in LDS by a loader wave (0: direct
                                   // gated loads; development build)
     int chase_delay_us = 0;       // development probe: every chase producer workgroup starts this late
+    int chase_probe = 0;          // development probe: ChaseArgs::probe (the staged walk's step cost; results wrong)
     int joint_reduce_hact = 1;    // joint reduce: 1 reads Hact; 0 (development build) recomputes the activation from
                                   // enc / pred (the gradient pass's bits; measured slower, mrnnt_joint.hip)
     int joint_probe = 0;          // development probe: JointArgs::probe of the joint forward (results wrong)
@@ -245,6 +246,8 @@ struct ChaseArgs {
                                // computes the column itself
     uint32_t delay;            // development probe (ticks): producer workgroups start this late
     int stage;                 // one-wave recursion: LDS-staged frames (the product's only form) or direct loads
+    int probe;                 // development probe of the staged walk's step (results wrong): bit 0 no alpha/beta
+                               // stores, bit 1 a max in place of the log-sum-exp, bit 2 no ring reads after the first P
 };
 // The log-softmax body the chase launch carries for f32 rows of V elements: 0 rows on 16-lane groups (<= 64
 // vectors), 2 / 3 single-chunk rows of <= 128 vectors (full / partial chunk), 4 / 5 of <= 256; -1 none.

@@ -33,6 +33,9 @@ redab)
   python3 $R/tools/pmc_kernel.py $O/pmc_red_fetch --match reduce --match joint_fwd > $O/pmc_red_fetch.txt && \
   python3 $R/tools/pmc_kernel.py $O/pmc_red_fetch_xcd --match reduce --match joint_fwd > $O/pmc_red_fetch_xcd.txt
   rc=$?; echo rc=$rc; tail -n 2 $O/pytest_joint.log; cat $O/joint_ab.json; cat $O/pmc_red_fetch.txt $O/pmc_red_fetch_xcd.txt; exit $rc ;;
+cprobe)
+  timeout -k 10 300 python tools/kbench.py --config c2 --rounds 40 --probe --variants '[{"chase_probe":0},{"chase_probe":1},{"chase_probe":2},{"chase_probe":3},{"chase_probe":4},{"chase_probe":7}]' > $O/chase_probe.json 2> $O/chase_probe.err
+  rc=$?; echo rc=$rc; cat $O/chase_probe.json; exit $rc ;;
 dpre)
   timeout -k 10 300 python tools/dpre_bench.py > $O/dpre_bench.json 2> $O/dpre_bench.err && \
   timeout -k 10 300 python -u -m pytest tests/test_gpu_joint.py -x -q --timeout 300 --timeout-method thread -k dpre > $O/pytest_dpre.log 2>&1
