@@ -24,9 +24,12 @@ labels = torch.randint(1, V, (B, S), device=dev, dtype=torch.int32, generator=g)
 Th = torch.full((B,), T, dtype=torch.int32)
 Sh = torch.full((B,), S, dtype=torch.int32)
 out = {}
-for form, stage in [("device", 1), ("host", 1)]:
+# (lengths form, chase_stage, chase_probe): the product's staged walk, the walk without ring reads after its first
+# frames (probe 4: it no longer waits for frames) and with a max in place of the log-sum-exp (probe 2) -- the probes'
+# results are wrong, timing only. (A 32-frame ring, measured in round 5: profiles/r05/chase/.)
+for form, stage, probe in [("device", 1, 0), ("host", 1, 0), ("device", 1, 4), ("device", 1, 2)]:
     Tt, St = (Th, Sh) if form == "host" else (Th.to(dev), Sh.to(dev))
-    with knobs(chase=1, chase_stage=stage):
+    with knobs(chase=1, chase_stage=stage, chase_probe=probe):
         lib = L.load_dev()
         res = []
         for it in range(6):
@@ -59,6 +62,6 @@ for form, stage in [("device", 1), ("host", 1)]:
                 "alpha0": [float(x) for x in rel[0]],
                 "beta0": [float(x) for x in rel[1]],
             })
-        out[f"{form}_stage{stage}"] = res
-        print(form, stage, json.dumps(res[-1]), flush=True)
+        out[f"{form}_stage{stage}_probe{probe}"] = res
+        print(form, stage, probe, json.dumps(res[-1]), flush=True)
 json.dump(out, open(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/chase_trace.json", "w"), indent=1)
