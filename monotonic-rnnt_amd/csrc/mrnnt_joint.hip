@@ -825,7 +825,10 @@ constexpr int kReduceTT = 64;  // frames per workgroup (blocked form, and the sp
 //   kRedPre: dH already holds dpre = dH * (1 - Hact^2) (mrnnt_joint_dpre's epilogue).
 constexpr int kRedTanh = 0, kRedHact = 1, kRedPre = 2;
 
-template <int HS, int SRC>
+// AP: LDS row pitch of the accumulators (HS + 1: a column's consecutive rows start on successive banks, so the four
+// 4-byte accesses per thread -- 8 threads per row, 4 rows per 32-lane bank group -- are conflict-free; a pitch of HS
+// put rows s and s + 2 on the same banks, SQ_LDS_BANK_CONFLICT 0.67 of the LDS cycles in round 4).
+template <int HS, int SRC, int AP>
 __global__ __launch_bounds__(256) void joint_reduce_kernel(DevProblem p, JointArgs j, const int64_t *__restrict__ off,
                                                            const unsigned short *__restrict__ dH,
                                                            float *__restrict__ d_enc, float *__restrict__ d_pred,
@@ -833,7 +836,7 @@ __global__ __launch_bounds__(256) void joint_reduce_kernel(DevProblem p, JointAr
                                                            int *__restrict__ rng) {
     constexpr int TPR = HS / 4;     // threads per row slice
     constexpr int RP = 256 / TPR;   // rows in parallel
-    extern __shared__ float lds[];  // acc[(S_b+1) * HS], red[RP][HS], then (kRedTanh) pred slice [S_b+1][HS] bf16
+    extern __shared__ float lds[];  // acc[(S_b+1) * AP], red[RP][AP], then (kRedTanh) pred slice [S_b+1][HS] bf16
     const int H = j.H;
     const int nh = H / HS;
     // the h-slices of one block of frames are consecutive workgroups: they read the same rows (L2 reuse)
@@ -852,7 +855,7 @@ __global__ __launch_bounds__(256) void joint_reduce_kernel(DevProblem p, JointAr
     }
     const int hl = (tid % TPR) * 4, rsub = tid / TPR;
     float *acc = lds;
-    float *red = lds + (S + 1) * HS;
+    float *red = lds + (S + 1) * AP;
     const int64_t tslots = j.enc_sb / H, sslots = j.pred_sb / H;
     const int t1 = min(t0 + tt, T);
     // label positions this block of frames touches: rows of a column are listed by ascending s, so the first and
@@ -874,9 +877,9 @@ __global__ __launch_bounds__(256) void joint_reduce_kernel(DevProblem p, JointAr
     }
     __syncthreads();
     const int s_lo = srange[0], s_hi = srange[1];
-    for (int i = s_lo * HS + tid; i < (s_hi + 1) * HS; i += 256) acc[i] = 0.0f;
+    for (int i = s_lo * HS + tid; i < (s_hi + 1) * HS; i += 256) acc[i / HS * AP + i % HS] = 0.0f;
     // kRedTanh: pred[b, s, h0 .. h0 + HS) for the touched s, 8 bytes per thread and row
-    unsigned short *pl = reinterpret_cast<unsigned short *>(red + RP * HS);
+    unsigned short *pl = reinterpret_cast<unsigned short *>(red + RP * AP);
     if constexpr (SRC == kRedTanh) {
         for (int i = s_lo * TPR + tid; i < (s_hi + 1) * TPR; i += 256) {
             const int ss = i / TPR, hq = (i % TPR) * 4;
@@ -917,13 +920,13 @@ __global__ __launch_bounds__(256) void joint_reduce_kernel(DevProblem p, JointAr
             e1 += v1;
             e2 += v2;
             e3 += v3;
-            float *a = acc + s * HS + hl;  // distinct s within a column: one writer per element
+            float *a = acc + s * AP + hl;  // distinct s within a column: one writer per element
             a[0] += v0;
             a[1] += v1;
             a[2] += v2;
             a[3] += v3;
         }
-        float *rr = red + rsub * HS + hl;
+        float *rr = red + rsub * AP + hl;
         rr[0] = e0;
         rr[1] = e1;
         rr[2] = e2;
@@ -932,18 +935,19 @@ __global__ __launch_bounds__(256) void joint_reduce_kernel(DevProblem p, JointAr
         if (tid < HS) {
             float sum = 0.0f;
 #pragma unroll 4
-            for (int g = 0; g < RP; ++g) sum += red[g * HS + tid];
+            for (int g = 0; g < RP; ++g) sum += red[g * AP + tid];
             d_enc[((int64_t)b * tslots + t) * H + h0 + tid] = sum;
         }
         __syncthreads();
     }
     if (!part) {  // one block per utterance: this workgroup is the one writer
         for (int i = s_lo * HS + tid; i < (s_hi + 1) * HS; i += 256)
-            d_pred[((int64_t)b * sslots + i / HS) * H + h0 + i % HS] += acc[i];
+            d_pred[((int64_t)b * sslots + i / HS) * H + h0 + i % HS] += acc[i / HS * AP + i % HS];
         return;
     }
     float *pb = part + (int64_t)bx * wstride * H;
-    for (int i = s_lo * HS + tid; i < (s_hi + 1) * HS; i += 256) pb[(int64_t)(i / HS) * H + h0 + i % HS] = acc[i];
+    for (int i = s_lo * HS + tid; i < (s_hi + 1) * HS; i += 256)
+        pb[(int64_t)(i / HS) * H + h0 + i % HS] = acc[i / HS * AP + i % HS];
     if (h0 == 0 && tid == 0) {
         rng[2 * bx] = s_lo;
         rng[2 * bx + 1] = s_hi;
@@ -1051,8 +1055,14 @@ hipError_t launch_joint_reduce(const DevProblem &p, const JointArgs &j, const in
     const bool tanh_src = kVariants && tuning().joint_reduce_hact == 0 && !pre;
     auto go = [&](auto hs_tag) {
         constexpr int HS = decltype(hs_tag)::value;
-        auto kern = pre ? joint_reduce_kernel<HS, kRedPre>
-                        : (tanh_src ? joint_reduce_kernel<HS, kRedTanh> : joint_reduce_kernel<HS, kRedHact>);
+        // (accumulator pitch HS + 1; the development build's joint_reduce_pad = 0 runs pitch HS, bit-identical)
+        constexpr int AP = HS + 1;
+        const bool nopad = kVariants && tuning().joint_reduce_pad == 0;
+        auto kern = pre ? (nopad ? joint_reduce_kernel<HS, kRedPre, HS> : joint_reduce_kernel<HS, kRedPre, AP>)
+                        : (tanh_src ? joint_reduce_kernel<HS, kRedTanh, AP>
+                                    : (nopad ? joint_reduce_kernel<HS, kRedHact, HS>
+                                             : joint_reduce_kernel<HS, kRedHact, AP>));
+        const int apitch = nopad ? HS : AP;
         if (sparse) {
             const size_t lds = sizeof(float) * ((size_t)W * HS + (size_t)kReduceTT * HS);
             joint_reduce_sparse_kernel<HS><<<p.B * ntb * (j.H / HS), 256, lds, stream>>>(p, j, off, dH, d_enc,
@@ -1060,7 +1070,7 @@ hipError_t launch_joint_reduce(const DevProblem &p, const JointArgs &j, const in
             return;
         }
         // (+ the staged pred slice, bf16 [W][HS], of the recomputing form: up to 88 KiB)
-        const size_t lds = sizeof(float) * ((size_t)W * HS + 256 / (HS / 4) * HS) +
+        const size_t lds = sizeof(float) * ((size_t)W * apitch + 256 / (HS / 4) * apitch) +
                            (tanh_src ? sizeof(unsigned short) * W * HS : 0);
         if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)

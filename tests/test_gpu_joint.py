@@ -327,3 +327,15 @@ def test_joint_reduce_recomputed_activation_is_bit_identical(jop, dev, H, V):
     with knobs(joint_reduce_hact=1):
         _, de1, dp1, dw1, _ = run_joint(jop, dev, enc, pred, w, bias, labels, T, S)
     assert torch.equal(de0, de1) and torch.equal(dp0, dp1) and torch.equal(dw0, dw1)
+
+
+@pytest.mark.parametrize("H,V,S_max", [(512, 256, 100), (256, 1000, 20), (640, 130, 90), (128, 64, 5)])
+def test_joint_reduce_padded_pitch_bit_identical(jop, dev, H, V, S_max):
+    """The reduce's accumulators at LDS pitch HS + 1 (default, bank-conflict-free) equal pitch HS (development build,
+    joint_reduce_pad = 0) bit for bit: only the layout differs, every sum keeps its order."""
+    enc, pred, w, bias, labels, T, S = make_case(H + V + S_max, 3, (max(30, S_max - 10), S_max + 31), S_max, H, V)
+    with knobs(joint_reduce_pad=0):
+        _, de0, dp0, dw0, _ = run_joint(jop, dev, enc, pred, w, bias, labels, T, S)
+    with knobs(joint_reduce_pad=1):
+        _, de1, dp1, dw1, _ = run_joint(jop, dev, enc, pred, w, bias, labels, T, S)
+    assert torch.equal(de0, de1) and torch.equal(dp0, dp1) and torch.equal(dw0, dw1)

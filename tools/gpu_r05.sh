@@ -24,18 +24,15 @@ reduce)
   timeout -k 10 300 python tools/joint_bench.py --no-unfused --steps 5 --tune joint_reduce_pf=1 > $O/joint_h512_pf1.json 2> $O/joint_h512_pf1.err
   rc=$?; echo rc=$rc; tail -n 3 $O/pytest_joint.log; cat $O/joint_h512.json $O/joint_h512_pf1.json; exit $rc ;;
 redab)
-  [ -n "$AB" ] || AB='[{"joint_reduce_pf":1},{"joint_reduce_pf":4},{"joint_reduce_pf":4,"joint_reduce_xcd":1},{"joint_reduce_pf":1,"joint_reduce_xcd":1}]'
+  [ -n "$AB" ] || AB='[{"joint_reduce_pad":0},{"joint_reduce_pad":1}]'
   timeout -k 10 300 python -u -m pytest tests/test_gpu_joint.py -x -q --timeout 300 --timeout-method thread > $O/pytest_joint.log 2>&1 && \
   timeout -k 10 400 python tools/joint_bench.py --no-unfused --steps 3 --ab "$AB" > $O/joint_ab.json 2> $O/joint_ab.err && \
   cd /tmp && export TMPDIR=/tmp && \
-  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_red_fetch -- python3 $R/tools/joint_bench.py --no-unfused --steps 1 --warmup 1 --tune joint_reduce_xcd=0 > $O/pmc_red_fetch.json 2> $O/pmc_red_fetch.err && \
-  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_red_fetch_xcd -- python3 $R/tools/joint_bench.py --no-unfused --steps 1 --warmup 1 --tune joint_reduce_xcd=1 > $O/pmc_red_fetch_xcd.json 2> $O/pmc_red_fetch_xcd.err && \
-  python3 $R/tools/pmc_kernel.py $O/pmc_red_fetch --match reduce --match joint_fwd > $O/pmc_red_fetch.txt && \
-  python3 $R/tools/pmc_kernel.py $O/pmc_red_fetch_xcd --match reduce --match joint_fwd > $O/pmc_red_fetch_xcd.txt
-  rc=$?; echo rc=$rc; tail -n 2 $O/pytest_joint.log; cat $O/joint_ab.json; cat $O/pmc_red_fetch.txt $O/pmc_red_fetch_xcd.txt; exit $rc ;;
-cprobe)
-  timeout -k 10 300 python tools/kbench.py --config c2 --rounds 40 --probe --variants '[{"chase_probe":0},{"chase_probe":1},{"chase_probe":2},{"chase_probe":3},{"chase_probe":4},{"chase_probe":7}]' > $O/chase_probe.json 2> $O/chase_probe.err
-  rc=$?; echo rc=$rc; cat $O/chase_probe.json; exit $rc ;;
+  for pad in 0 1; do \
+    timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d $O/pmc_red_sq_pad$pad -- python3 $R/tools/joint_bench.py --no-unfused --steps 1 --warmup 1 --tune joint_reduce_pad=$pad > $O/pmc_red_sq_pad$pad.json 2> $O/pmc_red_sq_pad$pad.err || exit 1; \
+    python3 $R/tools/pmc_kernel.py $O/pmc_red_sq_pad$pad --match reduce > $O/pmc_red_sq_pad$pad.txt || exit 1; \
+  done
+  rc=$?; echo rc=$rc; tail -n 2 $O/pytest_joint.log; python3 -c "import json;d=json.load(open('$O/joint_ab.json'));[print(v['knobs'],v['median_ms']) for v in d['ab']]"; cat $O/pmc_red_sq_pad0.txt $O/pmc_red_sq_pad1.txt; exit $rc ;;
 dpre)
   timeout -k 10 300 python tools/dpre_bench.py > $O/dpre_bench.json 2> $O/dpre_bench.err && \
   timeout -k 10 300 python -u -m pytest tests/test_gpu_joint.py -x -q --timeout 300 --timeout-method thread -k dpre > $O/pytest_dpre.log 2>&1
