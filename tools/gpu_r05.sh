@@ -33,6 +33,20 @@ redab)
     python3 $R/tools/pmc_kernel.py $O/pmc_red_sq_pad$pad --match reduce > $O/pmc_red_sq_pad$pad.txt || exit 1; \
   done
   rc=$?; echo rc=$rc; tail -n 2 $O/pytest_joint.log; python3 -c "import json;d=json.load(open('$O/joint_ab.json'));[print(v['knobs'],v['median_ms']) for v in d['ab']]"; cat $O/pmc_red_sq_pad0.txt $O/pmc_red_sq_pad1.txt; exit $rc ;;
+sweeps)
+  # opt-in full-batch parity runs (minutes of CPU oracle each: a heartbeat file shows the run alive)
+  mkdir -p $O/tests
+  ( while true; do date > $O/tests/heartbeat; sleep 30; done ) &
+  HB=$!
+  MRNNT_FULL_BATCH=1 timeout -k 10 600 python -u -m pytest tests/test_gpu_fullsize.py -v -rs --timeout 600 --timeout-method thread -s > $O/tests/full_batch_headline_64utt.log 2>&1 && \
+  MRNNT_FULL_BATCH=1 timeout -k 10 600 python -u -m pytest tests/test_gpu_c4_shards.py -v -rs --timeout 600 --timeout-method thread -s > $O/tests/c4_full_batch_costs_512utt.log 2>&1 && \
+  MRNNT_FULL_BATCH=1 timeout -k 10 600 python -u -m pytest tests/test_gpu_c5_chunks.py -v -rs --timeout 600 --timeout-method thread -s > $O/tests/c5_full_batch_costs_64utt.log 2>&1
+  rc=$?; kill $HB; echo rc=$rc; tail -n 3 $O/tests/*.log; exit $rc ;;
+fuzz)
+  mkdir -p $O/tests
+  MRNNT_FUZZ_CASES=1000 MRNNT_FUZZ_FIRST=150000 timeout -k 10 500 python -u -m pytest tests/test_gpu_fuzz.py -q --timeout 300 --timeout-method thread > $O/tests/fuzz_1000_seed150000.log 2>&1 && \
+  MRNNT_JOINT_CASES=120 MRNNT_FUZZ_FIRST=7000 timeout -k 10 500 python -u -m pytest tests/test_gpu_joint.py -k test_joint_random_cases -q --timeout 300 --timeout-method thread > $O/tests/joint_fuzz_120_seed7000.log 2>&1
+  rc=$?; echo rc=$rc; tail -n 2 $O/tests/*fuzz*.log; exit $rc ;;
 dpre)
   timeout -k 10 300 python tools/dpre_bench.py > $O/dpre_bench.json 2> $O/dpre_bench.err && \
   timeout -k 10 300 python -u -m pytest tests/test_gpu_joint.py -x -q --timeout 300 --timeout-method thread -k dpre > $O/pytest_dpre.log 2>&1
