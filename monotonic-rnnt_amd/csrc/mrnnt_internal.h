@@ -96,8 +96,9 @@ struct JointArgs {
     float *dbias;                // [V] fp32: the backward adds sum_i G[i] into it (16x16x32 backward only), or nullptr
     float *dbias_part;           // with dbias: the backward's per-workgroup column sums, then the segment sums
                                  // (joint_dbias_part_bytes), summed in order by launch_joint_dbias_sum
-    int probe;                   // development build, forward timing probe (results wrong): bit 0 every row's
-                                 // activation reads pred row s = 0, bit 1 enc row t = 0 (0 otherwise)
+    int probe;                   // development build, timing probes (results wrong): forward bit 0 every row's
+                                 // activation reads pred row s = 0, bit 1 enc row t = 0; reduce bit 2 no frame
+                                 // barriers / d_enc sum (0 otherwise)
 };
 
 // Row lists over the lattice: mode 0 = every in-band row, mode 1 = live rows (needs alpha/beta/ll).

@@ -926,6 +926,16 @@ __global__ __launch_bounds__(256) void joint_reduce_kernel(DevProblem p, JointAr
             a[2] += v2;
             a[3] += v3;
         }
+        if (kVariants && (j.probe & 4)) {  // development timing probe: no frame barriers / d_enc sum (wrong results)
+            if (rsub == 0) {
+                float *de = d_enc + ((int64_t)b * tslots + t) * H + h0 + hl;
+                de[0] = e0;
+                de[1] = e1;
+                de[2] = e2;
+                de[3] = e3;
+            }
+            continue;
+        }
         float *rr = red + rsub * AP + hl;
         rr[0] = e0;
         rr[1] = e1;
@@ -1044,9 +1054,11 @@ __global__ __launch_bounds__(256) void joint_reduce_sparse_kernel(DevProblem p, 
     }
 }
 
-hipError_t launch_joint_reduce(const DevProblem &p, const JointArgs &j, const int64_t *off, int T_max, int S_max,
+hipError_t launch_joint_reduce(const DevProblem &p, const JointArgs &j_in, const int64_t *off, int T_max, int S_max,
                                const unsigned short *dH, float *d_enc, float *d_pred, void *scratch,
                                size_t scratch_bytes, hipStream_t stream) {
+    JointArgs j = j_in;
+    if (kVariants) j.probe = tuning().joint_probe;
     const int ntb = (T_max + kReduceTT - 1) / kReduceTT;
     const int W = S_max + 1;
     // the row-parallel sparse kernel with float atomics: development A/B only (joint_reduce_sparse = 2; dH + Hact)
