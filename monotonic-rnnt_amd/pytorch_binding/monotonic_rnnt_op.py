@@ -268,13 +268,16 @@ class _Prepared:
         self.device = dev
 
     def workspace(self) -> torch.Tensor:
-        key = (self.on_gpu, self.alignment is not None, _L.load())
+        p = self.problem
+        # the plan also depends on V and the acts element type (whether the chase launch applies, and so whether the
+        # workspace holds its ready flags) and on the device (its CU count bounds the chase)
+        key = (self.on_gpu, self.alignment is not None, _L.load(), p.V, p.acts_dtype, str(self.device), p.pad_T,
+               p.pad_S1)
         if self.dyn:  # sized from bounds: the shapes of acts and labels
-            p = self.problem
-            key = key + (p.B, p.num_rows, p.label_stride, p.pad_T, p.pad_S1)
+            key = key + (p.B, p.num_rows, p.label_stride)
             cache = _DYN_WS
         else:
-            cache = self.lengths.ws  # a function of the lengths and the alignment flag only
+            cache = self.lengths.ws  # with the key above, a function of the lengths
         n = cache.get(key)
         if n is None:
             c = ctypes.c_size_t(0)

@@ -287,3 +287,23 @@ def test_device_lengths_launch_count(op, dev, B):
     else:
         assert prof["chase"][1] == 0 and prof["log_softmax"][1] == 1 and prof["alpha_beta"][1] == 1, prof
     assert prof["grad"][1] == 1, prof
+
+
+@pytest.mark.parametrize("device_lengths", [True, False])
+def test_workspace_cache_follows_dtype_and_V(op, dev, device_lengths):
+    """The op caches workspace sizes per shape; the size also depends on the acts element type and V (the chase
+    launch, and with it the workspace's ready flags, applies to f32 rows of V <= 1024 only). Found by the round-5
+    fuzz sweep (seed 150450: a bf16 call of the same shape before an f32 one left a size without the flags)."""
+    rng = np.random.default_rng(150450)
+    T, S = np.array([28], np.int32), np.array([0], np.int32)
+    labels = _t(np.array([[65]], np.int32), dev)
+    Tt, St = (_t(T, dev), _t(S, dev)) if device_lengths else (_t(T), _t(S))
+    for dt, V in ((torch.bfloat16, 256), (torch.float32, 256), (torch.float32, 2048), (torch.float32, 256)):
+        acts32 = rng.standard_normal((28, V)).astype(np.float32)
+        acts = _t(acts32, dev, dt)
+        c, g = _run(op, acts, labels, Tt, St, blank=160 % V)
+        ref = acts.float().cpu().numpy()
+        cr, gr = O.oracle_rnnt(ref, np.array([[65]], np.int32), T, S, blank=160 % V)
+        assert_costs(c.cpu().numpy(), cr)
+        tol = 1e-4 if dt == torch.float32 else 2e-2
+        assert_grads(g.float().cpu().numpy(), gr, tol=tol)
