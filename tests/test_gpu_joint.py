@@ -340,22 +340,3 @@ def test_joint_reduce_padded_pitch_bit_identical(jop, dev, H, V, S_max):
         _, de1, dp1, dw1, _ = run_joint(jop, dev, enc, pred, w, bias, labels, T, S)
     assert torch.equal(de0, de1) and torch.equal(dp0, dp1) and torch.equal(dw0, dw1)
 
-
-@pytest.mark.parametrize("H,V,S_max,dpre", [(512, 256, 100, False), (512, 256, 100, True), (256, 1000, 20, False),
-                                             (640, 130, 90, False), (128, 64, 5, False)])
-def test_joint_reduce_wave_private_form(jop, dev, monkeypatch, H, V, S_max, dpre):
-    """The reduce with wave-private accumulators (development build, joint_reduce_form = 1: no barrier per frame)
-    equals the default form within fp32 summation-order rounding and is bitwise reproducible itself."""
-    if dpre:
-        monkeypatch.setattr(jop, "_DH_BLAS", False)
-    enc, pred, w, bias, labels, T, S = make_case(H + V + S_max + 1, 3, (max(30, S_max - 10), S_max + 31), S_max, H, V)
-    with knobs(joint_reduce_form=0):
-        _, de0, dp0, dw0, _ = run_joint(jop, dev, enc, pred, w, bias, labels, T, S)
-    with knobs(joint_reduce_form=1):
-        _, de1, dp1, dw1, _ = run_joint(jop, dev, enc, pred, w, bias, labels, T, S)
-        _, de2, dp2, _, _ = run_joint(jop, dev, enc, pred, w, bias, labels, T, S)
-    assert torch.equal(de1, de2) and torch.equal(dp1, dp2)
-    assert torch.equal(dw0, dw1)
-    for x, y in ((de1, de0), (dp1, dp0)):
-        err = (x.float() - y.float()).abs().max().item()
-        assert err <= 1e-5 * max(1.0, y.float().abs().max().item()), err

@@ -24,12 +24,12 @@ reduce)
   timeout -k 10 300 python tools/joint_bench.py --no-unfused --steps 5 --tune joint_reduce_pf=1 > $O/joint_h512_pf1.json 2> $O/joint_h512_pf1.err
   rc=$?; echo rc=$rc; tail -n 3 $O/pytest_joint.log; cat $O/joint_h512.json $O/joint_h512_pf1.json; exit $rc ;;
 redab)
-  [ -n "$AB" ] || AB='[{"joint_reduce_form":0},{"joint_reduce_form":1},{"joint_probe":4}]'
+  [ -n "$AB" ] || AB='[{"joint_probe":0},{"joint_probe":4}]'
   timeout -k 10 300 python -u -m pytest tests/test_gpu_joint.py -x -q --timeout 300 --timeout-method thread > $O/pytest_joint.log 2>&1 && \
   timeout -k 10 400 python tools/joint_bench.py --no-unfused --steps 3 --ab "$AB" > $O/joint_ab.json 2> $O/joint_ab.err && \
   cd /tmp && export TMPDIR=/tmp && \
   for form in 0 1; do \
-    timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d $O/pmc_red_sq_form$form -- python3 $R/tools/joint_bench.py --no-unfused --steps 1 --warmup 1 --tune joint_reduce_form=$form > $O/pmc_red_sq_form$form.json 2> $O/pmc_red_sq_form$form.err || exit 1; \
+    timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d $O/pmc_red_sq_form$form -- python3 $R/tools/joint_bench.py --no-unfused --steps 1 --warmup 1 --tune joint_probe=$((4*form)) > $O/pmc_red_sq_form$form.json 2> $O/pmc_red_sq_form$form.err || exit 1; \
     python3 $R/tools/pmc_kernel.py $O/pmc_red_sq_form$form --match reduce > $O/pmc_red_sq_form$form.txt || exit 1; \
   done
   rc=$?; echo rc=$rc; tail -n 2 $O/pytest_joint.log; python3 -c "import json;d=json.load(open('$O/joint_ab.json'));[print(v['knobs'],v['median_ms']) for v in d['ab']]"; cat $O/pmc_red_sq_form0.txt $O/pmc_red_sq_form1.txt; exit $rc ;;
