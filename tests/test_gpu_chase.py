@@ -419,3 +419,24 @@ def test_chase_device_lengths_batch_limit(op, dev, B):
     else:
         assert n["chase"] == 0 and n["setup"] == 1, n
     op.check_lengths()
+
+
+@pytest.mark.parametrize("lengths", ["host", "device"])
+@pytest.mark.parametrize("name", list(CASES))
+def test_product_chase_vs_oracle(op, dev, name, lengths):
+    """The PRODUCT library (no knobs: the tuned defaults) on every chase shape, against the fp64 oracle directly.
+    The bit-identity tests above anchor the chase to the development build's two-kernel path; this anchors the
+    product build's own launch to the reference semantics, on host and device lengths."""
+    acts, labels, T, S, a, lab = _problem(name, dev)
+    if lengths == "host":
+        Tt, St = torch.from_numpy(T), torch.from_numpy(S)
+    else:
+        Tt, St = torch.from_numpy(T).to(dev), torch.from_numpy(S).to(dev)
+    got = {}
+    n = _launches(lambda: got.setdefault("r", _run(op, a, lab, Tt, St)))
+    if name == "c2_row16_one_wave":  # configs[1]: the shape the chase is tuned for takes it on both forms
+        assert n["chase"] == 1 and n["log_softmax"] == 0, n
+    c, g = got["r"]
+    cr, gr = O.oracle_rnnt(acts, labels, T, S)
+    assert_costs(c.cpu().numpy(), cr)
+    assert_grads(g.cpu().numpy(), gr)

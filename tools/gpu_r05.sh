@@ -47,6 +47,12 @@ fuzz)
   MRNNT_FUZZ_CASES=1000 MRNNT_FUZZ_FIRST=150000 timeout -k 10 500 python -u -m pytest tests/test_gpu_fuzz.py -q --timeout 300 --timeout-method thread > $O/tests/fuzz_1000_seed150000.log 2>&1 && \
   MRNNT_JOINT_CASES=120 MRNNT_FUZZ_FIRST=7000 timeout -k 10 500 python -u -m pytest tests/test_gpu_joint.py -k test_joint_random_cases -q --timeout 300 --timeout-method thread > $O/tests/joint_fuzz_120_seed7000.log 2>&1
   rc=$?; echo rc=$rc; tail -n 2 $O/tests/*fuzz*.log; exit $rc ;;
+final)
+  # the round's closing measurements on the final library: full suite, smoke, bench lines, PMC traffic
+  MODE=full bash $R/tools/gpu_r05.sh && \
+  TAG=r05 bash $R/tools/gpu_profile.sh && \
+  MODE=c2 TAG=r05final bash $R/tools/gpu_r05.sh
+  rc=$?; echo rc=$rc; exit $rc ;;
 dpre)
   timeout -k 10 300 python tools/dpre_bench.py > $O/dpre_bench.json 2> $O/dpre_bench.err && \
   timeout -k 10 300 python -u -m pytest tests/test_gpu_joint.py -x -q --timeout 300 --timeout-method thread -k dpre > $O/pytest_dpre.log 2>&1
