@@ -139,12 +139,19 @@ def main():
         variants = json.loads(a.ab)
         saved = [{k: L.tune(k) for k in v} for v in variants]
         runs = [dict() for _ in variants]
+        steps = [[] for _ in variants]
         for r in range(a.ab_rounds):
             for vi, v in enumerate(variants):
                 for k, x in v.items():
                     assert L.tune(k, int(x)) >= 0, k
                 fused()
                 torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                fused()
+                e1.record()
+                torch.cuda.synchronize()
+                steps[vi].append(e0.elapsed_time(e1))
                 L.profile_enable(True)
                 fused()
                 torch.cuda.synchronize()
@@ -155,7 +162,9 @@ def main():
                         runs[vi].setdefault(k, []).append(pr[k][0] / pr[k][1])
                 for k, x in saved[vi].items():
                     L.tune(k, x)
-        out["ab"] = [{"knobs": v, "median_ms": {k: round(float(np.median(x)), 4) for k, x in runs[vi].items()},
+        out["ab"] = [{"knobs": v, "step_ms_median": round(float(np.median(steps[vi])), 3),
+                      "step_ms_min": round(float(np.min(steps[vi])), 3),
+                      "median_ms": {k: round(float(np.median(x)), 4) for k, x in runs[vi].items()},
                       "min_ms": {k: round(float(np.min(x)), 4) for k, x in runs[vi].items()}}
                      for vi, v in enumerate(variants)]
     print(json.dumps(out), flush=True)
