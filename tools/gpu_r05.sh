@@ -53,6 +53,9 @@ final)
   TAG=r05 bash $R/tools/gpu_profile.sh && \
   MODE=c2 TAG=r05final bash $R/tools/gpu_r05.sh
   rc=$?; echo rc=$rc; exit $rc ;;
+jtrace)
+  timeout -k 10 300 python tools/joint_trace.py $O/joint_trace.json > $O/joint_trace.txt 2>&1
+  rc=$?; echo rc=$rc; cat $O/joint_trace.txt | tail -6; exit $rc ;;
 dpre)
   timeout -k 10 300 python tools/dpre_bench.py > $O/dpre_bench.json 2> $O/dpre_bench.err && \
   timeout -k 10 300 python -u -m pytest tests/test_gpu_joint.py -x -q --timeout 300 --timeout-method thread -k dpre > $O/pytest_dpre.log 2>&1
