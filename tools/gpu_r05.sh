@@ -56,6 +56,13 @@ final)
 jtrace)
   timeout -k 10 300 python tools/joint_trace.py $O/joint_trace.json > $O/joint_trace.txt 2>&1
   rc=$?; echo rc=$rc; cat $O/joint_trace.txt | tail -6; exit $rc ;;
+fuzzvar)
+  # seeded sweeps through other launch variants of the development build (MRNNT_FUZZ_TUNE)
+  mkdir -p $O/tests
+  MRNNT_FUZZ_TUNE="dp_halo=0,grad_variant=3" MRNNT_FUZZ_CASES=1000 MRNNT_FUZZ_FIRST=160000 timeout -k 10 500 python -u -m pytest tests/test_gpu_fuzz.py -q --timeout 300 --timeout-method thread > $O/tests/fuzz_1000_seed160000_dphalo0_grad3.log 2>&1 && \
+  MRNNT_FUZZ_TUNE="chase=0" MRNNT_FUZZ_CASES=1000 MRNNT_FUZZ_FIRST=170000 timeout -k 10 500 python -u -m pytest tests/test_gpu_fuzz.py -q --timeout 300 --timeout-method thread > $O/tests/fuzz_1000_seed170000_chase0.log 2>&1 && \
+  MRNNT_FUZZ_TUNE="chase_stage=0,chase_wait_us=0" MRNNT_FUZZ_CASES=1000 MRNNT_FUZZ_FIRST=180000 timeout -k 10 500 python -u -m pytest tests/test_gpu_fuzz.py -q --timeout 300 --timeout-method thread > $O/tests/fuzz_1000_seed180000_direct_selfhelp.log 2>&1
+  rc=$?; echo rc=$rc; tail -n 2 $O/tests/fuzz_1000_seed1[678]*.log; exit $rc ;;
 dpre)
   timeout -k 10 300 python tools/dpre_bench.py > $O/dpre_bench.json 2> $O/dpre_bench.err && \
   timeout -k 10 300 python -u -m pytest tests/test_gpu_joint.py -x -q --timeout 300 --timeout-method thread -k dpre > $O/pytest_dpre.log 2>&1
