@@ -63,6 +63,9 @@ fuzzvar)
   MRNNT_FUZZ_TUNE="chase=0" MRNNT_FUZZ_CASES=1000 MRNNT_FUZZ_FIRST=170000 timeout -k 10 500 python -u -m pytest tests/test_gpu_fuzz.py -q --timeout 300 --timeout-method thread > $O/tests/fuzz_1000_seed170000_chase0.log 2>&1 && \
   MRNNT_FUZZ_TUNE="chase_stage=0,chase_wait_us=0" MRNNT_FUZZ_CASES=1000 MRNNT_FUZZ_FIRST=180000 timeout -k 10 500 python -u -m pytest tests/test_gpu_fuzz.py -q --timeout 300 --timeout-method thread > $O/tests/fuzz_1000_seed180000_direct_selfhelp.log 2>&1
   rc=$?; echo rc=$rc; tail -n 2 $O/tests/fuzz_1000_seed1[678]*.log; exit $rc ;;
+cgrid)
+  timeout -k 10 300 python tools/kbench.py --config c2 --rounds 30 --variants '[{"chase_grid_per_cu":0},{"chase_grid_per_cu":4},{"chase_grid_per_cu":6},{"chase_grid_per_cu":8},{"chase_grid_per_cu":12},{"chase_grid_per_cu":16}]' > $O/chase_grid.json 2> $O/chase_grid.err
+  rc=$?; echo rc=$rc; python3 -c "import json;d=json.load(open('$O/chase_grid.json'));[print(v['knobs'],round(v['median_ms']['chase']*1e3,2)) for v in d['variants']]"; exit $rc ;;
 dpre)
   timeout -k 10 300 python tools/dpre_bench.py > $O/dpre_bench.json 2> $O/dpre_bench.err && \
   timeout -k 10 300 python -u -m pytest tests/test_gpu_joint.py -x -q --timeout 300 --timeout-method thread -k dpre > $O/pytest_dpre.log 2>&1
