@@ -22,8 +22,9 @@ import threading
 import torch  # noqa: F401
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-# MRNNT_LIB_PATH: load another build of the library in place of the product (the host-only sanitizer build,
-# `make -C monotonic-rnnt_amd asan`, which has the CPU entry points only; tests/test_sanitizers.py)
+# MRNNT_LIB_PATH: load another build of the library in place of the product -- the host-only sanitizer build
+# (`make -C monotonic-rnnt_amd asan`, CPU entry points only; tests/test_sanitizers.py) or the product with its host
+# orchestration sanitized (`asan-gpu`; tests/test_gpu_host_asan.py)
 HOST_ONLY_PATH = os.environ.get("MRNNT_LIB_PATH") or None
 LIB_PATH = HOST_ONLY_PATH or os.path.join(PKG_DIR, "libmonotonic_rnnt_amd.so")
 DEV_PATH = os.path.join(PKG_DIR, "libmonotonic_rnnt_amd_dev.so")

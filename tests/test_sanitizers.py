@@ -56,7 +56,8 @@ def test_reference_cpu_program_under_asan(asan_build):
 
 
 def test_cpu_parity_suite_under_asan(asan_build):
-    pre = ":".join([_runtime("libasan.so"), _runtime("libubsan.so")])
+    # the sanitizer runtimes first in the initial library list; whatever the environment already preloads stays
+    pre = ":".join([_runtime("libasan.so"), _runtime("libubsan.so")] + list(filter(None, [os.environ.get("LD_PRELOAD")])))
     env = _env(LD_PRELOAD=pre, MRNNT_LIB_PATH=asan_build, MRNNT_SAN_FLAGS=SAN)
     cmd = [sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "not gpu",
            "-k", "not gpu_reference_client_builds",

@@ -66,6 +66,12 @@ fuzzvar)
 cgrid)
   timeout -k 10 300 python tools/kbench.py --config c2 --rounds 30 --variants '[{"chase_grid_per_cu":0},{"chase_grid_per_cu":4},{"chase_grid_per_cu":6},{"chase_grid_per_cu":8},{"chase_grid_per_cu":12},{"chase_grid_per_cu":16}]' > $O/chase_grid.json 2> $O/chase_grid.err
   rc=$?; echo rc=$rc; python3 -c "import json;d=json.load(open('$O/chase_grid.json'));[print(v['knobs'],round(v['median_ms']['chase']*1e3,2)) for v in d['variants']]"; exit $rc ;;
+hasan)
+  # the GPU library's host orchestration under ASan / UBSan (a child pytest process; a heartbeat file shows it alive)
+  ( while true; do date > $O/hasan_heartbeat; sleep 30; done ) &
+  HB=$!
+  timeout -k 10 1100 python -u -m pytest tests/test_gpu_host_asan.py -x -v -rs --timeout 1050 --timeout-method thread > $O/pytest_host_asan.log 2>&1
+  rc=$?; kill $HB; echo rc=$rc; tail -n 30 $O/pytest_host_asan.log; exit $rc ;;
 dpre)
   timeout -k 10 300 python tools/dpre_bench.py > $O/dpre_bench.json 2> $O/dpre_bench.err && \
   timeout -k 10 300 python -u -m pytest tests/test_gpu_joint.py -x -q --timeout 300 --timeout-method thread -k dpre > $O/pytest_dpre.log 2>&1
