@@ -1177,10 +1177,82 @@ static hipError_t launch_joint(const DevProblem &p, const JointArgs &j, bool bwd
     }
 }
 
+// Development A/B (joint_probe bit 3, H = 512): the forward's epilogue without the running max -- a plain exp-sum,
+// valid only while every logit stays below ~80 (no fp32 overflow of 1024 terms); the candidate of DESIGN.md 9.5
+// measured before a bound check is built. Otherwise joint_fwd_kernel<32, 2, 8, 2> line for line.
+template <int KS, int NB, int NW, int RG>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2))) void joint_fwd_nomax_kernel(
+    DevProblem p, JointArgs j) {
+    extern __shared__ __attribute__((aligned(16))) unsigned short wsh[];
+    if ((int64_t)blockIdx.x * (32 * NW) >= list_len(j)) return;
+    const int lane = threadIdx.x & 63, half = lane >> 5;
+    const int64_t i = (int64_t)blockIdx.x * (32 * NW) + (threadIdx.x >> 6) * 32 + (lane & 31);
+    const RowPos q = row_pos(p, j, i);
+    const int V = p.V, blank = p.blank;
+    const float *bias = load_bias<KS, NB>(j, V, wsh);
+    __syncthreads();
+    bf16x8 bfr[KS];
+    build_act<KS, false>(j, q, half, i, bfr);
+    const f2 l2e = {kLog2e, kLog2e};
+    float sum = 0.0f, zb = 0.0f, ze = 0.0f;
+    bool fb = false, fe = false;
+    chunk_loop<KS, NB, NW, RG>(j, V, wsh, bfr, lane, 0, [&](const f32x16 &acc, int c) {
+        f2 z[8];
+        logits2(acc, bias, c, half, z);
+        f2 s2 = {0.0f, 0.0f};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const f2 t = mul2(z[k], l2e);
+            s2 = add2(s2, (f2){fast_exp2(t.x), fast_exp2(t.y)});
+        }
+        sum += s2.x + s2.y;
+        const int jb = blank - 32 * c;
+        if (jb >= 0 && jb < 32) {
+            const int rb = acc_reg_of(jb, half);
+            if (rb >= 0) {
+                zb = tree_pick(z, rb);
+                fb = true;
+            }
+        }
+        const int jl = q.lab - 32 * c;
+        const int rl = acc_reg_of(jl & 31, half);
+        const bool mine = q.lab >= 0 && jl >= 0 && jl < 32 && rl >= 0;
+        if (__ballot(mine)) {
+            const float x = tree_pick(z, rl);
+            if (mine) {
+                ze = x;
+                fe = true;
+            }
+        }
+    });
+    sum += __shfl_xor(sum, 32);
+    const float zb2 = __shfl_xor(zb, 32), ze2 = __shfl_xor(ze, 32);
+    const int fb2 = __shfl_xor((int)fb, 32), fe2 = __shfl_xor((int)fe, 32);
+    if (!fb && fb2) zb = zb2;
+    if (!fe && fe2) ze = ze2;
+    if (q.valid && half == 0) {
+        const double den = -log_row_sum(sum);
+        p.den[q.row] = (float)den;
+        p.lp[q.row] = Lp{(double)zb + den, (q.lab >= 0 ? (double)ze : (q.lab == -2 ? __builtin_nan("") : 0.0)) + den};
+    }
+}
+
 hipError_t launch_joint_forward(const DevProblem &p, const JointArgs &j, hipStream_t stream) {
     if (kVariants && tuning().joint_probe) {
         JointArgs jp = j;
         jp.probe = tuning().joint_probe;
+        if constexpr (kVariants) {
+            if ((jp.probe & 8) && jp.H == 512 && jp.n > 0) {
+                const size_t lds = 2 * sizeof(unsigned short) * WTile<32>::ELEMS + sizeof(float) * ((p.V + 31) / 32 * 32);
+                const int64_t blocks = (jp.n + 255) / 256;
+                auto kern = joint_fwd_nomax_kernel<32, 2, 8, 2>;
+                if (hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)lds) != hipSuccess)
+                    return hipErrorInvalidValue;
+                kern<<<(int)blocks, 512, lds, stream>>>(p, jp);
+                return hipGetLastError();
+            }
+        }
         return launch_joint(p, jp, false, stream);
     }
     return launch_joint(p, j, false, stream);
