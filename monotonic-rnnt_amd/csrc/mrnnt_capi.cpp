@@ -702,7 +702,7 @@ namespace {
 struct JointPlan {
     Plan base;
     int64_t n_inband = 0;
-    size_t off_cnt = 0, off_lcol = 0, off_ls = 0, off_total = 0, off_dbias = 0, total = 0;
+    size_t off_cnt = 0, off_lcol = 0, off_ls = 0, off_total = 0, off_wplain = 0, off_dbias = 0, total = 0;
 };
 
 mrnnt_problem base_problem(const mrnnt_joint_problem *jp) {
@@ -763,6 +763,7 @@ RNNTStatus make_joint_plan(const mrnnt_joint_problem *jp, JointPlan *jl) {
     q.off_lcol = take(sizeof(int) * std::max<int64_t>(1, q.n_inband));
     q.off_ls = take(sizeof(int) * std::max<int64_t>(1, q.n_inband));
     q.off_total = take(sizeof(unsigned long long));
+    q.off_wplain = take(sizeof(int));  // the forward's weight-bound flag (launch_joint_wbound)
     // the gradient pass's per-workgroup dbias column sums (fixed-order reduction), when there is a bias
     q.off_dbias = (jp->bias && H <= 512) ? take(joint_dbias_part_bytes(std::max<int64_t>(1, q.n_inband), jp->V)) : 0;
     q.total = o;
@@ -845,7 +846,13 @@ RNNTStatus mrnnt_joint_forward(const mrnnt_joint_problem *jp, void *ws, size_t w
     if (e != hipSuccess) return fail_hip(e, "row list kernels");
     JointArgs j = joint_args(jp, jl, ws, jl.n_inband);
     if (pl.align) j.n_dev = reinterpret_cast<const unsigned long long *>(w + jl.off_total);  // alignment windows
-    e = timed(K_JOINT_FWD, stream, [&] { return launch_joint_forward(d, j, stream); });
+    // the weight bound decides the forward's epilogue on the device (no host sync): counted in the forward's time
+    int *wplain = reinterpret_cast<int *>(w + jl.off_wplain);
+    j.wplain = wplain;
+    e = timed(K_JOINT_FWD, stream, [&] {
+        const hipError_t eb = launch_joint_wbound(j.W, j.bias, jp->V, jp->H, wplain, stream);
+        return eb != hipSuccess ? eb : launch_joint_forward(d, j, stream);
+    });
     if (e != hipSuccess) return fail_hip(e, "joint log-softmax kernel");
     e = timed(K_DP, stream, [&] { return launch_dp(d, pl.S_max, with_beta ? 1 : 0, costs_dev, stream); });
     if (e != hipSuccess) return fail_hip(e, "alpha/beta kernel");

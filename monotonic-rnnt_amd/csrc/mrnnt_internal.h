@@ -96,15 +96,19 @@ struct JointArgs {
     float *dbias;                // [V] fp32: the backward adds sum_i G[i] into it (16x16x32 backward only), or nullptr
     float *dbias_part;           // with dbias: the backward's per-workgroup column sums, then the segment sums
                                  // (joint_dbias_part_bytes), summed in order by launch_joint_dbias_sum
+    const int *wplain;           // forward only: device flag, 1 when no logit can leave [-64, 64] (the weight bound of
+                                 // joint_wbound_kernel) -- the epilogue then sums exp(z) without a running max
     int probe;                   // development build, timing probes (results wrong): forward bit 0 every row's
-                                 // activation reads pred row s = 0, bit 1 enc row t = 0; reduce bit 2 no frame
-                                 // barriers / d_enc sum (0 otherwise)
+                                 // activation reads pred row s = 0, bit 1 enc row t = 0, bit 3 the running-max
+                                 // epilogue whatever the weight bound; reduce bit 2 no frame barriers / d_enc sum
 };
 
 // Row lists over the lattice: mode 0 = every in-band row, mode 1 = live rows (needs alpha/beta/ll).
 hipError_t launch_row_list(const DevProblem &p, int mode, int64_t *col_cnt, int *lcol, int *ls,
                            unsigned long long *total, hipStream_t stream);
 hipError_t launch_joint_forward(const DevProblem &p, const JointArgs &j, hipStream_t stream);
+// flag = 1 when max_v (sum_h |W[v, h]| + |bias[v]|) <= 64 (then |z| <= 64 for every logit: |tanh| <= 1), else 0
+hipError_t launch_joint_wbound(const unsigned short *W, const float *bias, int V, int H, int *flag, hipStream_t stream);
 hipError_t launch_joint_backward(const DevProblem &p, const JointArgs &j, hipStream_t stream);
 hipError_t launch_joint_reduce(const DevProblem &p, const JointArgs &j, const int64_t *off, int T_max, int S_max,
                                const unsigned short *dH, float *d_enc, float *d_pred, void *scratch,

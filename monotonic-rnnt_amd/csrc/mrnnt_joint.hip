@@ -483,23 +483,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const f2 l2e = {kLog2e, kLog2e};
     float m = NEG_INF_F, sum = 0.0f, zb = 0.0f, ze = 0.0f;
     bool fb = false, fe = false;
-    chunk_loop<KS, NB, NW, RG, true>(j, V, wsh, bfr, lane, 0, [&](const f32x16 &acc, int c) {
-        f2 z[8];
-        logits2(acc, bias, c, half, z);
-        float cm = fmaxf(z[0].x, z[0].y);
-#pragma unroll
-        for (int k = 1; k < 8; ++k) cm = max3(cm, z[k].x, z[k].y);
-        const float mn = fmaxf(m, cm);
-        const float mr = (mn == NEG_INF_F) ? 0.0f : mn;
-        const f2 nb = {-mr * kLog2e, -mr * kLog2e};
-        f2 s2 = {0.0f, 0.0f};
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const f2 t = fma2(z[k], l2e, nb);
-            s2 = add2(s2, (f2){fast_exp2(t.x), fast_exp2(t.y)});
-        }
-        sum = sum * fast_exp2((m - mr) * kLog2e) + (s2.x + s2.y);
-        m = mn;
+    // the blank / label logits of this lane's half of chunk c (the same selects in both epilogues)
+    auto capture = [&](const f2 (&z)[8], int c) {
         const int jb = blank - 32 * c;  // wave-uniform: one chunk holds the blank
         if (jb >= 0 && jb < 32) {
             const int rb = acc_reg_of(jb, half);
@@ -518,6 +503,56 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
                 fe = true;
             }
         }
+    };
+    // Bounded weights (j.wplain: |z| <= 64 for every logit, joint_wbound_kernel): a plain exp-sum -- 1024 terms of
+    // at most e^64 cannot overflow fp32 and the largest cannot underflow -- without the running max, whose
+    // per-chunk max / rescale chain cost 15 % of the forward. Otherwise the online log-sum-exp.
+    const bool plain = j.wplain != nullptr && *j.wplain != 0;
+    if (plain) {
+        chunk_loop<KS, NB, NW, RG, true>(j, V, wsh, bfr, lane, 0, [&](const f32x16 &acc, int c) {
+            f2 z[8];
+            logits2(acc, bias, c, half, z);
+            f2 s2 = {0.0f, 0.0f};
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const f2 t = mul2(z[k], l2e);
+                s2 = add2(s2, (f2){fast_exp2(t.x), fast_exp2(t.y)});
+            }
+            sum += s2.x + s2.y;
+            capture(z, c);
+            if (c == 0) JOINT_MARK(3);
+        });
+        sum += __shfl_xor(sum, 32);
+        const float zb2 = __shfl_xor(zb, 32), ze2 = __shfl_xor(ze, 32);
+        const int fb2 = __shfl_xor((int)fb, 32), fe2 = __shfl_xor((int)fe, 32);
+        if (!fb && fb2) zb = zb2;
+        if (!fe && fe2) ze = ze2;
+        if (q.valid && half == 0) {
+            const double den = -log_row_sum(sum);
+            p.den[q.row] = (float)den;
+            p.lp[q.row] = Lp{(double)zb + den, (q.lab >= 0 ? (double)ze : (q.lab == -2 ? __builtin_nan("") : 0.0)) + den};
+        }
+        JOINT_MARK(4);
+        return;
+    }
+    chunk_loop<KS, NB, NW, RG, true>(j, V, wsh, bfr, lane, 0, [&](const f32x16 &acc, int c) {
+        f2 z[8];
+        logits2(acc, bias, c, half, z);
+        float cm = fmaxf(z[0].x, z[0].y);
+#pragma unroll
+        for (int k = 1; k < 8; ++k) cm = max3(cm, z[k].x, z[k].y);
+        const float mn = fmaxf(m, cm);
+        const float mr = (mn == NEG_INF_F) ? 0.0f : mn;
+        const f2 nb = {-mr * kLog2e, -mr * kLog2e};
+        f2 s2 = {0.0f, 0.0f};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const f2 t = fma2(z[k], l2e, nb);
+            s2 = add2(s2, (f2){fast_exp2(t.x), fast_exp2(t.y)});
+        }
+        sum = sum * fast_exp2((m - mr) * kLog2e) + (s2.x + s2.y);
+        m = mn;
+        capture(z, c);
         if (c == 0) JOINT_MARK(3);
     });
     // merge the two lane halves (same row, disjoint vocabulary)
@@ -1177,82 +1212,64 @@ static hipError_t launch_joint(const DevProblem &p, const JointArgs &j, bool bwd
     }
 }
 
-// Development A/B (joint_probe bit 3, H = 512): the forward's epilogue without the running max -- a plain exp-sum,
-// valid only while every logit stays below ~80 (no fp32 overflow of 1024 terms); the candidate of DESIGN.md 9.5
-// measured before a bound check is built. Otherwise joint_fwd_kernel<32, 2, 8, 2> line for line.
-template <int KS, int NB, int NW, int RG>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2))) void joint_fwd_nomax_kernel(
-    DevProblem p, JointArgs j) {
-    extern __shared__ __attribute__((aligned(16))) unsigned short wsh[];
-    if ((int64_t)blockIdx.x * (32 * NW) >= list_len(j)) return;
-    const int lane = threadIdx.x & 63, half = lane >> 5;
-    const int64_t i = (int64_t)blockIdx.x * (32 * NW) + (threadIdx.x >> 6) * 32 + (lane & 31);
-    const RowPos q = row_pos(p, j, i);
-    const int V = p.V, blank = p.blank;
-    const float *bias = load_bias<KS, NB>(j, V, wsh);
+// flag = 1 when max_v (sum_h |W[v, h]| + |bias[v]|) <= 64: every logit z = W_v . h + b_v with |h| <= 1 (tanh,
+// rounded to bf16) then lies in [-64, 64]. One workgroup (no cross-workgroup combine, no flag reset launch), a wave per
+// weight row at a time, 16-byte loads (a 1 KiB row of H = 512 in one load per lane group): the V x H bf16 weights
+// (1 MiB at the headline joint size) are read once, a few microseconds. NaN / inf weights compare false: flag 0, the
+// running-max epilogue.
+__global__ __launch_bounds__(1024) void joint_wbound_kernel(const unsigned short *__restrict__ W,
+                                                            const float *__restrict__ bias, int V, int H,
+                                                            int *__restrict__ flag) {
+    __shared__ int bad;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (threadIdx.x == 0) bad = 0;
     __syncthreads();
-    bf16x8 bfr[KS];
-    build_act<KS, false>(j, q, half, i, bfr);
-    const f2 l2e = {kLog2e, kLog2e};
-    float sum = 0.0f, zb = 0.0f, ze = 0.0f;
-    bool fb = false, fe = false;
-    chunk_loop<KS, NB, NW, RG>(j, V, wsh, bfr, lane, 0, [&](const f32x16 &acc, int c) {
-        f2 z[8];
-        logits2(acc, bias, c, half, z);
-        f2 s2 = {0.0f, 0.0f};
+    int mine = 0;
+    for (int v0 = wave; v0 < V; v0 += 64) {  // four rows per wave per pass: eight loads in flight per lane
+        float s[4];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const f2 t = mul2(z[k], l2e);
-            s2 = add2(s2, (f2){fast_exp2(t.x), fast_exp2(t.y)});
-        }
-        sum += s2.x + s2.y;
-        const int jb = blank - 32 * c;
-        if (jb >= 0 && jb < 32) {
-            const int rb = acc_reg_of(jb, half);
-            if (rb >= 0) {
-                zb = tree_pick(z, rb);
-                fb = true;
+        for (int r = 0; r < 4; ++r) {
+            const int v = v0 + 16 * r;
+            s[r] = 0.0f;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {  // H <= 640 < 1024 (the joint plan's shapes), a multiple of 8
+                const int h = 8 * lane + 512 * k;
+                if (v < V && h < H) {
+                    const uint4 u = *reinterpret_cast<const uint4 *>(W + (int64_t)v * H + h);
+                    s[r] += (fabsf(bf16_lo(u.x)) + fabsf(bf16_hi(u.x))) + (fabsf(bf16_lo(u.y)) + fabsf(bf16_hi(u.y))) +
+                            (fabsf(bf16_lo(u.z)) + fabsf(bf16_hi(u.z))) + (fabsf(bf16_lo(u.w)) + fabsf(bf16_hi(u.w)));
+                }
             }
         }
-        const int jl = q.lab - 32 * c;
-        const int rl = acc_reg_of(jl & 31, half);
-        const bool mine = q.lab >= 0 && jl >= 0 && jl < 32 && rl >= 0;
-        if (__ballot(mine)) {
-            const float x = tree_pick(z, rl);
-            if (mine) {
-                ze = x;
-                fe = true;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int v = v0 + 16 * r;
+            float t = s[r];
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o);
+            if (v < V) {
+                if (bias) t += fabsf(bias[v]);
+                if (!(t <= 64.0f)) mine = 1;
             }
         }
-    });
-    sum += __shfl_xor(sum, 32);
-    const float zb2 = __shfl_xor(zb, 32), ze2 = __shfl_xor(ze, 32);
-    const int fb2 = __shfl_xor((int)fb, 32), fe2 = __shfl_xor((int)fe, 32);
-    if (!fb && fb2) zb = zb2;
-    if (!fe && fe2) ze = ze2;
-    if (q.valid && half == 0) {
-        const double den = -log_row_sum(sum);
-        p.den[q.row] = (float)den;
-        p.lp[q.row] = Lp{(double)zb + den, (q.lab >= 0 ? (double)ze : (q.lab == -2 ? __builtin_nan("") : 0.0)) + den};
     }
+    if (mine && lane == 0) atomicOr(&bad, 1);
+    __syncthreads();
+    if (threadIdx.x == 0) *flag = bad ? 0 : 1;
+}
+
+hipError_t launch_joint_wbound(const unsigned short *W, const float *bias, int V, int H, int *flag,
+                               hipStream_t stream) {
+    if (V <= 0 || H <= 0 || H > 1024 || (H & 7)) return hipErrorInvalidValue;
+    joint_wbound_kernel<<<1, 1024, 0, stream>>>(W, bias, V, H, flag);
+    return hipGetLastError();
 }
 
 hipError_t launch_joint_forward(const DevProblem &p, const JointArgs &j, hipStream_t stream) {
     if (kVariants && tuning().joint_probe) {
         JointArgs jp = j;
         jp.probe = tuning().joint_probe;
-        if constexpr (kVariants) {
-            if ((jp.probe & 8) && jp.H == 512 && jp.n > 0) {
-                const size_t lds = 2 * sizeof(unsigned short) * WTile<32>::ELEMS + sizeof(float) * ((p.V + 31) / 32 * 32);
-                const int64_t blocks = (jp.n + 255) / 256;
-                auto kern = joint_fwd_nomax_kernel<32, 2, 8, 2>;
-                if (hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)lds) != hipSuccess)
-                    return hipErrorInvalidValue;
-                kern<<<(int)blocks, 512, lds, stream>>>(p, jp);
-                return hipGetLastError();
-            }
-        }
+        if (jp.probe & 8) jp.wplain = nullptr;  // (A/B: the running-max epilogue whatever the bound)
         return launch_joint(p, jp, false, stream);
     }
     return launch_joint(p, j, false, stream);

@@ -340,3 +340,58 @@ def test_joint_reduce_padded_pitch_bit_identical(jop, dev, H, V, S_max):
         _, de1, dp1, dw1, _ = run_joint(jop, dev, enc, pred, w, bias, labels, T, S)
     assert torch.equal(de0, de1) and torch.equal(dp0, dp1) and torch.equal(dw0, dw1)
 
+
+
+def _check_vs_host(jop, dev, enc, pred, w, bias, labels, T, S, blank=0, cost_rel=1e-5):
+    scale = [1.0, -0.5, 2.0][: len(T)]
+    c, de, dp, dw, db = run_joint(jop, dev, enc, pred, w, bias, labels, T, S, blank=blank, scale=scale)
+    cr, de_r, dp_r, dw_r, db_r = host_reference(enc, pred, w, bias, labels, T, S, blank=blank, scale=scale)
+    assert np.all(np.isfinite(c)), c
+    assert np.all(np.abs(c - cr) <= cost_rel * np.maximum(1.0, np.abs(cr))), (c, cr)
+    close(de, de_r, name="d_enc")
+    close(dp, dp_r, name="d_pred")
+    close(dw, dw_r, name="d_weight")
+    if bias is not None:
+        close(db, db_r, name="d_bias")
+
+
+@pytest.mark.parametrize("H,V", [(512, 1000), (256, 130)])
+def test_joint_unbounded_weights_take_the_running_max(jop, dev, H, V):
+    """The forward sums exp(z) without a running max only when the device-side weight bound max_v (sum |W_v| + |b_v|)
+    is <= 64 (every |z| <= 64 since |tanh| <= 1: no fp32 overflow). Weights 50 / sqrt(H) put logits near +-170 --
+    e^170 overflows fp32 -- so the bound fails and the online log-sum-exp must run: costs finite and on the host
+    reference. Tolerance: costs 1e-5 relative (as above; the costs here are O(1e3))."""
+    enc, pred, w, bias, labels, T, S = make_case(H + V + 5, 3, (10, 40), 12, H, V)
+    w = (w.float() * 25.0).to(torch.bfloat16)
+    _check_vs_host(jop, dev, enc, pred, w, bias, labels, T, S)
+
+
+@pytest.mark.parametrize("over", [False, True])
+def test_joint_weight_bound_edge(jop, dev, over):
+    """Logits at exactly +-64 (saturated tanh, weight rows of +-1/8 at H = 512: sum |W_v| = 64, the bound's edge, the
+    plain exp-sum path) and the same weights with |bias| = 0.5 (bound 64.5: the running-max path): both on the host
+    reference (costs 1e-5 relative)."""
+    H, V = 512, 1024
+    enc, pred, w, bias, labels, T, S = make_case(3 + over, 3, (10, 30), 10, H, V)
+    enc = torch.full_like(enc, 8.0)  # tanh(8 + pred) rounds to 1 in bf16 for |pred| < ~4
+    pred = pred.clamp(-3.0, 3.0)
+    sign = torch.where(torch.arange(V) % 3 == 0, 1.0, -1.0)
+    w = (sign[:, None] * torch.full((V, H), 0.125)).to(torch.bfloat16)
+    bias = torch.full((V,), 0.5 if over else 0.0)
+    _check_vs_host(jop, dev, enc, pred, w, bias, labels, T, S)
+
+
+@pytest.mark.parametrize("H,V", [(512, 1024), (256, 1000), (640, 130)])
+def test_joint_plain_exp_sum_matches_running_max(dev, H, V):
+    """Bounded weights: the plain exp-sum forward (product) against the running-max epilogue forced on (development
+    build, joint_probe bit 3) on the same inputs: costs within 1e-6 relative (the two fp32 sums differ only in
+    rounding), gradients within 2^-7 of their max (bf16 logit-gradient rounding can flip)."""
+    import monotonic_rnnt_joint as jm
+    enc, pred, w, bias, labels, T, S = make_case(H * 3 + V, 3, (20, 60), 20, H, V)
+    a = run_joint(jm, dev, enc, pred, w, bias, labels, T, S, scale=[1.0, -0.5, 2.0])
+    with knobs(joint_probe=8):
+        b = run_joint(jm, dev, enc, pred, w, bias, labels, T, S, scale=[1.0, -0.5, 2.0])
+    assert np.all(np.abs(a[0] - b[0]) <= 1e-6 * np.maximum(1.0, np.abs(b[0]))), (a[0], b[0])
+    for x, y, name in zip(a[1:], b[1:], ("d_enc", "d_pred", "d_weight", "d_bias")):
+        err = (x.float() - y.float()).abs().max().item()
+        assert err <= 2.0 ** -7 * y.float().abs().max().item() + 1e-6, (name, err)

@@ -53,6 +53,20 @@ final)
   TAG=r05 bash $R/tools/gpu_profile.sh && \
   MODE=c2 TAG=r05final bash $R/tools/gpu_r05.sh
   rc=$?; echo rc=$rc; exit $rc ;;
+fwdab)
+  # the plain exp-sum forward (product) against the running max forced on (joint_probe bit 3)
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_joint.py -x -v -rs --timeout 300 --timeout-method thread > $O/pytest_joint.log 2>&1 && \
+  timeout -k 10 300 python tools/joint_bench.py --no-unfused --steps 5 > $O/joint_h512.json 2> $O/joint_h512.err && \
+  timeout -k 10 400 python tools/joint_bench.py --no-unfused --steps 3 --ab '[{"joint_probe":0},{"joint_probe":8}]' > $O/joint_fwd_ab.json 2> $O/joint_fwd_ab.err
+  rc=$?; echo rc=$rc; tail -n 3 $O/pytest_joint.log; cat $O/joint_h512.json; python3 -c "import json;d=json.load(open('$O/joint_fwd_ab.json'));[print(v) for v in d['ab']]"; exit $rc ;;
+libab)
+  # product library (plain exp-sum forward) against the previous commit's product library (running max, ablib/),
+  # alternating processes on one box
+  for i in 1 2 3; do \
+    timeout -k 10 200 python tools/joint_bench.py --no-unfused --steps 5 > $O/joint_new_$i.json 2> $O/joint_new_$i.err || exit 1; \
+    MRNNT_LIB_PATH=$R/ablib/lib_head_runmax.so timeout -k 10 200 python tools/joint_bench.py --no-unfused --steps 5 > $O/joint_old_$i.json 2> $O/joint_old_$i.err || exit 1; \
+  done
+  rc=$?; echo rc=$rc; for f in $O/joint_new_*.json $O/joint_old_*.json; do python3 -c "import json,sys;d=json.load(open('$f'));k=d['fused'];print('$f'.split('/')[-1],k['ms_per_step'],k['kernels_ms'])"; done; exit $rc ;;
 jtrace)
   timeout -k 10 300 python tools/joint_trace.py $O/joint_trace.json > $O/joint_trace.txt 2>&1
   rc=$?; echo rc=$rc; cat $O/joint_trace.txt | tail -6; exit $rc ;;
