@@ -1038,6 +1038,7 @@ __attribute__((visibility("default"))) int mrnnt_tune(const char *key, int value
     else if (!std::strcmp(key, "joint_dpre_nw")) slot = &t.joint_dpre_nw;
     else if (!std::strcmp(key, "joint_reduce_hact")) slot = &t.joint_reduce_hact;
     else if (!std::strcmp(key, "joint_probe")) slot = &t.joint_probe;
+    else if (!std::strcmp(key, "joint_trace")) slot = &t.joint_trace;
     else if (!std::strcmp(key, "joint_reduce_pad")) slot = &t.joint_reduce_pad;
     else if (!std::strcmp(key, "softmax_grid_per_cu")) slot = &t.softmax_grid_per_cu;
     else if (!std::strcmp(key, "grad_grid_per_cu")) slot = &t.grad_grid_per_cu;

@@ -168,6 +168,7 @@ struct Tuning {
     int joint_reduce_hact = 1;    // joint reduce: 1 reads Hact; 0 (development build) recomputes the activation from
                                   // enc / pred (the gradient pass's bits; measured slower, mrnnt_joint.hip)
     int joint_reduce_pad = 1;     // joint reduce: accumulator LDS pitch HS + 1 (0: HS, development A/B; bit-identical)
+    int joint_trace = 0;          // development build: the joint forward with its timeline stamps (tools/joint_trace.py)
     int joint_probe = 0;          // development probe: JointArgs::probe of the joint forward (results wrong)
     int joint_dpre_nw = 0;        // joint dpre GEMM (mrnnt_joint_gemm.hip): 0 -> persistent, G loaded straight into
                                   // registers, W^T through LDS (8 waves, 32 rows x 256 h each); development build: 1 the

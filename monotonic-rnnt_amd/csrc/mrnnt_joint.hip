@@ -40,6 +40,10 @@ __device__ unsigned long long g_joint_trace[kJointTraceWgs * 64];
 #else
 #define JOINT_MARK(i) ((void)0)
 #endif
+#define FWD_MARK(i)                 \
+    do {                            \
+        if constexpr (TR) JOINT_MARK(i); \
+    } while (0)
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -463,22 +467,24 @@ __device__ __forceinline__ float *load_bias(const JointArgs &j, int V, unsigned 
 }
 
 // two waves per SIMD: the compiler keeps each kernel within 256 registers per lane
-template <int KS, int NB, int NW, int RG>
+// TR: the development build's timeline stamps (JOINT_MARK), instantiated only when the joint_trace knob asks for them:
+// the stamps (a scalar clock read and a store per mark, one inside the chunk loop) cost that build's forward ~15 %
+template <int KS, int NB, int NW, int RG, bool TR = false>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2))) void joint_fwd_kernel(DevProblem p,
                                                                                              JointArgs j) {
     extern __shared__ __attribute__((aligned(16))) unsigned short wsh[];
     if ((int64_t)blockIdx.x * (32 * NW) >= list_len(j)) return;  // whole workgroup past a shorter list
-    JOINT_MARK(0);
+    FWD_MARK(0);
     const int lane = threadIdx.x & 63, half = lane >> 5;
     const int64_t i = (int64_t)blockIdx.x * (32 * NW) + (threadIdx.x >> 6) * 32 + (lane & 31);
     const RowPos q = row_pos(p, j, i);
     const int V = p.V, blank = p.blank;
     const float *bias = load_bias<KS, NB>(j, V, wsh);
     __syncthreads();
-    JOINT_MARK(1);
+    FWD_MARK(1);
     bf16x8 bfr[KS];
     build_act<KS, false>(j, q, half, i, bfr);
-    JOINT_MARK(2);
+    FWD_MARK(2);
 
     const f2 l2e = {kLog2e, kLog2e};
     float m = NEG_INF_F, sum = 0.0f, zb = 0.0f, ze = 0.0f;
@@ -509,7 +515,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     // per-chunk max / rescale chain cost 15 % of the forward. Otherwise the online log-sum-exp.
     const bool plain = j.wplain != nullptr && *j.wplain != 0;
     if (plain) {
-        chunk_loop<KS, NB, NW, RG, true>(j, V, wsh, bfr, lane, 0, [&](const f32x16 &acc, int c) {
+        chunk_loop<KS, NB, NW, RG, TR>(j, V, wsh, bfr, lane, 0, [&](const f32x16 &acc, int c) {
             f2 z[8];
             logits2(acc, bias, c, half, z);
             f2 s2 = {0.0f, 0.0f};
@@ -520,7 +526,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
             }
             sum += s2.x + s2.y;
             capture(z, c);
-            if (c == 0) JOINT_MARK(3);
+            if (c == 0) FWD_MARK(3);
         });
         sum += __shfl_xor(sum, 32);
         const float zb2 = __shfl_xor(zb, 32), ze2 = __shfl_xor(ze, 32);
@@ -532,10 +538,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
             p.den[q.row] = (float)den;
             p.lp[q.row] = Lp{(double)zb + den, (q.lab >= 0 ? (double)ze : (q.lab == -2 ? __builtin_nan("") : 0.0)) + den};
         }
-        JOINT_MARK(4);
+        FWD_MARK(4);
         return;
     }
-    chunk_loop<KS, NB, NW, RG, true>(j, V, wsh, bfr, lane, 0, [&](const f32x16 &acc, int c) {
+    chunk_loop<KS, NB, NW, RG, TR>(j, V, wsh, bfr, lane, 0, [&](const f32x16 &acc, int c) {
         f2 z[8];
         logits2(acc, bias, c, half, z);
         float cm = fmaxf(z[0].x, z[0].y);
@@ -553,7 +559,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
         sum = sum * fast_exp2((m - mr) * kLog2e) + (s2.x + s2.y);
         m = mn;
         capture(z, c);
-        if (c == 0) JOINT_MARK(3);
+        if (c == 0) FWD_MARK(3);
     });
     // merge the two lane halves (same row, disjoint vocabulary)
     const float m2 = __shfl_xor(m, 32), s2 = __shfl_xor(sum, 32);
@@ -569,7 +575,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
         p.den[q.row] = (float)den;
         p.lp[q.row] = Lp{(double)zb + den, (q.lab >= 0 ? (double)ze : (q.lab == -2 ? __builtin_nan("") : 0.0)) + den};
     }
-    JOINT_MARK(4);
+    FWD_MARK(4);
 }
 
 #ifdef MRNNT_DEVTOOLS
@@ -1151,7 +1157,11 @@ static hipError_t launch_knw(const DevProblem &p, const JointArgs &j, size_t lds
     void (*kern)(DevProblem, JointArgs);
     if constexpr (MF == 16 && BWD) kern = joint_bwd16_kernel<KS, NB, NW>;
     else if constexpr (BWD) kern = joint_bwd_kernel<KS, NB, NW, RG>;
-    else kern = joint_fwd_kernel<KS, NB, NW, RG>;
+    else {
+        kern = joint_fwd_kernel<KS, NB, NW, RG>;
+        if constexpr (kVariants)
+            if (tuning().joint_trace) kern = joint_fwd_kernel<KS, NB, NW, RG, true>;
+    }
     if (lds > 65536) {
         const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -27,6 +27,7 @@ labels = torch.from_numpy(np.random.default_rng(1).integers(1, V, (B, S)).astype
 Tl = torch.full((B,), T, dtype=torch.int32)
 Sl = torch.full((B,), S, dtype=torch.int32)
 lib = L.load_dev()
+L.tune("joint_trace", 1)  # the forward instantiation with the stamps (the default one has none)
 out = {}
 for probe in (0, 1):
     L.tune("joint_probe", probe)
@@ -58,4 +59,5 @@ for probe in (0, 1):
         out[f"joint_probe={probe}"].append(res)
         print(probe, json.dumps(res), flush=True)
 L.tune("joint_probe", 0)
+L.tune("joint_trace", 0)
 json.dump(out, open(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/joint_trace.json", "w"), indent=1)
