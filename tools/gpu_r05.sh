@@ -67,6 +67,15 @@ libab)
     MRNNT_LIB_PATH=$R/ablib/lib_head_runmax.so timeout -k 10 200 python tools/joint_bench.py --no-unfused --steps 5 > $O/joint_old_$i.json 2> $O/joint_old_$i.err || exit 1; \
   done
   rc=$?; echo rc=$rc; for f in $O/joint_new_*.json $O/joint_old_*.json; do python3 -c "import json,sys;d=json.load(open('$f'));k=d['fused'];print('$f'.split('/')[-1],k['ms_per_step'],k['kernels_ms'])"; done; exit $rc ;;
+post)
+  # after the development-build stamp change: the forward A/B again, the headline bench line (carrying the PMC
+  # traffic record of the same sources), the joint random sweep over the plain / running-max forward, then the sweeps
+  MODE=fwdab TAG=${TAG:-r05} bash $R/tools/gpu_r05.sh && \
+  timeout -k 10 300 python bench.py > $O/bench_post.json 2> $O/bench_post.err && \
+  mkdir -p $O/tests && \
+  MRNNT_JOINT_CASES=120 MRNNT_FUZZ_FIRST=9000 timeout -k 10 500 python -u -m pytest tests/test_gpu_joint.py -k test_joint_random_cases -q --timeout 300 --timeout-method thread > $O/tests/joint_fuzz_120_seed9000.log 2>&1
+  rc=$?; echo rc=$rc; cat $O/bench_post.json; tail -n 2 $O/tests/joint_fuzz_120_seed9000.log; [ $rc = 0 ] || exit $rc
+  MODE=sweeps TAG=${TAG:-r05} bash $R/tools/gpu_r05.sh; exit $? ;;
 jtrace)
   timeout -k 10 300 python tools/joint_trace.py $O/joint_trace.json > $O/joint_trace.txt 2>&1
   rc=$?; echo rc=$rc; cat $O/joint_trace.txt | tail -6; exit $rc ;;
