@@ -76,6 +76,11 @@ post)
   MRNNT_JOINT_CASES=120 MRNNT_FUZZ_FIRST=9000 timeout -k 10 500 python -u -m pytest tests/test_gpu_joint.py -k test_joint_random_cases -q --timeout 300 --timeout-method thread > $O/tests/joint_fuzz_120_seed9000.log 2>&1
   rc=$?; echo rc=$rc; cat $O/bench_post.json; tail -n 2 $O/tests/joint_fuzz_120_seed9000.log; [ $rc = 0 ] || exit $rc
   MODE=sweeps TAG=${TAG:-r05} bash $R/tools/gpu_r05.sh; exit $? ;;
+probeab)
+  # the forward's load probes again in the unstamped development build (1: every pred load on row 0, 2: every enc load
+  # on frame 0; results wrong, timing only), interleaved in one process
+  timeout -k 10 400 python tools/joint_bench.py --no-unfused --steps 3 --ab-rounds 4 --ab '[{"joint_probe":0},{"joint_probe":1},{"joint_probe":2},{"joint_probe":3}]' > $O/joint_probe_ab.json 2> $O/joint_probe_ab.err
+  rc=$?; echo rc=$rc; python3 -c "import json;d=json.load(open('$O/joint_probe_ab.json'));[print(v['knobs'],v['step_ms_median'],v['median_ms']) for v in d['ab']]"; exit $rc ;;
 jtrace)
   timeout -k 10 300 python tools/joint_trace.py $O/joint_trace.json > $O/joint_trace.txt 2>&1
   rc=$?; echo rc=$rc; cat $O/joint_trace.txt | tail -6; exit $rc ;;
