@@ -111,6 +111,10 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="host threads for the CPU baseline (0 = this process's CPU share: affinity / cgroup quota)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--acts-dist", default="normal", choices=["normal", "uniform"],
+                    help="synthetic logit distribution: counter-hash N(0,1)-like (default) or U[0,1), the reference's "
+                         "own generator's distribution (tests/random.cpp:4-20); the gradient kernel's bytes depend on "
+                         "it through the live-row fraction")
     ap.add_argument("--acts-dtype", default="f32", choices=["f32", "bf16", "f16"],
                     help="element type of acts/grads (extension; the headline metric is f32, the reference's type)")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
@@ -273,13 +277,14 @@ def run(args, world):
     max_chunk_rows = max(int(crow[hi] - crow[lo]) for lo, hi in chunks)
 
     stream_h = torch.cuda.current_stream(dev).cuda_stream
+    normal = args.acts_dist == "normal"
     acts_buf = torch.empty((max_chunk_rows, V), dtype=torch.float32, device=dev)
     labels_all = labels_for(args.config, scaling, cfg_rank, cfg_world, B, max(1, int(S.max())), V)
     labels_dev = torch.from_numpy(labels_all).to(dev)
 
     def synth(lo, hi):
         n = int(crow[hi] - crow[lo])
-        L.synth_acts(acts_buf.data_ptr(), (row0 + int(crow[lo])) * V, n * V, 0, True, stream_h)
+        L.synth_acts(acts_buf.data_ptr(), (row0 + int(crow[lo])) * V, n * V, 0, normal, stream_h)
         return acts_buf[:n]
 
     align = n_window = None
@@ -488,7 +493,7 @@ def run(args, world):
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_sample > 0 and args.acts_dtype == "f32":
-        cpu = cpu_baseline(op, T, S, V, labels_all, row0, args.cpu_sample, args.cpu_threads)
+        cpu = cpu_baseline(op, T, S, V, labels_all, row0, args.cpu_sample, args.cpu_threads, normal)
 
     if rank == 0:
         out = {
@@ -503,10 +508,10 @@ def run(args, world):
             "scaling": scaling,
             "vs_baseline": None,
             "dtype": args.acts_dtype,
-            "data": "synthetic: counter-hash N(0,1)-like acts (seed 0), labels U[1,V-1] (seed 1+rank; configs[3]: seed 1 over the global batch); inputs resident in HBM",
+            "data": f"synthetic: counter-hash {'N(0,1)-like' if normal else 'U[0,1)'} acts (seed 0), labels U[1,V-1] (seed 1+rank; configs[3]: seed 1 over the global batch); inputs resident in HBM",
             "config": {"workload": workload, "utterances_per_gpu": B, "global_batch": total_utts,
                        "rows_per_gpu": rows, "inband_rows_per_gpu": n_band, "V": V,
-                       "memory_mode": mode, "chunks_per_step": n_chunks,
+                       "acts_dist": args.acts_dist, "memory_mode": mode, "chunks_per_step": n_chunks,
                        "execution": "hip_graph_replay" if args.graph else "eager",
                        "lengths": "device" if (device_lengths or mode != "resident") else "host",
                        "rank_devices": rank_devices,
@@ -720,7 +725,7 @@ def cpu_worker(job):
     V = int(job["V"])
     labels = np.asarray(job["labels"], np.int32)
     rows = int(np.sum(T.astype(np.int64) * (S + 1)))
-    acts = O.synth_acts(int(job["begin"]), rows * V, seed=0).reshape(rows, V)
+    acts = O.synth_acts(int(job["begin"]), rows * V, seed=0, normal=bool(job.get("normal", True))).reshape(rows, V)
     fn = O.ref_rnnt if job["kind"] == "reference" else O.oracle_rnnt
     t0 = time.perf_counter()
     costs, _ = fn(acts, labels, T, S, precision="f32", num_threads=int(job["threads"]))
@@ -729,7 +734,7 @@ def cpu_worker(job):
     return 0
 
 
-def cpu_baseline(op, T, S, V, labels, row0, n_sample, threads_arg=0):
+def cpu_baseline(op, T, S, V, labels, row0, n_sample, threads_arg=0, normal=True):
     """Time the reference CPU path on the first n_sample utterances of the same synthetic workload, using the
     host's CPU share. The reference indexes acts with 32-bit offsets (cpu_workspace_manager.h:48,125-135) and
     parallelises over utterances only (cpu_rnnt.h:54-57), so one call takes at most 2^31 / (rows per utterance
@@ -755,7 +760,7 @@ def cpu_baseline(op, T, S, V, labels, row0, n_sample, threads_arg=0):
         lo, hi = int(bounds[c]), int(bounds[c + 1])
         job = {"T": T[lo:hi].tolist(), "S": S[lo:hi].tolist(), "V": V,
                "labels": labels[lo:hi, :max(1, int(S[lo:hi].max()))].tolist(),
-               "begin": int((row0 + crow[lo]) * V), "kind": kind, "threads": threads[c]}
+               "begin": int((row0 + crow[lo]) * V), "kind": kind, "threads": threads[c], "normal": normal}
         env = dict(os.environ, OMP_NUM_THREADS=str(threads[c]))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-worker", json.dumps(job)],
                                       stdout=subprocess.PIPE, env=env, text=True))
@@ -774,17 +779,17 @@ def cpu_baseline(op, T, S, V, labels, row0, n_sample, threads_arg=0):
                      f"call: 32-bit offsets), cost_and_grad at fp32, OpenMP over utterances, slowest call "
                      f"{wall:.2f} s",
            "finite": all(r["finite"] for r in res)}
-    out["product_cpu"] = product_cpu_rate(op, T[:n], S[:n], V, labels[:n], row0, cores)
+    out["product_cpu"] = product_cpu_rate(op, T[:n], S[:n], V, labels[:n], row0, cores, normal)
     return out
 
 
-def product_cpu_rate(op, T, S, V, labels, row0, threads):
+def product_cpu_rate(op, T, S, V, labels, row0, threads, normal=True):
     """The library's own host implementation (RNNT_CPU, cpu_monotonic_rnnt) on the same sample: one call,
     OpenMP over lattice columns on every core of the share. Reported next to the reference baseline."""
     import torch
     import oracle as O
     rows = int(np.sum(T.astype(np.int64) * (S + 1)))
-    acts = torch.from_numpy(O.synth_acts(row0 * V, rows * V, seed=0).reshape(rows, V))
+    acts = torch.from_numpy(O.synth_acts(row0 * V, rows * V, seed=0, normal=normal).reshape(rows, V))
     grads = torch.empty_like(acts)
     costs = torch.zeros(len(T))
     lab = torch.from_numpy(np.ascontiguousarray(labels[:, :max(1, int(S.max()))]))

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MRNNT_VERSION 10
+#define MRNNT_VERSION 11
 
 /* acts / grads element types */
 #define MRNNT_F32 0
@@ -235,18 +235,23 @@ RNNTStatus mrnnt_joint_backward(const mrnnt_joint_problem *p, void *workspace, i
  * tiles (mrnnt_joint_gemm.hip): the dH GEMM with the tanh derivative in its epilogue. weight_t is the weight
  * transposed, bf16 [H, V] row-major; Hact as mrnnt_joint_backward wrote it (row stride p->hact_ld, 0 = H). Needs
  * H = 256 or 512 and V a multiple of 8 (RNNT_STATUS_INVALID_VALUE otherwise: use a library GEMM for dH and
- * mrnnt_joint_reduce with Hact). Pass dpre to mrnnt_joint_reduce with Hact = NULL. */
+ * mrnnt_joint_reduce with Hact). Sum dpre with mrnnt_joint_reduce_pre. */
 RNNTStatus mrnnt_joint_dpre(const mrnnt_joint_problem *p, int64_t n_live, const void *G, const void *weight_t,
                             const void *Hact, void *dpre, hipStream_t stream);
 
 /* After mrnnt_joint_backward, with dH = G weight (bf16 [n_live, H], e.g. a library GEMM): accumulate
  * dpre = dH * (1 - Hact^2) into d_enc (fp32, enc's [B, enc_stride/H, H] shape; rows (b, t < T_b) are
  * overwritten) and d_pred (fp32, pred's shape; added to: zero it first). Zero d_enc's padding rows yourself.
- * Hact = NULL (version 10): dH already holds dpre (mrnnt_joint_dpre) and is summed as it is.
- * Every sum has a fixed order (bitwise reproducible). p->reduce_scratch (version 9) lets it run on blocks of frames
+ * Hact is required (RNNT_STATUS_INVALID_VALUE when NULL with n_live > 0). Every sum has a fixed order (bitwise reproducible). p->reduce_scratch (version 9) lets it run on blocks of frames
  * whose d_pred sums are then added in block order; see mrnnt_joint_reduce_scratch_bytes. */
 RNNTStatus mrnnt_joint_reduce(const mrnnt_joint_problem *p, void *workspace, int64_t n_live, const void *dH,
                               const void *Hact, float *d_enc, float *d_pred, hipStream_t stream);
+
+/* (version 11) mrnnt_joint_reduce for a dH that already holds dpre = dH * (1 - Hact^2) (mrnnt_joint_dpre's output,
+ * bf16 [n_live, H]): the same sums of dpre into d_enc / d_pred, in the same fixed order. (Version 10 signalled this
+ * with Hact = NULL on mrnnt_joint_reduce, which made a forgotten Hact a silent wrong gradient.) */
+RNNTStatus mrnnt_joint_reduce_pre(const mrnnt_joint_problem *p, void *workspace, int64_t n_live, const void *dpre,
+                                  float *d_enc, float *d_pred, hipStream_t stream);
 
 /* (version 9) Bytes of p->reduce_scratch for the blocked form of mrnnt_joint_reduce. */
 RNNTStatus mrnnt_joint_reduce_scratch_bytes(const mrnnt_joint_problem *p, size_t *bytes);

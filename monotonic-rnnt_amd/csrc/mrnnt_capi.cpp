@@ -912,20 +912,24 @@ RNNTStatus mrnnt_joint_backward(const mrnnt_joint_problem *jp, void *ws, int64_t
     return RNNT_STATUS_SUCCESS;
 }
 
-RNNTStatus mrnnt_joint_reduce(const mrnnt_joint_problem *jp, void *ws, int64_t n_live, const void *dH,
-                              const void *Hact, float *d_enc, float *d_pred, hipStream_t stream) {
+// pre: dH already holds dpre (Hact unused; the kRedPre kernel form)
+static RNNTStatus joint_reduce(const mrnnt_joint_problem *jp, void *ws, int64_t n_live, const void *dH,
+                               const void *Hact, bool pre, float *d_enc, float *d_pred, hipStream_t stream) {
     JointPlan jl;
     RNNTStatus st = make_joint_plan(jp, &jl);
     if (st != RNNT_STATUS_SUCCESS) return st;
     if ((st = check_joint_pointers(jp)) != RNNT_STATUS_SUCCESS) return st;
     if (!ws || !d_enc || !d_pred) return fail(RNNT_STATUS_INVALID_VALUE, "workspace / d_enc / d_pred is null");
     if (n_live < 0 || n_live > jl.n_inband) return fail(RNNT_STATUS_INVALID_VALUE, "n_live outside [0, in-band rows]");
-    if (n_live > 0 && (!dH || (reinterpret_cast<uintptr_t>(dH) & 7) || (reinterpret_cast<uintptr_t>(Hact) & 7)))
-        return fail(RNNT_STATUS_INVALID_VALUE, "dH null or dH / Hact not 8-byte aligned");
+    if (n_live > 0 && (!dH || (reinterpret_cast<uintptr_t>(dH) & 7)))
+        return fail(RNNT_STATUS_INVALID_VALUE, pre ? "dpre null or not 8-byte aligned" : "dH null or not 8-byte aligned");
+    if (!pre && n_live > 0 && (!Hact || (reinterpret_cast<uintptr_t>(Hact) & 7)))
+        return fail(RNNT_STATUS_INVALID_VALUE, "Hact null or not 8-byte aligned (a dH that already holds dpre: "
+                                               "mrnnt_joint_reduce_pre)");
     const mrnnt_problem p = base_problem(jp);
     DevProblem d = make_dev(&p, jl.base, ws);
     JointArgs j = joint_args(jp, jl, ws, n_live);
-    j.Hact = static_cast<unsigned short *>(const_cast<void *>(Hact));
+    j.Hact = pre ? nullptr : static_cast<unsigned short *>(const_cast<void *>(Hact));
     const int64_t *off = reinterpret_cast<const int64_t *>(static_cast<char *>(ws) + jl.off_cnt);
     const hipError_t e = timed(K_JOINT_RED, stream, [&] {
         return launch_joint_reduce(d, j, off, jl.base.T_max, jl.base.S_max, static_cast<const unsigned short *>(dH),
@@ -933,6 +937,16 @@ RNNTStatus mrnnt_joint_reduce(const mrnnt_joint_problem *jp, void *ws, int64_t n
     });
     if (e != hipSuccess) return fail_hip(e, "joint reduce kernel");
     return RNNT_STATUS_SUCCESS;
+}
+
+RNNTStatus mrnnt_joint_reduce(const mrnnt_joint_problem *jp, void *ws, int64_t n_live, const void *dH,
+                              const void *Hact, float *d_enc, float *d_pred, hipStream_t stream) {
+    return joint_reduce(jp, ws, n_live, dH, Hact, false, d_enc, d_pred, stream);
+}
+
+RNNTStatus mrnnt_joint_reduce_pre(const mrnnt_joint_problem *jp, void *ws, int64_t n_live, const void *dpre,
+                                  float *d_enc, float *d_pred, hipStream_t stream) {
+    return joint_reduce(jp, ws, n_live, dpre, nullptr, true, d_enc, d_pred, stream);
 }
 
 RNNTStatus mrnnt_joint_dpre(const mrnnt_joint_problem *jp, int64_t n_live, const void *G, const void *weight_t,

@@ -1106,7 +1106,7 @@ hipError_t launch_joint_reduce(const DevProblem &p, const JointArgs &j_in, const
     const bool pre = j.Hact == nullptr;  // dH holds dpre (mrnnt_joint_dpre)
     const bool sparse = kVariants && tuning().joint_reduce_sparse == 2 && !pre;
     const bool tanh_src = kVariants && tuning().joint_reduce_hact == 0 && !pre;
-    auto go = [&](auto hs_tag) {
+    auto go = [&](auto hs_tag) -> hipError_t {
         constexpr int HS = decltype(hs_tag)::value;
         // (accumulator pitch HS + 1; the development build's joint_reduce_pad = 0 runs pitch HS, bit-identical)
         constexpr int AP = HS + 1;
@@ -1120,14 +1120,16 @@ hipError_t launch_joint_reduce(const DevProblem &p, const JointArgs &j_in, const
             const size_t lds = sizeof(float) * ((size_t)W * HS + (size_t)kReduceTT * HS);
             joint_reduce_sparse_kernel<HS><<<p.B * ntb * (j.H / HS), 256, lds, stream>>>(p, j, off, dH, d_enc,
                                                                                           d_pred, ntb);
-            return;
+            return hipSuccess;
         }
         // (+ the staged pred slice, bf16 [W][HS], of the recomputing form: up to 88 KiB)
         const size_t lds = sizeof(float) * ((size_t)W * apitch + 256 / (HS / 4) * apitch) +
                            (tanh_src ? sizeof(unsigned short) * W * HS : 0);
-        if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-            return;  // (the launch below then fails and reports)
+        if (lds > 65536) {  // (no launch with too little LDS: the attribute's failure is the call's error)
+            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+        }
         if (scratch && scratch_bytes >= joint_reduce_scratch_bytes(p.B, T_max, S_max, j.H)) {
             // blocks of kReduceTT frames, their d_pred sums added in block order by pred_sum_kernel
             float *part = static_cast<float *>(scratch);
@@ -1139,14 +1141,15 @@ hipError_t launch_joint_reduce(const DevProblem &p, const JointArgs &j_in, const
         } else {  // one block per utterance (no scratch)
             kern<<<p.B * (j.H / HS), 256, lds, stream>>>(p, j, off, dH, d_enc, d_pred, T_max, 1, W, nullptr, nullptr);
         }
+        return hipSuccess;
     };
     if ((int64_t)p.B * ntb * (j.H / 4) > (1ll << 24)) return hipErrorInvalidValue;  // 32-bit dispatch size
     // LDS = W * HS fp32 + 4 KiB + W * HS bf16: about 43 KiB at the headline (three workgroups per CU), <= 88 KiB
-    if (W <= 448) go(std::integral_constant<int, 32>());
-    else if (W <= 896) go(std::integral_constant<int, 16>());
-    else if (W <= 1792) go(std::integral_constant<int, 8>());
-    else go(std::integral_constant<int, 4>());
-    return hipGetLastError();
+    const hipError_t e = W <= 448    ? go(std::integral_constant<int, 32>())
+                         : W <= 896  ? go(std::integral_constant<int, 16>())
+                         : W <= 1792 ? go(std::integral_constant<int, 8>())
+                                     : go(std::integral_constant<int, 4>());
+    return e != hipSuccess ? e : hipGetLastError();
 }
 
 // kernel of a launch shape: MF = the backward's MFMA tile (32: 32x32x16, 16: 16x16x32); the forward runs 32x32x16

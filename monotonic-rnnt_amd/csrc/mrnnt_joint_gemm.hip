@@ -87,8 +87,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4,
         unsigned char *s = glds + (c % kGStages) * kGStageBytes;
 #pragma unroll
         for (int i = 0; i < DPI; ++i) {
-            gemm_dma(rg, s + 1024 * (DPI * wave + i), voff[i], (unsigned)(c * kGKC * 2));
-            gemm_dma(rw, s + kGImage + 1024 * (DPI * wave + i), voff[i], (unsigned)(c * kGKC * 2));
+            gemm_dma(rg, s + 1024 * (DPI * wave + i), voff[i] + (unsigned)(c * kGKC * 2), 0u);
+            gemm_dma(rw, s + kGImage + 1024 * (DPI * wave + i), voff[i] + (unsigned)(c * kGKC * 2), 0u);
         }
     };
 #pragma unroll
@@ -163,6 +163,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4,
     }
 }
 
+// Every buffer access below puts the whole offset (row, piece and k chunk) in voffset, none in soffset: a raw buffer's
+// range check covers voffset (+ the instruction offset) only, so a tail chunk's k offset in soffset would let the
+// last row of a resource read past its end.
+//
 // The default form (joint_dpre_nw = 0): only W^T goes through LDS; each wave owns 32 rows x all 256 hidden units of
 // the tile (8 x 1 tiles, 128 accumulator registers) and loads its rows of G straight into the B operand with 16-byte
 // global loads -- every G element reaches the CU once, and the LDS-DMA per MFMA is half the staged forms' (the DMA
@@ -251,13 +255,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     auto stage = [&](int c) {
         unsigned char *s = glds + (c % kDStages) * kDImage;
 #pragma unroll
-        for (int i = 0; i < DPI; ++i) gemm_dma(rw, s + 1024 * (DPI * wave + i), wvoff[i], (unsigned)(c * kDKC * 2));
+        for (int i = 0; i < DPI; ++i) gemm_dma(rw, s + 1024 * (DPI * wave + i), wvoff[i] + (unsigned)(c * kDKC * 2), 0u);
     };
     auto gload = [&](int c, gbf16x8 (&f)[4]) {
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks)
             f[ks] = __builtin_bit_cast(gbf16x8, __builtin_amdgcn_raw_buffer_load_b128(
-                                                    rg, gvoff + 16u * ks, (unsigned)(c * kDKC * 2), 0));
+                                                    rg, gvoff + 16u * ks + (unsigned)(c * kDKC * 2), 0u, 0));
     };
 #pragma unroll
     for (int c = 0; c < kDStages - 1; ++c)
@@ -387,7 +391,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             const_cast<unsigned short *>(Wt) + (int64_t)x.h0 * V, (short)0, kGT * V * 2, 0x00020000);
         unsigned char *s = glds + (q % kDStages) * kDImage;
 #pragma unroll
-        for (int i = 0; i < DPI; ++i) gemm_dma(rw, s + 1024 * (DPI * wave + i), wvoff[i], (unsigned)(c * kDKC * 2));
+        for (int i = 0; i < DPI; ++i) gemm_dma(rw, s + 1024 * (DPI * wave + i), wvoff[i] + (unsigned)(c * kDKC * 2), 0u);
     };
     auto gload = [&](int q, gbf16x8 (&f)[4]) {
         if (q >= nq) return;
@@ -398,7 +402,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks)
             f[ks] = __builtin_bit_cast(gbf16x8, __builtin_amdgcn_raw_buffer_load_b128(
-                                                    rg, gvoff + 16u * ks, (unsigned)(c * kDKC * 2), 0));
+                                                    rg, gvoff + 16u * ks + (unsigned)(c * kDKC * 2), 0u, 0));
     };
     auto is_last_full = [&](int q) {  // q ends a tile whose 256 rows are all valid (its epilogue issued kEpi ops)
         if (q < 0) return false;

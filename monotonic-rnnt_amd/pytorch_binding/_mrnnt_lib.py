@@ -152,6 +152,7 @@ def _bind(path: str, dev: bool = False) -> ctypes.CDLL:
         "mrnnt_joint_live_rows": (i, [JP, vp, vp, vp]),
         "mrnnt_joint_backward": (i, [JP, vp, i64, vp, vp, vp, vp, vp, vp]),
         "mrnnt_joint_reduce": (i, [JP, vp, i64, vp, vp, vp, vp, vp]),
+        "mrnnt_joint_reduce_pre": (i, [JP, vp, i64, vp, vp, vp, vp]),
         "mrnnt_joint_reduce_scratch_bytes": (i, [JP, ctypes.POINTER(sz)]),
         "mrnnt_joint_dpre": (i, [JP, i64, vp, vp, vp, vp, vp]),
         "mrnnt_last_error": (ctypes.c_char_p, []),
@@ -174,8 +175,8 @@ def _bind(path: str, dev: bool = False) -> ctypes.CDLL:
             raise ImportError(f"{path} does not export {name}")
         fn.restype = res
         fn.argtypes = args
-    if lib.mrnnt_version() < 10:
-        raise ImportError(f"{path} is a stale build (ABI version {lib.mrnnt_version()} < 10); "
+    if lib.mrnnt_version() < 11:
+        raise ImportError(f"{path} is a stale build (ABI version {lib.mrnnt_version()} < 11); "
                           "rebuild with `make -C monotonic-rnnt_amd`")
     return lib
 

@@ -152,7 +152,7 @@ class _JointPrepared:
 
     def reduce(self, ws, dH, Hact, need_enc, need_pred, scratch=None):
         """d_enc / d_pred (fp32) from dH = G weight over the live rows (mrnnt_joint_reduce); Hact None: dH is already
-        dpre (mrnnt_joint_dpre). scratch: a dead device buffer (G, once dH exists) for the blocked form; a fresh one is
+        dpre (mrnnt_joint_dpre), summed by mrnnt_joint_reduce_pre. scratch: a dead device buffer (G, once dH exists) for the blocked form; a fresh one is
         allocated when it is too small."""
         d_enc = torch.zeros(self.enc.shape, dtype=torch.float32, device=self.device)
         d_pred = torch.zeros(self.pred.shape, dtype=torch.float32, device=self.device)
@@ -164,9 +164,14 @@ class _JointPrepared:
         self.problem.reduce_scratch = scratch.data_ptr()
         self.problem.reduce_scratch_bytes = scratch.numel() * scratch.element_size()
         with torch.cuda.device(self.device):
-            _L.check(_L.load().mrnnt_joint_reduce(ctypes.byref(self.problem), _vp(ws), dH.shape[0], _vp(dH),
-                                                  _vp(Hact), _vp(d_enc), _vp(d_pred), self.stream()),
-                     "mrnnt_joint_reduce")
+            if Hact is None:  # dH holds dpre (mrnnt_joint_dpre)
+                _L.check(_L.load().mrnnt_joint_reduce_pre(ctypes.byref(self.problem), _vp(ws), dH.shape[0], _vp(dH),
+                                                          _vp(d_enc), _vp(d_pred), self.stream()),
+                         "mrnnt_joint_reduce_pre")
+            else:
+                _L.check(_L.load().mrnnt_joint_reduce(ctypes.byref(self.problem), _vp(ws), dH.shape[0], _vp(dH),
+                                                      _vp(Hact), _vp(d_enc), _vp(d_pred), self.stream()),
+                         "mrnnt_joint_reduce")
         return d_enc if need_enc else None, d_pred if need_pred else None
 
 

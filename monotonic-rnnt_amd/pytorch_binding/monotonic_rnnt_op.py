@@ -281,8 +281,13 @@ class _Prepared:
         n = cache.get(key)
         if n is None:
             c = ctypes.c_size_t(0)
-            fn = _L.load().mrnnt_workspace_size if self.on_gpu else _L.load().mrnnt_cpu_workspace_size
-            _L.check(fn(ctypes.byref(self.problem), ctypes.byref(c)), "workspace_size")
+            if self.on_gpu:  # the plan reads the CU count of the CURRENT device: make it this call's
+                with _on_device(self.device):
+                    _L.check(_L.load().mrnnt_workspace_size(ctypes.byref(self.problem), ctypes.byref(c)),
+                             "workspace_size")
+            else:
+                _L.check(_L.load().mrnnt_cpu_workspace_size(ctypes.byref(self.problem), ctypes.byref(c)),
+                         "workspace_size")
             n = cache[key] = max(1, c.value)
             if self.dyn and len(_DYN_WS) > 256:
                 _DYN_WS.clear()

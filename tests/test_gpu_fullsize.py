@@ -137,6 +137,40 @@ def test_subset_matches_oracle(headline):
         assert np.abs(gg - gr[i * rows_per: (i + 1) * rows_per]).max() <= 1e-4
 
 
+def test_uniform_acts_subset_matches_oracle():
+    """The reference's own input distribution (tests/random.cpp:4-20: U[0,1) logits) at the headline lattice size:
+    8 full utterances (T, S, V) = (1000, 200, 1024) generated on the device with the uniform counter-hash generator
+    (bench.py --acts-dist uniform), lengths on the device, every cost and gradient element against the fp64 oracle.
+    Uniform logits are flat, so far more in-band rows carry occupancy than with N(0,1) logits: the occupancy skip's
+    decisions are exercised on a different live set (the count is printed)."""
+    import _mrnnt_lib as L
+    import monotonic_rnnt_op as op
+    dev = torch.device("cuda:0")
+    Bu, rows_per = 8, T * (S + 1)
+    rows = Bu * rows_per
+    begin = 5 * rows_per * V  # an offset into the generator's stream: not the headline batch's first utterances
+    acts = torch.empty((rows, V), dtype=torch.float32, device=dev)
+    L.synth_acts(acts.data_ptr(), begin, rows * V, 0, 0, torch.cuda.current_stream().cuda_stream)
+    labels = np.random.default_rng(21).integers(1, V, (Bu, S)).astype(np.int32)
+    c, g = _loss_and_grad(op, acts, torch.from_numpy(labels).to(dev), torch.full((Bu,), T, dtype=torch.int32, device=dev),
+                          torch.full((Bu,), S, dtype=torch.int32, device=dev))
+    c = c.cpu().numpy().astype(np.float64)
+    host = O.synth_acts(begin, rows * V, seed=0, normal=False).reshape(rows, V)
+    assert np.array_equal(host[:rows_per], acts[:rows_per].cpu().numpy())  # device generator == host twin
+    assert host.min() >= 0.0 and host.max() < 1.0
+    live = int((g.abs().amax(dim=1) != 0).sum().item())
+    n_band = Bu * ((S + 1) * (T - S + 1) - 1)
+    print(f"uniform acts: {live} of {n_band} in-band rows carry a nonzero gradient ({live / n_band:.3f})")
+    cr, gr = O.oracle_rnnt(host, labels, [T] * Bu, [S] * Bu, precision="f64", num_threads=8)
+    del host
+    assert np.all(np.abs(c - cr) <= 1e-4 * np.abs(cr))
+    for i in range(Bu):
+        gg = g[i * rows_per: (i + 1) * rows_per].cpu().numpy()
+        assert np.abs(gg - gr[i * rows_per: (i + 1) * rows_per]).max() <= 1e-4
+    del acts, g
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.skipif(os.environ.get("MRNNT_FULL_BATCH", "0") != "1",
                     reason="opt-in (MRNNT_FULL_BATCH=1): all 64 headline utterances against the oracle, ~2 min on "
                            "the box's 16 cores; its last run is recorded under profiles/r03/tests/")

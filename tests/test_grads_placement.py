@@ -17,13 +17,14 @@ class Fake:
     storage use count 2 when nothing else uses it: allocator_refs=1); a block the arena lets go of (on_release) is
     free again unless `busy` (another stream still uses it: the device allocator holds such a block back until
     that stream passes its event), and alloc() hands a free block of the size back, as the device allocator's best
-    fit does."""
+    fit does (of two free blocks of the size, the one released first: a deterministic order -- CPU addresses are not,
+    so ordering by address made the take-back test depend on where the host allocator put the two blocks)."""
 
     def __init__(self, rates, free=1 << 60):
         self.rates = list(rates)
         self.free = free
         self.blocks = {}    # data_ptr -> tensor
-        self.freed = set()
+        self.freed = {}     # data_ptr -> None, in release order
         self.allocs = []    # data_ptr of every block handed out, in order
         self.busy = set()
         self.released = 0
@@ -32,9 +33,9 @@ class Fake:
         return self.rates.pop(0)
 
     def alloc(self, n, dev):
-        for q in sorted(self.freed):
+        for q in list(self.freed):
             if self.blocks[q].numel() == n and q not in self.busy:
-                self.freed.discard(q)
+                del self.freed[q]
                 blk = self.blocks[q]
                 break
         else:
@@ -44,12 +45,12 @@ class Fake:
         return torch.empty(0, dtype=torch.uint8).set_(blk.untyped_storage())
 
     def on_release(self, ptr):
-        self.freed.add(ptr)
+        self.freed[ptr] = None
 
     def release_unused(self):
         self.released += 1
         for q in [q for q in self.freed if q not in self.busy]:
-            self.freed.discard(q)
+            del self.freed[q]
             del self.blocks[q]
 
     def arena(self, **kw):
