@@ -1,0 +1,34 @@
+# Round-6 GPU steps, chained with && (each under its own time limit); MODE picks the set. Output under
+# gpurun_out/$TAG (default r06).
+#   first : joint tests + the new uniform-acts oracle test, headline bench lines on N(0,1) / U[0,1) logits and with
+#           every in-band row live (development build, occ_skip=0), then the joint step's kernel stats + SQ counters on
+#           the shipping library
+#   full  : every gpu-marked test, smoke(), the default bench line, configs[1] graph bench
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/${TAG:-r06}
+mkdir -p $O
+cd $R
+sha() { python3 -c "import hashlib,sys;print(hashlib.sha256(open(sys.argv[1],'rb').read()).hexdigest())" $1; }
+case ${MODE:-full} in
+first)
+  sha monotonic-rnnt_amd/libmonotonic_rnnt_amd.so > $O/lib_sha256.txt
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_joint.py -x -q -rs --timeout 300 --timeout-method thread > $O/pytest_joint.log 2>&1 && \
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_fullsize.py -x -v -rs -s --timeout 300 --timeout-method thread -k uniform > $O/pytest_uniform.log 2>&1 && \
+  timeout -k 10 300 python bench.py > $O/bench_normal.json 2> $O/bench_normal.err && \
+  timeout -k 10 300 python bench.py --acts-dist uniform > $O/bench_uniform.json 2> $O/bench_uniform.err && \
+  timeout -k 10 300 python bench.py --tune occ_skip=0 --no-cpu > $O/bench_allrows.json 2> $O/bench_allrows.err && \
+  timeout -k 10 300 python bench.py --acts-dist uniform --tune occ_skip=0 --no-cpu > $O/bench_uniform_allrows.json 2> $O/bench_uniform_allrows.err && \
+  TAG=r06 bash tools/gpu_joint_profile.sh > $O/joint_profile.txt 2>&1
+  rc=$?; echo rc=$rc; tail -n 2 $O/pytest_joint.log $O/pytest_uniform.log
+  for f in normal uniform allrows uniform_allrows; do python3 -c "
+import json,sys;d=json.load(open('$O/bench_$f.json'));r=d['roofline'];k=d['kernels']
+print('$f',d['value'],d['ms_per_step'],'live',r['live_rows'],'/',r['inband_rows'],'frac',r['frac'],'grad',k['grad']['avg_ms'],'lsm',k['log_softmax']['avg_ms'])"; done
+  cat $O/joint_profile.txt; exit $rc ;;
+full)
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rs --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 && \
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && \
+  timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err && \
+  timeout -k 10 300 python bench.py --config c2 --graph --steps 2000 --warmup 200 > $O/bench_c2_graph.json 2> $O/bench_c2_graph.err
+  rc=$?; echo rc=$rc; tail -n 3 $O/pytest_gpu.log; cat $O/smoke.log $O/bench.json $O/bench_c2_graph.json; exit $rc ;;
+esac
