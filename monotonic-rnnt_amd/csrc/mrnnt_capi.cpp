@@ -499,6 +499,9 @@ RNNTStatus mrnnt_forward(const mrnnt_problem *p, void *ws, size_t ws_bytes, floa
         ca.delay = kVariants ? (uint32_t)std::max(0, tuning().chase_delay_us) * 100u : 0u;
         ca.stage = kVariants ? tuning().chase_stage : 1;
         ca.probe = kVariants ? tuning().chase_probe : 0;
+        ca.pair = kVariants ? tuning().chase_pair : 2;
+        ca.early_free = kVariants ? tuning().chase_early_free : 1;
+        ca.ring = kVariants ? tuning().chase_ring : 64;
         const int nrec = with_beta ? 2 * pl.B : pl.B;
         const int producers = (int)std::min<int64_t>(streaming_grid(slot_bound, tuning().chase_grid_per_cu),
                                                      ((int64_t)1 << 22) - nrec);
@@ -1035,6 +1038,9 @@ int mrnnt_profile_read(double *total_ms, int64_t *launches, int n) {
 // development build: columns chase recursion waves computed themselves since the last reset (mrnnt_chase.hip)
 __attribute__((visibility("default"))) unsigned long long mrnnt_chase_helped(int reset) { return chase_helped(reset != 0); }
 __attribute__((visibility("default"))) int mrnnt_chase_trace(unsigned long long *out, int n) { return chase_trace(out, n); }
+__attribute__((visibility("default"))) int mrnnt_chase_walk_trace(unsigned long long *out, int n) {
+    return chase_walk_trace(out, n);
+}
 __attribute__((visibility("default"))) int mrnnt_joint_trace(unsigned long long *out, int n) { return joint_trace(out, n); }
 
 // launch knobs: exported by the development build only (libmonotonic_rnnt_amd_dev.so, `make dev`)
@@ -1068,6 +1074,9 @@ __attribute__((visibility("default"))) int mrnnt_tune(const char *key, int value
     else if (!std::strcmp(key, "chase_stage")) slot = &t.chase_stage;
     else if (!std::strcmp(key, "chase_delay_us")) slot = &t.chase_delay_us;
     else if (!std::strcmp(key, "chase_probe")) slot = &t.chase_probe;
+    else if (!std::strcmp(key, "chase_pair")) slot = &t.chase_pair;
+    else if (!std::strcmp(key, "chase_early_free")) slot = &t.chase_early_free;
+    else if (!std::strcmp(key, "chase_ring")) slot = &t.chase_ring;
     else if (!std::strcmp(key, "chase_grid_per_cu")) slot = &t.chase_grid_per_cu;
     else if (!std::strcmp(key, "nt_load")) slot = &t.nt_load;
     else if (!std::strcmp(key, "occ_skip")) slot = &t.occ_skip;

@@ -57,8 +57,18 @@ __device__ unsigned long long g_chase_trace[kTraceWgs * 4];
         if (threadIdx.x == 0 && blockIdx.x < (unsigned)kTraceWgs)                              \
             g_chase_trace[blockIdx.x * 4 + (i)] = __builtin_amdgcn_s_memrealtime();            \
     } while (0)
+// development build: walk progress of the first kWalkWgs recursion workgroups, 64 stamps each -- [0, 32): the walk
+// wave finished walk positions [0, 8 (i + 1)); [32, 64): the loader published `loaded` >= 8 (i - 31)
+constexpr int kWalkWgs = 128;
+__device__ unsigned long long g_walk_trace[kWalkWgs * 64];
+#define WALK_MARK(i)                                                                                         \
+    do {                                                                                                     \
+        if ((threadIdx.x & 63) == 0 && blockIdx.x < (unsigned)kWalkWgs && (unsigned)(i) < 64u)               \
+            g_walk_trace[blockIdx.x * 64 + (i)] = __builtin_amdgcn_s_memrealtime();                          \
+    } while (0)
 #else
 #define CHASE_MARK(i) ((void)0)
+#define WALK_MARK(i) ((void)0)
 #endif
 
 // this launch's ready tag (scalar unit): a bijection of the dispatch id for a given epoch and queue
@@ -176,10 +186,14 @@ struct Chase {
 
 // ---- one-wave recursion with LDS-staged frames -----------------------------------------------------------------
 
-constexpr int kRing = 16;  // lp frames in the LDS ring (1 KiB each: 16 KiB, which keeps 8 workgroups per CU)
+// The LDS ring of lp frames, packed at the frame's width (W = S + 1 rows of 16 bytes): 21 KiB, 32 frames of <= 42 rows
+// (configs[1]), 16 of <= 64. 21 KiB + the counters keeps 7 workgroups per CU, the occupancy the kernel's registers
+// allow its producers anyway; the ring's depth bounds the loader's frames in flight per poll round trip.
+constexpr int kRingLp = 1344;
+__device__ __forceinline__ int ring_frames(int W, int cap) { return min(W <= 21 ? 64 : (W <= 42 ? 32 : 16), cap); }
 
 struct StageLds {
-    Lp ring[kRing][64];
+    Lp ring[kRingLp];
     int loaded;        // walk positions [0, loaded) are in the ring (the loader wave)
     int consumed[64];  // [0]: walk positions [0, consumed) have been read by the recursion wave (every lane of it
                        // stores its own word, so the store needs no lane-0 branch)
@@ -193,13 +207,13 @@ __device__ __forceinline__ void lds_put(int *w, int v) {
     __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// Wave 1: walk position u (frame fwd ? u : T - 1 - u) into ring slot u % kRing, lane l <- lp row min(l, S) of that
+// Wave 1: walk position u (frame fwd ? u : T - 1 - u) into ring slot u % R (R = ring_frames), lane l < W <- lp row l
 // frame. One iteration = one poll round trip: the explicit vmcnt(0) before publishing `loaded` covers every DMA
 // issued before the poll, then the DMAs of the frames the poll found ready (as far as the ring has room) are issued.
 template <class Help>
 __device__ __forceinline__ void stage_loader(const DevProblem &p, const Utt &u, bool fwd, const unsigned long long *flags,
                                              unsigned long long want, uint32_t budget, const Help &help,
-                                             StageLds &st) {
+                                             StageLds &st, int R, int probe = 0) {
     const int lane = threadIdx.x & 63;
     const int T = u.T, W = u.S + 1;
     const unsigned col = (unsigned)min(lane, u.S);
@@ -207,11 +221,20 @@ __device__ __forceinline__ void stage_loader(const DevProblem &p, const Utt &u, 
     int issued = 0;
     uint32_t t_wait = 0;
     bool waiting = false;
+#ifdef MRNNT_DEVTOOLS
+    int marked = 0;
+#endif
     for (;;) {
         const int i = issued + lane;
         const unsigned long long v = i < T ? load_wt(&flags[fwd ? i : T - 1 - i]) : want;
         wait_vmcnt0();  // the poll and every earlier DMA have landed
         lds_put(&st.loaded, issued);
+#ifdef MRNNT_DEVTOOLS
+        if (probe & 8) {
+            for (int m = marked + 1; m <= issued / 8; ++m) WALK_MARK(31 + m);
+            marked = max(marked, issued / 8);
+        }
+#endif
         if (issued >= T) return;
         const unsigned long long miss = ~__ballot(v == want);
         int ready = issued + (miss ? __builtin_ctzll(miss) : 64);
@@ -229,13 +252,15 @@ __device__ __forceinline__ void stage_loader(const DevProblem &p, const Utt &u, 
             }
         }
         if (ready > issued) waiting = false;
-        const int room = lds_get(&st.consumed[0]) + kRing;
+        const int room = lds_get(&st.consumed[0]) + R;
         const int end = min(min(ready, room), T);
         for (; issued < end; ++issued) {
             const int t = fwd ? issued : T - 1 - issued;
             const unsigned off = (unsigned)((u.r0 + (int64_t)t * W) * (int64_t)sizeof(Lp)) + col * (unsigned)sizeof(Lp);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)&st.ring[issued % kRing][0],
-                                                     16, off, 0, 0, kAuxSc1);
+            if (lane < W)  // (the frame's rows only: the next slot starts right after them)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rs, (__attribute__((address_space(3))) void *)&st.ring[(issued & (R - 1)) * W], 16, off, 0, 0,
+                    kAuxSc1);
         }
         if (end < ready && ready > issued) __builtin_amdgcn_s_sleep(1);  // ring full: the recursion wave catches up
     }
@@ -249,14 +274,15 @@ template <int P>
 struct RingReader {
     StageLds &st;
     int avail = 0;
-    __device__ __forceinline__ explicit RingReader(StageLds &s) : st(s) {}
+    const int R, W, col;  // ring frames, frame width, this lane's row in a frame (lanes past S read row S)
+    __device__ __forceinline__ RingReader(StageLds &s, int R_, int S) : st(s), R(R_), W(S + 1), col(min((int)(threadIdx.x & 63), S)) {}
     __device__ __forceinline__ Lp read(int u) {
         while (avail <= u) {
             avail = lds_get(&st.loaded);
             if (avail <= u) __builtin_amdgcn_s_sleep(1);
         }
         asm volatile("" ::: "memory");
-        return st.ring[u % kRing][threadIdx.x & 63];
+        return st.ring[(u & (R - 1)) * W + col];
     }
     __device__ __forceinline__ void done(int u) {  // walk positions [0, u] may be refilled (once per block of P)
         lds_put(&st.consumed[threadIdx.x & 63], u + 1);
@@ -280,13 +306,25 @@ struct RowStore {
 
 // The steps of alpha_pass_halo / beta_pass_halo at NW = 1, HL = 0, lean (the same operations, so the same bits),
 // laid out for a one-wave chain: blocks of P steps with no branch inside (the ring read of each step clamps its frame
-// instead of testing it, the stores are buffer stores, consumption is published once per block).
-template <int P>
+// instead of testing it, the stores are buffer stores, consumption is published once per block: the positions read
+// into registers so far with early_free, else the positions used).
+//
+// PAIR = 2: the chain advances two frames per dependent log-sum-exp. Over frames t, t + 1 a cell s is reached from
+// s (two blanks), s - 1 (an emission at t or at t + 1) or s - 2 (two emissions), so
+//   alpha(t+1, s) = lse3(alpha(t-1, s)   + lpb(t, s) + lpb(t+1, s),
+//                        alpha(t-1, s-1) + lse2(lpe(t, s-1) + lpb(t+1, s), lpb(t, s-1) + lpe(t+1, s-1)),
+//                        alpha(t-1, s-2) + lpe(t, s-2) + lpe(t+1, s-1))
+// whose coefficients do not depend on alpha: the chain carries one three-term step (two DPP shifts deep) where it
+// carried two two-term steps, and alpha(t, .) -- the single step, exactly as PAIR = 1 forms it from alpha(t-1, .) -- is
+// formed beside it for the store. Results agree with the single-step chain to fp64 rounding of the LSE corrections
+// (~1e-7), not bit for bit.
+template <int P, int PAIR>
 __device__ __forceinline__ void alpha_staged(const DevProblem &p, const Utt &u, int b, float *__restrict__ costs,
-                                             StageLds &st, int probe = 0) {
+                                             StageLds &st, int R, int probe = 0, int early_free = 1) {
+    static_assert(P % 2 == 0, "frame pairs inside a block");
     const int lane = threadIdx.x & 63;
     const int T = u.T, S = u.S, W = S + 1;
-    RingReader<P> rr(st);
+    RingReader<P> rr(st, R, S);
     wait_vmcnt0();  // (see RingReader)
     const RowStore out(p.alpha + u.r0, (int64_t)T * W, lane, W);
     double a = (lane == 0) ? 0.0 : NEG_INF_D;
@@ -295,6 +333,7 @@ __device__ __forceinline__ void alpha_staged(const DevProblem &p, const Utt &u, 
     for (int d = 0; d < P; ++d) q[d] = rr.read(min(d, T - 1));
     CHASE_MARK(2);
     unsigned soff = 0;
+    const unsigned row = (unsigned)W * 8u;
     auto step = [&](int t, int d) {
         const double y = dpp_shr1_ninf(a + q[d].e);  // alpha(t-1, s-1) + lpe(t, s-1), from lane s-1 (lane 0: -inf)
         if (kVariants && (probe & 2))
@@ -302,19 +341,54 @@ __device__ __forceinline__ void alpha_staged(const DevProblem &p, const Utt &u, 
         else
             a = lse2(a + q[d].b, y);
         if (!kVariants || !(probe & 1)) out.put(a, soff);
-        soff += (unsigned)W * 8u;
+        soff += row;
         if (!kVariants || !(probe & 4)) q[d] = rr.read(min(t + P, T - 1));
+    };
+    auto pair = [&](int t, int d) {  // frames t, t + 1 from q[d], q[d + 1]
+        const Lp q0 = q[d], q1 = q[d + 1];
+        const double y = dpp_shr1_ninf(a + q0.e);                       // alpha(t-1, s-1) + lpe(t, s-1)
+        const double a1 = lse2(a + q0.b, y);                            // alpha(t, s), off the chain
+        const double k1 = lse2(q0.e + dpp_shl1_ninf(q1.b), q0.b + q1.e);  // s -> s+1 over t, t+1 (lane s)
+        const double x0 = a + (q0.b + q1.b);
+        const double x1 = dpp_shr1_ninf(a + k1);
+        const double x2 = dpp_shr1_ninf(y + q1.e);
+        a = lse3(x0, x1, x2);
+        out.put(a1, soff);
+        out.put(a, soff + row);
+        soff += 2 * row;
+        if (!kVariants || !(probe & 4)) {
+            q[d] = rr.read(min(t + P, T - 1));
+            q[d + 1] = rr.read(min(t + 1 + P, T - 1));
+        }
     };
     int t0 = 0;
     for (; t0 + P <= T; t0 += P) {
+        if constexpr (PAIR == 2) {
 #pragma unroll
-        for (int d = 0; d < P; ++d) step(t0 + d, d);
-        rr.done(t0 + P - 1);
+            for (int d = 0; d < P; d += 2) pair(t0 + d, d);
+        } else {
+#pragma unroll
+            for (int d = 0; d < P; ++d) step(t0 + d, d);
+        }
+        rr.done(early_free ? t0 + 2 * P - 1 : t0 + P - 1);
+#ifdef MRNNT_DEVTOOLS
+        if ((probe & 8) && ((t0 + P) & 7) == 0) WALK_MARK((t0 + P) / 8 - 1);
+#endif
     }
+    if constexpr (PAIR == 2) {
 #pragma unroll
-    for (int d = 0; d < P; ++d) {
-        if (t0 + d >= T) break;
-        step(t0 + d, d);
+        for (int d = 0; d < P; d += 2) {
+            if (t0 + d + 1 < T)
+                pair(t0 + d, d);
+            else if (t0 + d < T)
+                step(t0 + d, d);
+        }
+    } else {
+#pragma unroll
+        for (int d = 0; d < P; ++d) {
+            if (t0 + d >= T) break;
+            step(t0 + d, d);
+        }
     }
     if (lane == S) {
         p.ll[b] = a;
@@ -322,11 +396,17 @@ __device__ __forceinline__ void alpha_staged(const DevProblem &p, const Utt &u, 
     }
 }
 
-template <int P>
-__device__ __forceinline__ void beta_staged(const DevProblem &p, const Utt &u, int b, StageLds &st, int probe = 0) {
+// PAIR = 2 (as alpha_staged), walk positions w, w + 1 = frames t = T - 1 - w and t - 1:
+//   beta(t-1, s) = lse3(beta(t+1, s)   + lpb(t-1, s) + lpb(t, s),
+//                       beta(t+1, s+1) + lse2(lpb(t-1, s) + lpe(t, s), lpe(t-1, s) + lpb(t, s+1)),
+//                       beta(t+1, s+2) + lpe(t-1, s) + lpe(t, s+1))
+template <int P, int PAIR>
+__device__ __forceinline__ void beta_staged(const DevProblem &p, const Utt &u, int b, StageLds &st, int R,
+                                            int probe = 0, int early_free = 1) {
+    static_assert(P % 2 == 0, "frame pairs inside a block");
     const int lane = threadIdx.x & 63;
     const int T = u.T, S = u.S, W = S + 1;
-    RingReader<P> rr(st);
+    RingReader<P> rr(st, R, S);
     wait_vmcnt0();  // (see RingReader)
     const RowStore out(p.beta + u.r0, (int64_t)T * W, lane, W);
     double bn = (lane == S) ? 0.0 : NEG_INF_D;  // beta(T, s)
@@ -334,7 +414,8 @@ __device__ __forceinline__ void beta_staged(const DevProblem &p, const Utt &u, i
 #pragma unroll
     for (int d = 0; d < P; ++d) q[d] = rr.read(min(d, T - 1));
     CHASE_MARK(2);
-    unsigned soff = (unsigned)(T - 1) * (unsigned)W * 8u;
+    const unsigned row = (unsigned)W * 8u;
+    unsigned soff = (unsigned)(T - 1) * row;
     auto step = [&](int w, int d) {  // walk position w = frame T - 1 - w
         const double carry = dpp_shl1_ninf(bn);  // beta(t+1, s+1), from lane s+1 (lane 63: -inf)
         if (kVariants && (probe & 2))
@@ -342,19 +423,55 @@ __device__ __forceinline__ void beta_staged(const DevProblem &p, const Utt &u, i
         else
             bn = lse2(bn + q[d].b, carry + q[d].e);
         if (!kVariants || !(probe & 1)) out.put(bn, soff);
-        soff -= (unsigned)W * 8u;
+        soff -= row;
         if (!kVariants || !(probe & 4)) q[d] = rr.read(min(w + P, T - 1));
+    };
+    auto pair = [&](int w, int d) {  // frames t = T - 1 - w (q[d]) and t - 1 (q[d + 1])
+        const Lp q0 = q[d], q1 = q[d + 1];
+        const double carry = dpp_shl1_ninf(bn);                         // beta(t+1, s+1)
+        const double g = carry + q0.e;
+        const double b1 = lse2(bn + q0.b, g);                           // beta(t, s), off the chain
+        const double d1 = lse2(q1.b + q0.e, q1.e + dpp_shl1_ninf(q0.b));  // s -> s+1 over t-1, t (lane s)
+        const double x0 = bn + (q1.b + q0.b);
+        const double x1 = carry + d1;
+        const double x2 = dpp_shl1_ninf(g) + q1.e;
+        bn = lse3(x0, x1, x2);
+        out.put(b1, soff);
+        out.put(bn, soff - row);
+        soff -= 2 * row;
+        if (!kVariants || !(probe & 4)) {
+            q[d] = rr.read(min(w + P, T - 1));
+            q[d + 1] = rr.read(min(w + 1 + P, T - 1));
+        }
     };
     int w0 = 0;
     for (; w0 + P <= T; w0 += P) {
+        if constexpr (PAIR == 2) {
 #pragma unroll
-        for (int d = 0; d < P; ++d) step(w0 + d, d);
-        rr.done(w0 + P - 1);
+            for (int d = 0; d < P; d += 2) pair(w0 + d, d);
+        } else {
+#pragma unroll
+            for (int d = 0; d < P; ++d) step(w0 + d, d);
+        }
+        rr.done(early_free ? w0 + 2 * P - 1 : w0 + P - 1);
+#ifdef MRNNT_DEVTOOLS
+        if ((probe & 8) && ((w0 + P) & 7) == 0) WALK_MARK((w0 + P) / 8 - 1);
+#endif
     }
+    if constexpr (PAIR == 2) {
 #pragma unroll
-    for (int d = 0; d < P; ++d) {
-        if (w0 + d >= T) break;
-        step(w0 + d, d);
+        for (int d = 0; d < P; d += 2) {
+            if (w0 + d + 1 < T)
+                pair(w0 + d, d);
+            else if (w0 + d < T)
+                step(w0 + d, d);
+        }
+    } else {
+#pragma unroll
+        for (int d = 0; d < P; ++d) {
+            if (w0 + d >= T) break;
+            step(w0 + d, d);
+        }
     }
     if (lane == 0) p.llb[b] = bn;
 }
@@ -403,6 +520,7 @@ __global__ __launch_bounds__(256) void chase_kernel(DevProblem p, ChaseArgs c, i
         const unsigned long long *flags = c.flags + u.c0;
         CHASE_MARK(1);
         if constexpr (STG && NW == 1) {
+            const int R = ring_frames(u.S + 1, kVariants ? c.ring : 64);
             if (threadIdx.x == 0) {  // (LDS holds whatever the CU's previous workgroup left)
                 st.loaded = 0;
                 st.consumed[0] = 0;
@@ -411,13 +529,21 @@ __global__ __launch_bounds__(256) void chase_kernel(DevProblem p, ChaseArgs c, i
             if (wave >= 2) return;
             if (wave == 1) {
                 const SelfHelp<SM, IO, NTL> help{&p, u, b, 0, u.S};
-                stage_loader(p, u, !bwd, flags, tag, c.budget, help, st);
+                stage_loader(p, u, !bwd, flags, tag, c.budget, help, st, R, kVariants ? c.probe : 0);
                 return;
             }
-            if (bwd)
-                beta_staged<4>(p, u, b, st, kVariants ? c.probe : 0);
-            else
-                alpha_staged<4>(p, u, b, costs, st, kVariants ? c.probe : 0);
+            const int probe = kVariants ? c.probe : 0, early = kVariants ? c.early_free : 1;
+            if (kVariants && c.pair == 1) {  // (development A/B: one log-sum-exp per frame)
+                if (bwd)
+                    beta_staged<4, 1>(p, u, b, st, R, probe, early);
+                else
+                    alpha_staged<4, 1>(p, u, b, costs, st, R, probe, early);
+            } else {
+                if (bwd)
+                    beta_staged<4, 2>(p, u, b, st, R, probe, early);
+                else
+                    alpha_staged<4, 2>(p, u, b, costs, st, R, probe, early);
+            }
             CHASE_MARK(3);
             return;
         }
@@ -559,6 +685,12 @@ hipError_t launch_chase(const DevProblem &p, const ChaseArgs &c, int elem, int S
 }
 
 #ifdef MRNNT_DEVTOOLS
+int chase_walk_trace(unsigned long long *out, int n) {
+    n = std::min(n, kWalkWgs * 64);
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_walk_trace), sizeof(unsigned long long) * n) != hipSuccess) return -1;
+    return n;
+}
+
 int chase_trace(unsigned long long *out, int n) {
     n = std::min(n, kTraceWgs * 4);
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chase_trace), sizeof(unsigned long long) * n) != hipSuccess) return -1;

@@ -45,6 +45,19 @@ __device__ __forceinline__ double lse2(double x, double y) {
     return (m == NEG_INF_D) ? NEG_INF_D : r;
 }
 
+// log(e^x + e^y + e^z), the same form with three terms: m + log(sum e^(x_i - m)), the sum in [1, 3] in fp32 (one
+// term is exactly 1), log2 on v_log_f32 -- <= ~2e-7 absolute, the error of two lse2 steps, for a step that replaces
+// two of them on a dependent chain (the staged walk's frame pairs, mrnnt_chase.hip). All -inf gives -inf.
+__device__ __forceinline__ double lse3(double x, double y, double z) {
+    const double m = max_f64(max_f64(x, y), z);
+    const float ex = fast_exp2((float)(x - m) * kLog2e);
+    const float ey = fast_exp2((float)(y - m) * kLog2e);
+    const float ez = fast_exp2((float)(z - m) * kLog2e);
+    const float c = fast_log2(ex + ey + ez) * kLn2;
+    const double r = m + (double)c;
+    return (m == NEG_INF_D) ? NEG_INF_D : r;
+}
+
 // wave64 butterfly reduction of an online-softmax (max, sum-exp) pair
 __device__ __forceinline__ void wave_reduce_max_sum(float &m, float &s) {
 #pragma unroll

@@ -165,6 +165,9 @@ struct Tuning {
                                   // gated loads; development build)
     int chase_delay_us = 0;       // development probe: every chase producer workgroup starts this late
     int chase_probe = 0;          // development probe: ChaseArgs::probe (the staged walk's step cost; results wrong)
+    int chase_pair = 2;           // staged chase walk: frames per dependent log-sum-exp (1: one LSE per frame)
+    int chase_early_free = 1;     // staged chase walk: ring slots freed when read into registers (0: after their use)
+    int chase_ring = 64;          // staged chase walk: cap on the LDS ring's frames (16: round 5's depth)
     int joint_reduce_hact = 1;    // joint reduce: 1 reads Hact; 0 (development build) recomputes the activation from
                                   // enc / pred (the gradient pass's bits; measured slower, mrnnt_joint.hip)
     int joint_reduce_pad = 1;     // joint reduce: accumulator LDS pitch HS + 1 (0: HS, development A/B; bit-identical)
@@ -255,6 +258,9 @@ struct ChaseArgs {
     int stage;                 // one-wave recursion: LDS-staged frames (the product's only form) or direct loads
     int probe;                 // development probe of the staged walk's step (results wrong): bit 0 no alpha/beta
                                // stores, bit 1 a max in place of the log-sum-exp, bit 2 no ring reads after the first P
+    int pair;                  // staged walk: frames per dependent log-sum-exp (1, or 2: a three-term step)
+    int early_free;            // staged walk: ring slots are freed once read into registers (else after their use)
+    int ring;                  // staged walk: at most this many frames in the LDS ring (development A/B)
 };
 // The log-softmax body the chase launch carries for f32 rows of V elements: 0 rows on 16-lane groups (<= 64
 // vectors), 2 / 3 single-chunk rows of <= 128 vectors (full / partial chunk), 4 / 5 of <= 256; -1 none.
@@ -274,6 +280,7 @@ inline int64_t chase_slots(int B, int T_max, int with_beta) {
 // development build: columns chase recursion waves computed themselves (since the last reset)
 unsigned long long chase_helped(bool reset);
 int chase_trace(unsigned long long *out, int n);  // development build: the chase launch timeline
+int chase_walk_trace(unsigned long long *out, int n);  // development build: walk / loader progress (probe bit 8)
 int joint_trace(unsigned long long *out, int n);  // development build: the fused joint forward's wave timeline
 hipError_t launch_chase(const DevProblem &p, const ChaseArgs &c, int elem, int S_max, int with_beta, int producers,
                         float *costs, hipStream_t stream);

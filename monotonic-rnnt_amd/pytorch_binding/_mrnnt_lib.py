@@ -165,6 +165,7 @@ def _bind(path: str, dev: bool = False) -> ctypes.CDLL:
         sig["mrnnt_tune"] = (i, [ctypes.c_char_p, i])
         sig["mrnnt_chase_helped"] = (ctypes.c_ulonglong, [i])
         sig["mrnnt_chase_trace"] = (i, [ctypes.POINTER(ctypes.c_ulonglong), i])
+        sig["mrnnt_chase_walk_trace"] = (i, [ctypes.POINTER(ctypes.c_ulonglong), i])
         sig["mrnnt_joint_trace"] = (i, [ctypes.POINTER(ctypes.c_ulonglong), i])
     for name, (res, args) in sig.items():
         fn = getattr(lib, name, None)

@@ -3,6 +3,7 @@
 #   first : joint tests + the new uniform-acts oracle test, headline bench lines on N(0,1) / U[0,1) logits and with
 #           every in-band row live (development build, occ_skip=0), then the joint step's kernel stats + SQ counters on
 #           the shipping library
+#   walk  : walk / loader progress inside the configs[1] chase launch (tools/walk_trace.py; probe 4: no ring reads)
 #   full  : every gpu-marked test, smoke(), the default bench line, configs[1] graph bench
 set -o pipefail
 R=$GRAFT_REPO_ROOT
@@ -25,6 +26,35 @@ first)
 import json,sys;d=json.load(open('$O/bench_$f.json'));r=d['roofline'];k=d['kernels']
 print('$f',d['value'],d['ms_per_step'],'live',r['live_rows'],'/',r['inband_rows'],'frac',r['frac'],'grad',k['grad']['avg_ms'],'lsm',k['log_softmax']['avg_ms'])"; done
   cat $O/joint_profile.txt; exit $rc ;;
+walk)
+  W="python tools/walk_trace.py"
+  timeout -k 10 200 $W $O/walk_p1e0.json chase_pair=1 chase_early_free=0 > $O/walk_p1e0.txt 2>&1 && \
+  timeout -k 10 200 $W $O/walk_p1e1.json chase_pair=1 chase_early_free=1 > $O/walk_p1e1.txt 2>&1 && \
+  timeout -k 10 200 $W $O/walk_p2e1.json chase_pair=2 chase_early_free=1 > $O/walk_p2e1.txt 2>&1 && \
+  timeout -k 10 200 $W $O/walk_p2e1_noring.json chase_pair=2 chase_early_free=1 chase_probe=4 > $O/walk_p2e1_noring.txt 2>&1 && \
+  timeout -k 10 200 $W $O/walk_p1e1_noring.json chase_pair=1 chase_early_free=1 chase_probe=4 > $O/walk_p1e1_noring.txt 2>&1 && \
+  timeout -k 10 300 python tools/kbench.py --config c2 --rounds 40 --variants '[{"chase_pair":1,"chase_early_free":0},{"chase_pair":1,"chase_early_free":1},{"chase_pair":2,"chase_early_free":0},{"chase_pair":2,"chase_early_free":1}]' > $O/kbench_c2_pair_early.json 2> $O/kbench.err
+  rc=$?; echo rc=$rc; for f in p1e0 p1e1 p2e1 p2e1_noring p1e1_noring; do echo == $f; tail -n 4 $O/walk_$f.txt; done
+  python3 -c "
+import json;d=json.load(open('$O/kbench_c2_pair_early.json'))
+for v in d['variants']: print(v['knobs'], {k: round(x*1e3,2) for k,x in v['median_ms'].items() if x})"; exit $rc ;;
+walkprobe)
+  W="python tools/walk_trace.py"
+  for pr in 4 5 6 7; do
+    timeout -k 10 200 $W $O/walk_p1_probe$pr.json chase_pair=1 chase_early_free=1 chase_probe=$pr > $O/walk_p1_probe$pr.txt 2>&1 || exit $?
+  done
+  for pr in 4 5 6 7; do echo == probe $pr; grep "alpha walk" $O/walk_p1_probe$pr.txt; done; exit 0 ;;
+chase)
+  W="python tools/walk_trace.py"
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_chase.py -x -q -rs --timeout 120 --timeout-method thread > $O/pytest_chase.log 2>&1
+  rc=$?; tail -n 3 $O/pytest_chase.log; [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 200 $W $O/walk_p2_r64.json chase_pair=2 chase_ring=64 > $O/walk_p2_r64.txt 2>&1 && \
+  timeout -k 10 200 $W $O/walk_p1_r64.json chase_pair=1 chase_ring=64 > $O/walk_p1_r64.txt 2>&1 && \
+  timeout -k 10 300 python tools/kbench.py --config c2 --rounds 40 --variants '[{"chase_pair":1,"chase_early_free":0,"chase_ring":16},{"chase_pair":2,"chase_ring":16},{"chase_pair":1,"chase_ring":64},{"chase_pair":2,"chase_ring":64}]' > $O/kbench_c2_ring.json 2> $O/kbench.err
+  rc=$?; echo rc=$rc; for f in p2_r64 p1_r64; do echo == $f; tail -n 4 $O/walk_$f.txt; done
+  python3 -c "
+import json;d=json.load(open('$O/kbench_c2_ring.json'))
+for v in d['variants']: print(v['knobs'], {k: round(x*1e3,2) for k,x in v['median_ms'].items() if x})"; exit $rc ;;
 full)
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rs --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 && \
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && \

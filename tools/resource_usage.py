@@ -28,4 +28,5 @@ for line in out.splitlines():
 for r in rows:
     if flt in r["name"]:
         print(f'{r.get("VGPRs","?"):>4} vgpr {r.get("AGPRs","?"):>3} agpr occ {r.get("Occupancy [waves/SIMD]","?"):>2} '
-              f'sspill {r.get("SGPRs Spill","?"):>3} vspill {r.get("VGPRs Spill","?"):>3} scratch {r.get("ScratchSize [bytes/lane]","?"):>4}  {r["name"]}')
+              f'sspill {r.get("SGPRs Spill","?"):>3} vspill {r.get("VGPRs Spill","?"):>3} scratch {r.get("ScratchSize [bytes/lane]","?"):>4} '
+          f'lds {r.get("LDS Size [bytes/block]","?"):>6}  {r["name"]}')
