@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MRNNT_VERSION 11
+#define MRNNT_VERSION 12
 
 /* acts / grads element types */
 #define MRNNT_F32 0
@@ -208,9 +208,20 @@ typedef struct mrnnt_joint_problem {
     void *reduce_scratch;    /* (version 9) device memory for mrnnt_joint_reduce, >= mrnnt_joint_reduce_scratch_bytes,
                                 or NULL (a slower one-block-per-utterance form runs); e.g. G once dH = G weight exists */
     size_t reduce_scratch_bytes;
+    const unsigned long long *live_count_dev; /* (version 12) device uint64 or NULL: the count mrnnt_joint_live_rows
+                                wrote. When set, the n_live argument of mrnnt_joint_backward (and of mrnnt_joint_dpre /
+                                mrnnt_joint_reduce / mrnnt_joint_reduce_pre) is a host-known UPPER BOUND on the count
+                                (mrnnt_joint_row_bound) and the kernels take the count from this word: no device-to-host
+                                read between the forward and the backward, so a training step can be captured in a HIP
+                                graph. mrnnt_joint_backward then also writes rows [count, n_live) of G and Hact as zeros,
+                                so library GEMMs over all n_live rows (dweight, dH) see zero rows there. */
 } mrnnt_joint_problem;
 
 RNNTStatus mrnnt_joint_workspace_size(const mrnnt_joint_problem *p, size_t *bytes);
+
+/* (version 12) A host-known upper bound on the live-row count of mrnnt_joint_live_rows: the lattice rows inside the
+ * monotonic band, from the host lengths (no device read). Size G / Hact with it under p->live_count_dev. */
+RNNTStatus mrnnt_joint_row_bound(const mrnnt_joint_problem *p, int64_t *rows);
 
 /* Forward: costs_dev[b] = -log P(labels_b | enc_b, pred_b); with_beta as in mrnnt_forward. */
 RNNTStatus mrnnt_joint_forward(const mrnnt_joint_problem *p, void *workspace, size_t workspace_bytes,

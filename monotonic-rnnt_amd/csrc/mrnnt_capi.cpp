@@ -499,7 +499,7 @@ RNNTStatus mrnnt_forward(const mrnnt_problem *p, void *ws, size_t ws_bytes, floa
         ca.delay = kVariants ? (uint32_t)std::max(0, tuning().chase_delay_us) * 100u : 0u;
         ca.stage = kVariants ? tuning().chase_stage : 1;
         ca.probe = kVariants ? tuning().chase_probe : 0;
-        ca.pair = kVariants ? tuning().chase_pair : 2;
+        ca.pair = kVariants ? tuning().chase_pair : 3;
         ca.early_free = kVariants ? tuning().chase_early_free : 1;
         ca.ring = kVariants ? tuning().chase_ring : 64;
         const int nrec = with_beta ? 2 * pl.B : pl.B;
@@ -814,6 +814,15 @@ RNNTStatus mrnnt_joint_workspace_size(const mrnnt_joint_problem *jp, size_t *byt
     return RNNT_STATUS_SUCCESS;
 }
 
+RNNTStatus mrnnt_joint_row_bound(const mrnnt_joint_problem *jp, int64_t *rows) {
+    if (!rows) return fail(RNNT_STATUS_INVALID_VALUE, "null rows pointer");
+    JointPlan jl;
+    const RNNTStatus st = make_joint_plan(jp, &jl);
+    if (st != RNNT_STATUS_SUCCESS) return st;
+    *rows = jl.n_inband;
+    return RNNT_STATUS_SUCCESS;
+}
+
 RNNTStatus mrnnt_joint_forward(const mrnnt_joint_problem *jp, void *ws, size_t ws_bytes, float *costs_dev,
                                int with_beta, hipStream_t stream) {
     JointPlan jl;
@@ -893,6 +902,7 @@ RNNTStatus mrnnt_joint_backward(const mrnnt_joint_problem *jp, void *ws, int64_t
     const mrnnt_problem p = base_problem(jp);
     DevProblem d = make_dev(&p, jl.base, ws);
     JointArgs j = joint_args(jp, jl, ws, n_live);
+    j.n_dev = jp->live_count_dev;  // n_live a host bound: workgroups past the device count exit (their rows zeroed below)
     j.G = static_cast<unsigned short *>(G);
     j.Hact = static_cast<unsigned short *>(Hact);
     j.bt_idx = bt_idx;
@@ -906,7 +916,11 @@ RNNTStatus mrnnt_joint_backward(const mrnnt_joint_problem *jp, void *ws, int64_t
     if (jp->dbias && !jl.off_dbias)
         return fail(RNNT_STATUS_INVALID_VALUE, "dbias needs a bias (the workspace holds its partial sums only then)");
     if (jp->dbias) j.dbias_part = reinterpret_cast<float *>(static_cast<char *>(ws) + jl.off_dbias);
-    hipError_t e = timed(K_JOINT_BWD, stream, [&] { return launch_joint_backward(d, j, stream); });
+    hipError_t e = timed(K_JOINT_BWD, stream, [&] {
+        const hipError_t eb = launch_joint_backward(d, j, stream);
+        if (eb != hipSuccess || !jp->live_count_dev) return eb;
+        return launch_joint_tail_zero(j.G, jp->V, j.Hact, j.hact_ld, n_live, jp->live_count_dev, stream);
+    });
     if (e != hipSuccess) return fail_hip(e, "joint gradient kernel");
     if (jp->dbias && n_live > 0) {
         e = launch_joint_dbias_sum(j, jp->V, stream);

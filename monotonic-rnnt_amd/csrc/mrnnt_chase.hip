@@ -196,7 +196,9 @@ struct StageLds {
     Lp ring[kRingLp];
     int loaded;        // walk positions [0, loaded) are in the ring (the loader wave)
     int consumed[64];  // [0]: walk positions [0, consumed) have been read by the recursion wave (every lane of it
-                       // stores its own word, so the store needs no lane-0 branch)
+                       // stores its own word, so the store needs no lane-0 branch); PAIR = 3: by the side wave
+    int chained[64];   // PAIR = 3, [0]: walk positions [0, chained) walked, their chain values handed to the side wave
+    double sink[64];   // PAIR = 3: where the hand-off stores of lanes past S go
 };
 struct NoStage {};
 
@@ -361,21 +363,53 @@ __device__ __forceinline__ void alpha_staged(const DevProblem &p, const Utt &u, 
             q[d + 1] = rr.read(min(t + 1 + P, T - 1));
         }
     };
+    // PAIR = 3: the chain only -- alpha(t, .) is left to the side wave (alpha_side), which takes the chain value
+    // alpha(t-1, .) from the ring slot of frame t - 1, where this wave writes it (lpb of that frame, read already)
+    double *const hand = lane < W ? &st.ring[lane].b : &st.sink[lane];
+    auto pair3 = [&](int t, int d) {
+        const Lp q0 = q[d], q1 = q[d + 1];
+        const double y = dpp_shr1_ninf(a + q0.e);
+        const double k1 = lse2(q0.e + dpp_shl1_ninf(q1.b), q0.b + q1.e);
+        const double x0 = a + (q0.b + q1.b);
+        const double x1 = dpp_shr1_ninf(a + k1);
+        const double x2 = dpp_shr1_ninf(y + q1.e);
+        a = lse3(x0, x1, x2);
+        out.put(a, soff + row);
+        hand[lane < W ? ((t + 1) & (R - 1)) * W * 2 : 0] = a;  // (Lp = two doubles: slot stride 2 W doubles)
+        asm volatile("" ::: "memory");
+        lds_put(&st.chained[lane], t + 2);
+        soff += 2 * row;
+        q[d] = rr.read(min(t + P, T - 1));
+        q[d + 1] = rr.read(min(t + 1 + P, T - 1));
+    };
     int t0 = 0;
     for (; t0 + P <= T; t0 += P) {
-        if constexpr (PAIR == 2) {
+        if constexpr (PAIR == 3) {
+#pragma unroll
+            for (int d = 0; d < P; d += 2) pair3(t0 + d, d);
+        } else if constexpr (PAIR == 2) {
 #pragma unroll
             for (int d = 0; d < P; d += 2) pair(t0 + d, d);
         } else {
 #pragma unroll
             for (int d = 0; d < P; ++d) step(t0 + d, d);
         }
-        rr.done(early_free ? t0 + 2 * P - 1 : t0 + P - 1);
+        if constexpr (PAIR != 3) rr.done(early_free ? t0 + 2 * P - 1 : t0 + P - 1);
 #ifdef MRNNT_DEVTOOLS
         if ((probe & 8) && ((t0 + P) & 7) == 0) WALK_MARK((t0 + P) / 8 - 1);
 #endif
     }
-    if constexpr (PAIR == 2) {
+    if constexpr (PAIR == 3) {
+#pragma unroll
+        for (int d = 0; d < P; d += 2) {
+            if (t0 + d + 1 < T)
+                pair3(t0 + d, d);
+            else if (t0 + d < T)
+                step(t0 + d, d);
+        }
+        asm volatile("" ::: "memory");
+        lds_put(&st.chained[lane], T);
+    } else if constexpr (PAIR == 2) {
 #pragma unroll
         for (int d = 0; d < P; d += 2) {
             if (t0 + d + 1 < T)
@@ -444,21 +478,52 @@ __device__ __forceinline__ void beta_staged(const DevProblem &p, const Utt &u, i
             q[d + 1] = rr.read(min(w + 1 + P, T - 1));
         }
     };
+    double *const hand = lane < W ? &st.ring[lane].b : &st.sink[lane];
+    auto pair3 = [&](int w, int d) {  // PAIR = 3: the chain only (beta_side forms beta(t, .))
+        const Lp q0 = q[d], q1 = q[d + 1];
+        const double carry = dpp_shl1_ninf(bn);
+        const double g = carry + q0.e;
+        const double d1 = lse2(q1.b + q0.e, q1.e + dpp_shl1_ninf(q0.b));
+        const double x0 = bn + (q1.b + q0.b);
+        const double x1 = carry + d1;
+        const double x2 = dpp_shl1_ninf(g) + q1.e;
+        bn = lse3(x0, x1, x2);
+        out.put(bn, soff - row);
+        hand[lane < W ? ((w + 1) & (R - 1)) * W * 2 : 0] = bn;
+        asm volatile("" ::: "memory");
+        lds_put(&st.chained[lane], w + 2);
+        soff -= 2 * row;
+        q[d] = rr.read(min(w + P, T - 1));
+        q[d + 1] = rr.read(min(w + 1 + P, T - 1));
+    };
     int w0 = 0;
     for (; w0 + P <= T; w0 += P) {
-        if constexpr (PAIR == 2) {
+        if constexpr (PAIR == 3) {
+#pragma unroll
+            for (int d = 0; d < P; d += 2) pair3(w0 + d, d);
+        } else if constexpr (PAIR == 2) {
 #pragma unroll
             for (int d = 0; d < P; d += 2) pair(w0 + d, d);
         } else {
 #pragma unroll
             for (int d = 0; d < P; ++d) step(w0 + d, d);
         }
-        rr.done(early_free ? w0 + 2 * P - 1 : w0 + P - 1);
+        if constexpr (PAIR != 3) rr.done(early_free ? w0 + 2 * P - 1 : w0 + P - 1);
 #ifdef MRNNT_DEVTOOLS
         if ((probe & 8) && ((w0 + P) & 7) == 0) WALK_MARK((w0 + P) / 8 - 1);
 #endif
     }
-    if constexpr (PAIR == 2) {
+    if constexpr (PAIR == 3) {
+#pragma unroll
+        for (int d = 0; d < P; d += 2) {
+            if (w0 + d + 1 < T)
+                pair3(w0 + d, d);
+            else if (w0 + d < T)
+                step(w0 + d, d);
+        }
+        asm volatile("" ::: "memory");
+        lds_put(&st.chained[lane], T);
+    } else if constexpr (PAIR == 2) {
 #pragma unroll
         for (int d = 0; d < P; d += 2) {
             if (w0 + d + 1 < T)
@@ -474,6 +539,60 @@ __device__ __forceinline__ void beta_staged(const DevProblem &p, const Utt &u, i
         }
     }
     if (lane == 0) p.llb[b] = bn;
+}
+
+// PAIR = 3, wave 2: alpha(t, .) for the first frame t of every pair, from the chain value alpha(t-1, .) the walk
+// handed over in the ring slot of frame t - 1 (t = 0: alpha(-1, .) = [0, -inf, ...]) and frame t's lp rows, still
+// in the ring: the walk's side step, exactly as PAIR = 2 forms it (the same bits). It frees ring slots for the loader.
+// (Polls only when the counts it last read do not cover the pair: one LDS round trip per pair besides the data.)
+__device__ __forceinline__ int side_wait(const int *w, int have, int need) {
+    while (have < need) {
+        have = lds_get(w);
+        if (have < need) __builtin_amdgcn_s_sleep(1);
+    }
+    return have;
+}
+
+__device__ __forceinline__ void alpha_side(const DevProblem &p, const Utt &u, StageLds &st, int R) {
+    const int lane = threadIdx.x & 63;
+    const int T = u.T, S = u.S, W = S + 1, col = min(lane, S);
+    const RowStore out(p.alpha + u.r0, (int64_t)T * W, lane, W);
+    const unsigned row = (unsigned)W * 8u;
+    double prev = (lane == 0) ? 0.0 : NEG_INF_D;
+    int chained = 0, loaded = 0;
+    for (int k = 0; 2 * k + 1 < T; ++k) {
+        chained = side_wait(&st.chained[0], chained, 2 * k);  // the chain value of frame 2k - 1
+        loaded = side_wait(&st.loaded, loaded, 2 * k + 1);     // frame 2k in the ring
+        asm volatile("" ::: "memory");
+        const Lp q0 = st.ring[((2 * k) & (R - 1)) * W + col];
+        if (k) prev = lane <= S ? st.ring[((2 * k - 1) & (R - 1)) * W + col].b : NEG_INF_D;
+        const double y = dpp_shr1_ninf(prev + q0.e);
+        out.put(lse2(prev + q0.b, y), (unsigned)(2 * k) * row);
+        asm volatile("" ::: "memory");
+        lds_put(&st.consumed[lane], 2 * k + 1);
+    }
+    lds_put(&st.consumed[lane], T);
+}
+
+__device__ __forceinline__ void beta_side(const DevProblem &p, const Utt &u, StageLds &st, int R) {
+    const int lane = threadIdx.x & 63;
+    const int T = u.T, S = u.S, W = S + 1, col = min(lane, S);
+    const RowStore out(p.beta + u.r0, (int64_t)T * W, lane, W);
+    const unsigned row = (unsigned)W * 8u;
+    double prev = (lane == S) ? 0.0 : NEG_INF_D;  // beta(T, .)
+    int chained = 0, loaded = 0;
+    for (int k = 0; 2 * k + 1 < T; ++k) {  // walk position 2k = frame T - 1 - 2k
+        chained = side_wait(&st.chained[0], chained, 2 * k);
+        loaded = side_wait(&st.loaded, loaded, 2 * k + 1);
+        asm volatile("" ::: "memory");
+        const Lp q0 = st.ring[((2 * k) & (R - 1)) * W + col];
+        if (k) prev = lane <= S ? st.ring[((2 * k - 1) & (R - 1)) * W + col].b : NEG_INF_D;
+        const double carry = dpp_shl1_ninf(prev);
+        out.put(lse2(prev + q0.b, carry + q0.e), (unsigned)(T - 1 - 2 * k) * row);
+        asm volatile("" ::: "memory");
+        lds_put(&st.consumed[lane], 2 * k + 1);
+    }
+    lds_put(&st.consumed[lane], T);
 }
 
 // ---- the launch ------------------------------------------------------------------------------------------------
@@ -524,8 +643,17 @@ __global__ __launch_bounds__(256) void chase_kernel(DevProblem p, ChaseArgs c, i
             if (threadIdx.x == 0) {  // (LDS holds whatever the CU's previous workgroup left)
                 st.loaded = 0;
                 st.consumed[0] = 0;
+                st.chained[0] = 0;
             }
             __syncthreads();
+            const int pair = kVariants ? c.pair : 3;
+            if (wave == 2 && pair == 3) {  // the side wave of the chain-only walk
+                if (bwd)
+                    beta_side(p, u, st, R);
+                else
+                    alpha_side(p, u, st, R);
+                return;
+            }
             if (wave >= 2) return;
             if (wave == 1) {
                 const SelfHelp<SM, IO, NTL> help{&p, u, b, 0, u.S};
@@ -533,16 +661,21 @@ __global__ __launch_bounds__(256) void chase_kernel(DevProblem p, ChaseArgs c, i
                 return;
             }
             const int probe = kVariants ? c.probe : 0, early = kVariants ? c.early_free : 1;
-            if (kVariants && c.pair == 1) {  // (development A/B: one log-sum-exp per frame)
+            if (kVariants && pair == 1) {  // (development A/B: one log-sum-exp per frame)
                 if (bwd)
                     beta_staged<4, 1>(p, u, b, st, R, probe, early);
                 else
                     alpha_staged<4, 1>(p, u, b, costs, st, R, probe, early);
-            } else {
+            } else if (kVariants && pair == 2) {  // (development A/B: the side step on the walk itself)
                 if (bwd)
                     beta_staged<4, 2>(p, u, b, st, R, probe, early);
                 else
                     alpha_staged<4, 2>(p, u, b, costs, st, R, probe, early);
+            } else {
+                if (bwd)
+                    beta_staged<4, 3>(p, u, b, st, R, probe, early);
+                else
+                    alpha_staged<4, 3>(p, u, b, costs, st, R, probe, early);
             }
             CHASE_MARK(3);
             return;

@@ -122,6 +122,9 @@ hipError_t launch_zero(void *ptr, size_t bytes, hipStream_t stream);
 // dbias: the fixed-order sum of the backward's per-workgroup column sums (scratch: joint_dbias_part_bytes)
 size_t joint_dbias_part_bytes(int64_t n_max, int V);
 hipError_t launch_joint_dbias_sum(const JointArgs &j, int V, hipStream_t stream);
+// rows [*count_dev, n) of G ([n, V]) and Hact ([n, hact_ld]) as zeros (the live count on the device, n a host bound)
+hipError_t launch_joint_tail_zero(unsigned short *G, int V, unsigned short *Hact, int64_t hact_ld, int64_t n,
+                                  const unsigned long long *count_dev, hipStream_t stream);
 // LDS the fused joint kernels need at least (two weight-tile buffers + the bias row); at most 160 KiB per CU
 size_t joint_min_lds_bytes(int H, int V);
 // ... and the 16x16x32 backward when it sums dbias (one column-sum row per wave more)
@@ -165,7 +168,8 @@ struct Tuning {
                                   // gated loads; development build)
     int chase_delay_us = 0;       // development probe: every chase producer workgroup starts this late
     int chase_probe = 0;          // development probe: ChaseArgs::probe (the staged walk's step cost; results wrong)
-    int chase_pair = 2;           // staged chase walk: frames per dependent log-sum-exp (1: one LSE per frame)
+    int chase_pair = 3;           // staged chase walk: 3 frame pairs, chain only (side values on wave 2); 2 pairs on the
+                                  // walk; 1 one log-sum-exp per frame
     int chase_early_free = 1;     // staged chase walk: ring slots freed when read into registers (0: after their use)
     int chase_ring = 64;          // staged chase walk: cap on the LDS ring's frames (16: round 5's depth)
     int joint_reduce_hact = 1;    // joint reduce: 1 reads Hact; 0 (development build) recomputes the activation from

@@ -590,6 +590,7 @@ template <int KS, int NB, int NW, int RG>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2))) void joint_bwd_kernel(DevProblem p,
                                                                                              JointArgs j) {
     extern __shared__ __attribute__((aligned(16))) unsigned short wsh[];
+    if (j.n_dev && (int64_t)blockIdx.x * (32 * NW) >= list_len(j)) return;  // past the device count (tail zeroed)
     const int lane = threadIdx.x & 63, half = lane >> 5;
     const int64_t i = (int64_t)blockIdx.x * (32 * NW) + (threadIdx.x >> 6) * 32 + (lane & 31);
     const RowPos q = row_pos(p, j, i);
@@ -682,6 +683,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     DevProblem p, JointArgs j) {
     extern __shared__ __attribute__((aligned(16))) unsigned short wsh[];
     constexpr int K32 = KS / 2;
+    if (j.n_dev && (int64_t)blockIdx.x * (32 * NW) >= list_len(j)) {  // past the device count: only its dbias row
+        if (j.dbias)
+            for (int v = threadIdx.x; v < (p.V + 31) / 32 * 32; v += blockDim.x)
+                j.dbias_part[(int64_t)blockIdx.x * ((p.V + 31) / 32 * 32) + v] = 0.0f;
+        return;
+    }
     const int lane = threadIdx.x & 63, c16 = lane & 15, g = lane >> 4;
     const int64_t i0 = (int64_t)blockIdx.x * (32 * NW) + (threadIdx.x >> 6) * 32 + c16;
     const RowPos q[2] = {row_pos(p, j, i0), row_pos(p, j, i0 + 16)};
@@ -828,6 +835,32 @@ __global__ __launch_bounds__(256) void dbias_total_kernel(const float *__restric
 }
 
 int64_t joint_bwd_blocks(int64_t n) { return (n + 255) / 256; }  // the backward's workgroups (8 waves x 32 rows)
+
+// Rows [count, n) of G ([n, V] bf16) and Hact ([n, ld] bf16) as zeros, count = *count_dev (a device-counted live-row
+// list sized by a host bound, JointArgs::n_dev): library GEMMs over all n rows then see zero rows there. Grid-stride
+// 16-byte stores over the tail's byte range (rows are contiguous), 2-byte stores for its unaligned ends.
+__global__ __launch_bounds__(256) void joint_tail_zero_kernel(unsigned short *__restrict__ G, int64_t gld,
+                                                              unsigned short *__restrict__ Hact, int64_t hld, int64_t n,
+                                                              const unsigned long long *__restrict__ count_dev) {
+    const int64_t c = min((int64_t)*count_dev, n);
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (int64_t)gridDim.x * blockDim.x;
+    for (int which = 0; which < 2; ++which) {
+        unsigned short *base = which ? Hact : G;
+        const int64_t ld = which ? hld : gld;
+        const int64_t e0 = c * ld, e1 = n * ld;  // elements
+        const int64_t a0 = min(e1, (e0 + 7) / 8 * 8), a1 = max(a0, e1 / 8 * 8);
+        if (tid < a0 - e0) base[e0 + tid] = 0;
+        if (tid < e1 - a1) base[a1 + tid] = 0;
+        for (int64_t o = a0 + tid * 8; o < a1; o += nth * 8) *reinterpret_cast<u4 *>(base + o) = u4{0u, 0u, 0u, 0u};
+    }
+}
+
+hipError_t launch_joint_tail_zero(unsigned short *G, int V, unsigned short *Hact, int64_t hact_ld, int64_t n,
+                                  const unsigned long long *count_dev, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    joint_tail_zero_kernel<<<2048, 256, 0, stream>>>(G, V, Hact, hact_ld, n, count_dev);
+    return hipGetLastError();
+}
 
 size_t joint_dbias_part_bytes(int64_t n_max, int V) {
     const int64_t vpad = (V + 31) / 32 * 32, nb = joint_bwd_blocks(n_max);

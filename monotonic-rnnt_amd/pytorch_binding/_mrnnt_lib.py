@@ -106,6 +106,8 @@ class MrnntJointProblem(ctypes.Structure):
         # version 9
         ("reduce_scratch", ctypes.c_void_p),
         ("reduce_scratch_bytes", ctypes.c_size_t),
+        # version 12
+        ("live_count_dev", ctypes.c_void_p),
     ]
 
 
@@ -154,6 +156,7 @@ def _bind(path: str, dev: bool = False) -> ctypes.CDLL:
         "mrnnt_joint_reduce": (i, [JP, vp, i64, vp, vp, vp, vp, vp]),
         "mrnnt_joint_reduce_pre": (i, [JP, vp, i64, vp, vp, vp, vp]),
         "mrnnt_joint_reduce_scratch_bytes": (i, [JP, ctypes.POINTER(sz)]),
+        "mrnnt_joint_row_bound": (i, [JP, ctypes.POINTER(i64)]),
         "mrnnt_joint_dpre": (i, [JP, i64, vp, vp, vp, vp, vp]),
         "mrnnt_last_error": (ctypes.c_char_p, []),
         "mrnnt_version": (i, []),
@@ -176,8 +179,8 @@ def _bind(path: str, dev: bool = False) -> ctypes.CDLL:
             raise ImportError(f"{path} does not export {name}")
         fn.restype = res
         fn.argtypes = args
-    if lib.mrnnt_version() < 11:
-        raise ImportError(f"{path} is a stale build (ABI version {lib.mrnnt_version()} < 11); "
+    if lib.mrnnt_version() < 12:
+        raise ImportError(f"{path} is a stale build (ABI version {lib.mrnnt_version()} < 12); "
                           "rebuild with `make -C monotonic-rnnt_amd`")
     return lib
 

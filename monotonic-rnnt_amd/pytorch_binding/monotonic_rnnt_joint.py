@@ -113,16 +113,27 @@ class _JointPrepared:
                                              1 if with_beta else 0, self.stream()), "mrnnt_joint_forward")
         return costs, ws
 
-    def backward_rows(self, ws, grad_scale, with_index=False, bias_column=False, dbias=None):
+    def backward_rows(self, ws, grad_scale, with_index=False, bias_column=False, dbias=None, capturable=False):
         """The fused gradient pass over the live rows: (G [n, V], Hact [n, H]) and, with_index, the enc / pred
         row of each live row (bt_idx, bs_idx). bias_column: Hact is [n, _HACT_LD[H]] with column H = 1 (and zeros
-        after it), so G^T Hact carries dbias = sum_i G[i] in column H (no separate pass over G)."""
+        after it), so G^T Hact carries dbias = sum_i G[i] in column H (no separate pass over G).
+        capturable: no device-to-host read -- n is the host-known bound on the live rows (mrnnt_joint_row_bound: the
+        in-band rows), the kernels take the live count from the device (ABI v12 live_count_dev) and rows past it are
+        zeros, so the step can be captured in a HIP graph; the GEMMs downstream then run over the bound."""
         lib = _L.load()
         with torch.cuda.device(self.device):
             cnt = torch.zeros(1, dtype=torch.int64, device=self.device)
             _L.check(lib.mrnnt_joint_live_rows(ctypes.byref(self.problem), _vp(ws), _vp(cnt), self.stream()),
                      "mrnnt_joint_live_rows")
-            n = int(cnt.item())  # one 8-byte read-back sizes the row buffers
+            if capturable:
+                nb = ctypes.c_int64(0)
+                _L.check(lib.mrnnt_joint_row_bound(ctypes.byref(self.problem), ctypes.byref(nb)), "joint_row_bound")
+                n = nb.value
+                self.live_count = cnt  # referenced by the problem until the backward's last kernel is queued
+                self.problem.live_count_dev = cnt.data_ptr()
+            else:
+                n = int(cnt.item())  # one 8-byte read-back sizes the row buffers
+                self.problem.live_count_dev = None
             G = torch.empty(max(1, n), self.V, dtype=torch.bfloat16, device=self.device)
             ld = _HACT_LD[self.H] if bias_column else self.H
             self.problem.hact_ld = ld  # mrnnt_joint_reduce reads Hact with the same stride
@@ -176,6 +187,7 @@ class _JointPrepared:
 
 
 _BIAS_SUM = os.environ.get("MRNNT_JOINT_BIAS_SUM") == "1"
+_CAPTURABLE = os.environ.get("MRNNT_JOINT_CAPTURABLE") == "1"
 # dH: a library GEMM (hipBLASLt) and the reduce's own multiply by default; MRNNT_JOINT_DH=mfma takes the library's
 # hand-written MFMA kernel with the tanh derivative fused (mrnnt_joint_dpre: H = 256 / 512, V % 8 == 0) -- opt-in
 # while it is slower than the GEMM it replaces (6.1 vs 3.8 ms at H = 512, the reduce 2.7 -> 2.1 ms)
@@ -238,7 +250,7 @@ def _split_k_weight_grad(G, Hact, chunks=32):
 class MonotonicRNNTJointFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, enc, pred, weight, bias, labels, input_lengths, label_lengths, blank_label=0, alignment=None,
-                max_distance_from_alignment=0):
+                max_distance_from_alignment=0, capturable=None):
         prep = _JointPrepared(enc, pred, weight, bias, labels, input_lengths, label_lengths, blank_label, alignment,
                               max_distance_from_alignment)
         need = any(ctx.needs_input_grad[:4])
@@ -248,6 +260,7 @@ class MonotonicRNNTJointFunction(torch.autograd.Function):
             ctx.save_for_backward(enc, pred, weight, ws)
             ctx.prep = prep
             ctx.bias_dtype = None if bias is None else bias.dtype
+            ctx.capturable = capturable
         return costs
 
     @staticmethod
@@ -261,7 +274,9 @@ class MonotonicRNNTJointFunction(torch.autograd.Function):
         fused_b = (need_b and not bias_col and not _BIAS_SUM and _bwd_sums_columns(prep.H)
                    and _dbias_lds_fits(prep.H, prep.V))
         db = torch.zeros(prep.V, dtype=torch.float32, device=prep.device) if fused_b else None
-        G, Hact = prep.backward_rows(ws, grad_costs, bias_column=bias_col, dbias=db)
+        # capturable (no host read of the live-row count): asked for, MRNNT_JOINT_CAPTURABLE=1, or inside HIP-graph capture
+        cap = ctx.capturable if ctx.capturable is not None else (_CAPTURABLE or torch.cuda.is_current_stream_capturing())
+        G, Hact = prep.backward_rows(ws, grad_costs, bias_column=bias_col, dbias=db, capturable=cap)
         d_enc = d_pred = d_w = d_b = None
         H = prep.H
         if ctx.needs_input_grad[2]:
@@ -286,19 +301,23 @@ class MonotonicRNNTJointFunction(torch.autograd.Function):
             del G
             d_enc = None if d_enc is None else d_enc.to(prep.enc.dtype)
             d_pred = None if d_pred is None else d_pred.to(prep.pred.dtype)
-        return d_enc, d_pred, d_w, d_b, None, None, None, None, None, None
+        return d_enc, d_pred, d_w, d_b, None, None, None, None, None, None, None
 
 
 def monotonic_rnnt_joint_loss(enc: torch.Tensor, pred: torch.Tensor, weight: torch.Tensor,
                               bias: Optional[torch.Tensor], labels: torch.Tensor, input_lengths: torch.Tensor,
                               label_lengths: torch.Tensor, blank_label: int = 0,
                               alignment: Optional[torch.Tensor] = None,
-                              max_distance_from_alignment: int = 0) -> torch.Tensor:
+                              max_distance_from_alignment: int = 0, capturable: Optional[bool] = None) -> torch.Tensor:
     """Monotonic RNN-T loss of the joint network tanh(enc + pred) @ weight.T + bias, fused (see module doc).
-    alignment / max_distance_from_alignment restrict the paths as in monotonic_rnnt_loss."""
+    alignment / max_distance_from_alignment restrict the paths as in monotonic_rnnt_loss. capturable: the backward
+    reads no live-row count back to the host (row buffers and GEMMs sized by the in-band rows instead of the live
+    ones: slower, graph-capturable); None = only inside HIP-graph capture (or MRNNT_JOINT_CAPTURABLE=1). A step
+    captured with it replays bit for bit what an eager capturable=True step computes."""
     cast = lambda x: x if x is None or x.dtype == torch.bfloat16 else x.to(torch.bfloat16)  # noqa: E731
     return MonotonicRNNTJointFunction.apply(cast(enc), cast(pred), cast(weight), bias, labels, input_lengths,
-                                            label_lengths, blank_label, alignment, max_distance_from_alignment)
+                                            label_lengths, blank_label, alignment, max_distance_from_alignment,
+                                            capturable)
 
 
 __all__ = ["MonotonicRNNTJointFunction", "monotonic_rnnt_joint_loss"]

@@ -4,8 +4,8 @@ one launch, the recursion workgroups consuming each lattice column as its log-so
 (gpu_rnnt.h:99-191).
 
 Every value the chase computes is the one the two-kernel path computes -- with one deliberate exception: the staged
-one-wave walk (S + 1 <= 64) advances two frames per dependent log-sum-exp by default (chase_pair = 2, a three-term
-step; round 6), which rounds differently. So the tests compare bit for bit against the development build with the
+one-wave walk (S + 1 <= 64) advances two frames per dependent log-sum-exp by default (a three-term step, the first
+frame of each pair formed by a side wave from the chain values: chase_pair = 3; round 6), which rounds differently. So the tests compare bit for bit against the development build with the
 chase off (chase = 0) wherever the chase runs the single-step walk (the development knob chase_pair = 1, the halo
 shapes, the direct form), and within fp64-rounding tolerance (_assert_same with the case's S) where the product's
 paired walk runs; the paired walk is also checked against the oracle. Covered: every log-softmax body the chase
@@ -120,9 +120,12 @@ def test_chase_bit_identical_to_two_kernels(op, dev, name, stage):
         got = _run(op, a, lab, Tt, St, scale=scale)
     assert n["chase"] == 1 and n["log_softmax"] == 0 and n["alpha_beta"] == 0, n
     _assert_same(got, ref)
-    with knobs(chase=1, chase_stage=stage, chase_pair=2):  # the product's frame pairs on the staged walk
+    with knobs(chase=1, chase_stage=stage, chase_pair=2):  # frame pairs, the side step on the walk
         paired = _run(op, a, lab, Tt, St, scale=scale)
     _assert_same(paired, ref, S, stage)
+    with knobs(chase=1, chase_stage=stage, chase_pair=3):  # the product: chain-only walk, side steps on wave 2
+        side = _run(op, a, lab, Tt, St, scale=scale)
+    _assert_same(side, paired)  # the same operations on the same values, split over two waves
     if name.startswith("c2"):  # the product library takes the same launch
         n = _launches(lambda: _run(op, a, lab, Tt, St, scale=scale))
         assert n["chase"] == 1, n

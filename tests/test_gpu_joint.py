@@ -395,3 +395,67 @@ def test_joint_plain_exp_sum_matches_running_max(dev, H, V):
     for x, y, name in zip(a[1:], b[1:], ("d_enc", "d_pred", "d_weight", "d_bias")):
         err = (x.float() - y.float()).abs().max().item()
         assert err <= 2.0 ** -7 * y.float().abs().max().item() + 1e-6, (name, err)
+
+
+def _joint_step(jm, enc, pred, w, bias, labels, T, S, capturable):
+    """costs.sum().backward() of the fused op on leaf tensors; returns (costs, d_enc, d_pred, d_weight, d_bias)."""
+    for x in (enc, pred, w, bias):
+        x.grad = None
+    costs = jm.monotonic_rnnt_joint_loss(enc, pred, w, bias, labels, T, S, capturable=capturable)
+    costs.sum().backward()
+    return (costs.detach().clone(), enc.grad.clone(), pred.grad.clone(), w.grad.clone(), bias.grad.clone())
+
+
+@pytest.mark.parametrize("H,V", [(256, 128), (512, 256), (128, 64), (640, 130)])
+def test_joint_step_graph_capture_replay(dev, H, V):
+    """the joint backward reads no live-row count back to the host when capturable (row buffers
+    and GEMMs sized by mrnnt_joint_row_bound, the kernels take the count from the device, rows past it zero), so a
+    training step captures in torch.cuda.graph. Replays on new inputs equal an eager capturable step bit for bit;
+    the capturable step agrees with the default (count read back) one at the fp32 rounding of the weight GEMM's
+    split-K order; and it makes no device-to-host synchronisation at all."""
+    import monotonic_rnnt_joint as jm
+    enc0, pred0, w0, bias0, labels, T, S = make_case(31 + H, 4, (20, 50), 12, H, V)
+    enc = enc0.to(dev).requires_grad_(True)
+    pred = pred0.to(dev).requires_grad_(True)
+    w = w0.to(dev).requires_grad_(True)
+    bias = bias0.to(dev).requires_grad_(True)
+    lab, Tt, St = torch.from_numpy(labels).to(dev), torch.from_numpy(T), torch.from_numpy(S)
+    # the capturable step against the default one
+    eager_cap = _joint_step(jm, enc, pred, w, bias, lab, Tt, St, True)
+    eager = _joint_step(jm, enc, pred, w, bias, lab, Tt, St, False)
+    assert torch.equal(eager_cap[0], eager[0])
+    for a, b, name in zip(eager_cap[1:], eager[1:], ("d_enc", "d_pred", "d_weight", "d_bias")):
+        close(a, b.double().cpu(), rel=1e-5, name=name)
+    torch.cuda.synchronize()
+    prev = torch.cuda.get_sync_debug_mode()
+    torch.cuda.set_sync_debug_mode("error")  # any device-to-host read in the step raises
+    try:
+        _joint_step(jm, enc, pred, w, bias, lab, Tt, St, True)
+    finally:
+        torch.cuda.set_sync_debug_mode(prev)
+    # capture (warm-up on a side stream first, as torch.cuda.graph asks), then replay on new inputs
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            _joint_step(jm, enc, pred, w, bias, lab, Tt, St, None)
+    torch.cuda.current_stream().wait_stream(s)
+    for x in (enc, pred, w, bias):
+        x.grad = None
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        costs = jm.monotonic_rnnt_joint_loss(enc, pred, w, bias, lab, Tt, St)  # capturable inside capture
+        costs.sum().backward()
+    gen = torch.Generator(device=dev).manual_seed(3)
+    for i in range(3):
+        with torch.no_grad():
+            enc.copy_(torch.randn(enc.shape, device=dev, generator=gen).to(enc.dtype))
+            pred.copy_(torch.randn(pred.shape, device=dev, generator=gen).to(pred.dtype))
+        g.replay()
+        torch.cuda.synchronize()
+        got = (costs.detach().clone(), enc.grad.clone(), pred.grad.clone(), w.grad.clone(), bias.grad.clone())
+        e2, p2 = enc.detach().clone().requires_grad_(True), pred.detach().clone().requires_grad_(True)
+        w2, b2 = w.detach().clone().requires_grad_(True), bias.detach().clone().requires_grad_(True)
+        ref = _joint_step(jm, e2, p2, w2, b2, lab, Tt, St, True)
+        for a, b in zip(got, ref):
+            assert torch.equal(a, b)

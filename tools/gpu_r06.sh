@@ -48,13 +48,20 @@ chase)
   W="python tools/walk_trace.py"
   timeout -k 10 400 python -u -m pytest tests/test_gpu_chase.py -x -q -rs --timeout 120 --timeout-method thread > $O/pytest_chase.log 2>&1
   rc=$?; tail -n 3 $O/pytest_chase.log; [ $rc -eq 0 ] || exit $rc
-  timeout -k 10 200 $W $O/walk_p2_r64.json chase_pair=2 chase_ring=64 > $O/walk_p2_r64.txt 2>&1 && \
-  timeout -k 10 200 $W $O/walk_p1_r64.json chase_pair=1 chase_ring=64 > $O/walk_p1_r64.txt 2>&1 && \
-  timeout -k 10 300 python tools/kbench.py --config c2 --rounds 40 --variants '[{"chase_pair":1,"chase_early_free":0,"chase_ring":16},{"chase_pair":2,"chase_ring":16},{"chase_pair":1,"chase_ring":64},{"chase_pair":2,"chase_ring":64}]' > $O/kbench_c2_ring.json 2> $O/kbench.err
-  rc=$?; echo rc=$rc; for f in p2_r64 p1_r64; do echo == $f; tail -n 4 $O/walk_$f.txt; done
+  timeout -k 10 200 $W $O/walk_p3.json chase_pair=3 > $O/walk_p3.txt 2>&1 && \
+  timeout -k 10 200 $W $O/walk_p3_noring.json chase_pair=3 chase_probe=4 > $O/walk_p3_noring.txt 2>&1 && \
+  timeout -k 10 300 python tools/kbench.py --config c2 --rounds 40 --variants '[{"chase_pair":1,"chase_early_free":0,"chase_ring":16},{"chase_pair":2},{"chase_pair":3}]' > $O/kbench_c2_pair3.json 2> $O/kbench.err && \
+  timeout -k 10 300 python bench.py --config c2 --graph --steps 2000 --warmup 200 > $O/bench_c2_graph.json 2> $O/bench_c2_graph.err && \
+  cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/rocprof_c2 -o run --output-format csv -- python3 $R/bench.py --config c2 --graph --steps 2000 --warmup 200 --no-cpu > $O/bench_c2_graph_prof.json 2> $O/bench_c2_graph_prof.err
+  rc=$?; cd $R; echo rc=$rc; for f in p3 p3_noring; do echo == $f; tail -n 4 $O/walk_$f.txt; done
   python3 -c "
-import json;d=json.load(open('$O/kbench_c2_ring.json'))
-for v in d['variants']: print(v['knobs'], {k: round(x*1e3,2) for k,x in v['median_ms'].items() if x})"; exit $rc ;;
+import json;d=json.load(open('$O/kbench_c2_pair3.json'))
+for v in d['variants']: print(v['knobs'], {k: round(x*1e3,2) for k,x in v['median_ms'].items() if x})
+b=json.load(open('$O/bench_c2_graph.json')); print('c2 graph', b['value'], b['ms_per_step'], b.get('kernels',{}).get('chase'))"
+  find $O/rocprof_c2 -name "*kernel_stats.csv" -exec head -5 {} \; ; exit $rc ;;
+joint)
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_joint.py -x -q -rs --timeout 300 --timeout-method thread > $O/pytest_joint.log 2>&1
+  rc=$?; tail -n 5 $O/pytest_joint.log; exit $rc ;;
 full)
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rs --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 && \
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && \
