@@ -499,7 +499,7 @@ RNNTStatus mrnnt_forward(const mrnnt_problem *p, void *ws, size_t ws_bytes, floa
         ca.delay = kVariants ? (uint32_t)std::max(0, tuning().chase_delay_us) * 100u : 0u;
         ca.stage = kVariants ? tuning().chase_stage : 1;
         ca.probe = kVariants ? tuning().chase_probe : 0;
-        ca.pair = kVariants ? tuning().chase_pair : 3;
+        ca.pair = kVariants ? tuning().chase_pair : 1;
         ca.early_free = kVariants ? tuning().chase_early_free : 1;
         ca.ring = kVariants ? tuning().chase_ring : 64;
         const int nrec = with_beta ? 2 * pl.B : pl.B;
@@ -798,6 +798,7 @@ JointArgs joint_args(const mrnnt_joint_problem *jp, const JointPlan &jl, void *w
     j.lcol = reinterpret_cast<const int *>(w + jl.off_lcol);
     j.ls = reinterpret_cast<const int *>(w + jl.off_ls);
     j.n = n;
+    j.opt = kVariants ? tuning().joint_opt : 3;
     return j;
 }
 
@@ -1072,6 +1073,7 @@ __attribute__((visibility("default"))) int mrnnt_tune(const char *key, int value
     else if (!std::strcmp(key, "joint_dpre_nw")) slot = &t.joint_dpre_nw;
     else if (!std::strcmp(key, "joint_reduce_hact")) slot = &t.joint_reduce_hact;
     else if (!std::strcmp(key, "joint_probe")) slot = &t.joint_probe;
+    else if (!std::strcmp(key, "joint_opt")) slot = &t.joint_opt;
     else if (!std::strcmp(key, "joint_trace")) slot = &t.joint_trace;
     else if (!std::strcmp(key, "joint_reduce_pad")) slot = &t.joint_reduce_pad;
     else if (!std::strcmp(key, "softmax_grid_per_cu")) slot = &t.softmax_grid_per_cu;

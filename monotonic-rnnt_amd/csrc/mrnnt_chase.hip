@@ -186,11 +186,28 @@ struct Chase {
 
 // ---- one-wave recursion with LDS-staged frames -----------------------------------------------------------------
 
-// The LDS ring of lp frames, packed at the frame's width (W = S + 1 rows of 16 bytes): 21 KiB, 32 frames of <= 42 rows
-// (configs[1]), 16 of <= 64. 21 KiB + the counters keeps 7 workgroups per CU, the occupancy the kernel's registers
-// allow its producers anyway; the ring's depth bounds the loader's frames in flight per poll round trip.
-constexpr int kRingLp = 1344;
-__device__ __forceinline__ int ring_frames(int W, int cap) { return min(W <= 21 ? 64 : (W <= 42 ? 32 : 16), cap); }
+// The LDS ring of lp frames, packed at the frame's width (W = S + 1 rows of 16 bytes; the loader's LDS-DMA writes
+// lanes < W only): 16 KiB, the largest power-of-two count of frames that fits (16 at configs[1]'s W = 41, 32 for W <=
+// 32, 64 for W <= 16). Round 6 measured the product launch (rocprofv3, one box, alternating builds: DESIGN.md 6):
+// this ring with ring slots freed as soon as the walk has read them into registers (early_free) 34.2 us against the
+// round-5 ring's 35.8; a 21 KiB ring of 32 frames costs the co-resident producers a workgroup per CU (7 instead of 9)
+// and the launch 37.8 us with frame pairs; the frame-pair walks (PAIR 2 / 3 below) 37.0-41.0 us -- the walk's chain
+// is not what bounds the product launch, the producers' occupancy is.
+#ifndef MRNNT_CHASE_RING_LP  // (product A/B builds of round 6 override these three)
+#define MRNNT_CHASE_RING_LP 1024
+#endif
+#ifndef MRNNT_CHASE_PAIR
+#define MRNNT_CHASE_PAIR 1
+#endif
+#ifndef MRNNT_CHASE_EARLY
+#define MRNNT_CHASE_EARLY 1
+#endif
+constexpr int kRingLp = MRNNT_CHASE_RING_LP;
+__device__ __forceinline__ int ring_frames(int W, int cap) {
+    int r = 64;
+    while (r > 1 && r * W > kRingLp) r >>= 1;  // the largest power of two that fits
+    return min(r, cap);
+}
 
 struct StageLds {
     Lp ring[kRingLp];
@@ -646,7 +663,7 @@ __global__ __launch_bounds__(256) void chase_kernel(DevProblem p, ChaseArgs c, i
                 st.chained[0] = 0;
             }
             __syncthreads();
-            const int pair = kVariants ? c.pair : 3;
+            const int pair = kVariants ? c.pair : MRNNT_CHASE_PAIR;
             if (wave == 2 && pair == 3) {  // the side wave of the chain-only walk
                 if (bwd)
                     beta_side(p, u, st, R);
@@ -660,13 +677,13 @@ __global__ __launch_bounds__(256) void chase_kernel(DevProblem p, ChaseArgs c, i
                 stage_loader(p, u, !bwd, flags, tag, c.budget, help, st, R, kVariants ? c.probe : 0);
                 return;
             }
-            const int probe = kVariants ? c.probe : 0, early = kVariants ? c.early_free : 1;
-            if (kVariants && pair == 1) {  // (development A/B: one log-sum-exp per frame)
+            const int probe = kVariants ? c.probe : 0, early = kVariants ? c.early_free : MRNNT_CHASE_EARLY;
+            if (pair == 1) {  // (development A/B: one log-sum-exp per frame)
                 if (bwd)
                     beta_staged<4, 1>(p, u, b, st, R, probe, early);
                 else
                     alpha_staged<4, 1>(p, u, b, costs, st, R, probe, early);
-            } else if (kVariants && pair == 2) {  // (development A/B: the side step on the walk itself)
+            } else if (pair == 2) {  // (development A/B: the side step on the walk itself)
                 if (bwd)
                     beta_staged<4, 2>(p, u, b, st, R, probe, early);
                 else

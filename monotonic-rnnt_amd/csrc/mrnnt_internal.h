@@ -98,6 +98,8 @@ struct JointArgs {
                                  // (joint_dbias_part_bytes), summed in order by launch_joint_dbias_sum
     const int *wplain;           // forward only: device flag, 1 when no logit can leave [-64, 64] (the weight bound of
                                  // joint_wbound_kernel) -- the epilogue then sums exp(z) without a running max
+    int opt = 3;                 // forward / backward loop forms (development A/B of round 6): bit 0 the weight-chunk DMA
+                                 // from loop-invariant per-lane offsets, bit 1 log2 e folded into a prescaled bias row
     int probe;                   // development build, timing probes (results wrong): forward bit 0 every row's
                                  // activation reads pred row s = 0, bit 1 enc row t = 0, bit 3 the running-max
                                  // epilogue whatever the weight bound; reduce bit 2 no frame barriers / d_enc sum
@@ -168,8 +170,9 @@ struct Tuning {
                                   // gated loads; development build)
     int chase_delay_us = 0;       // development probe: every chase producer workgroup starts this late
     int chase_probe = 0;          // development probe: ChaseArgs::probe (the staged walk's step cost; results wrong)
-    int chase_pair = 3;           // staged chase walk: 3 frame pairs, chain only (side values on wave 2); 2 pairs on the
-                                  // walk; 1 one log-sum-exp per frame
+    int joint_opt = 3;            // JointArgs::opt (development A/B of the round-6 forward loop forms)
+    int chase_pair = 1;           // staged chase walk: 1 one log-sum-exp per frame (the product); development A/B of
+                                  // round 6: 2 frame pairs on the walk, 3 frame pairs with the side values on wave 2
     int chase_early_free = 1;     // staged chase walk: ring slots freed when read into registers (0: after their use)
     int chase_ring = 64;          // staged chase walk: cap on the LDS ring's frames (16: round 5's depth)
     int joint_reduce_hact = 1;    // joint reduce: 1 reads Hact; 0 (development build) recomputes the activation from

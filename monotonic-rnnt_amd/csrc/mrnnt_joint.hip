@@ -275,7 +275,23 @@ struct WTile {
     template <int NW>
     __device__ static __forceinline__ void stage(const JointArgs &j, int V, int c, unsigned short *wbuf) {
         static_assert(NI % NW == 0, "DMA instructions must split evenly over the waves");
-        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        const int lane = threadIdx.x & 63;
+        const int wave = (!kVariants || (j.opt & 1)) ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : threadIdx.x >> 6;
+        if ((!kVariants || (j.opt & 1)) && 32 * c + 32 <= V) {
+            // a whole chunk: a wave-uniform chunk base plus loop-invariant 32-bit lane offsets (no per-chunk 64-bit
+            // address arithmetic or row clamp on the vector pipe; the last partial chunk takes the clamped form)
+            const char *base = reinterpret_cast<const char *>(j.W + (int64_t)32 * c * H);
+#pragma unroll
+            for (int ii = 0; ii < NI / NW; ++ii) {
+                const int i = NW * ii + wave;
+                const int L = 64 * i + lane;
+                const int r = L / CPR, pc = L % CPR;
+                const unsigned off = (unsigned)(r * H + 8 * (pc ^ (r & 15))) * 2u;
+                __builtin_amdgcn_global_load_lds(base + off, (__attribute__((address_space(3))) void *)(wbuf + 512 * i),
+                                                 16, 0, 0);
+            }
+            return;
+        }
 #pragma unroll
         for (int ii = 0; ii < NI / NW; ++ii) {
             const int i = NW * ii + wave;
@@ -458,11 +474,16 @@ __device__ __forceinline__ void chunk_loop(const JointArgs &j, int V, unsigned s
 
 // LDS: NB W tiles, then the bias padded to whole chunks
 template <int KS, int NB>
-__device__ __forceinline__ float *load_bias(const JointArgs &j, int V, unsigned short *wsh) {
+__device__ __forceinline__ float *load_bias(const JointArgs &j, int V, unsigned short *wsh, bool scaled = false) {
     float *bl = reinterpret_cast<float *>(wsh + NB * WTile<KS>::ELEMS);
     const int nb = (V + 31) / 32 * 32;
-    // past V: -inf, so z = acc + bias masks the tail chunk without a compare (the clamped W rows are finite)
-    for (int v = threadIdx.x; v < nb; v += blockDim.x) bl[v] = v < V ? (j.bias ? j.bias[v] : 0.0f) : NEG_INF_F;
+    // past V: -inf, so z = acc + bias masks the tail chunk without a compare (the clamped W rows are finite);
+    // scaled (the forward): a second row, bias * log2 e, right after it
+    for (int v = threadIdx.x; v < nb; v += blockDim.x) {
+        const float b = v < V ? (j.bias ? j.bias[v] : 0.0f) : NEG_INF_F;
+        bl[v] = b;
+        if (scaled) bl[nb + v] = b * kLog2e;
+    }
     return bl;
 }
 
@@ -479,7 +500,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const int64_t i = (int64_t)blockIdx.x * (32 * NW) + (threadIdx.x >> 6) * 32 + (lane & 31);
     const RowPos q = row_pos(p, j, i);
     const int V = p.V, blank = p.blank;
-    const float *bias = load_bias<KS, NB>(j, V, wsh);
+    const float *bias = load_bias<KS, NB>(j, V, wsh, (j.opt & 2) != 0);
     __syncthreads();
     FWD_MARK(1);
     bf16x8 bfr[KS];
@@ -514,7 +535,46 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     // at most e^64 cannot overflow fp32 and the largest cannot underflow -- without the running max, whose
     // per-chunk max / rescale chain cost 15 % of the forward. Otherwise the online log-sum-exp.
     const bool plain = j.wplain != nullptr && *j.wplain != 0;
-    if (plain) {
+    if (plain && (j.opt & 2)) {
+        // exp2(fma(acc, log2 e, bias log2 e)) from a prescaled bias row (bias2, after the bias row in LDS): one fma per
+        // logit where the bias add and the log2 e multiply were two; the captured blank / label logits are still
+        // acc + bias (picked from the accumulator, the bias added to the picked value: the same fp32 add)
+        const float *bias2 = bias + (V + 31) / 32 * 32;
+        chunk_loop<KS, NB, NW, RG, TR>(j, V, wsh, bfr, lane, 0, [&](const f32x16 &acc, int c) {
+            f2 s2 = {0.0f, 0.0f};
+            f2 a2[8];
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+                const f4 bv = *reinterpret_cast<const f4 *>(bias2 + 32 * c + 8 * q4 + 4 * half);
+                a2[2 * q4] = (f2){acc[4 * q4], acc[4 * q4 + 1]};
+                a2[2 * q4 + 1] = (f2){acc[4 * q4 + 2], acc[4 * q4 + 3]};
+                const f2 t0 = fma2(a2[2 * q4], l2e, (f2){bv.x, bv.y});
+                const f2 t1 = fma2(a2[2 * q4 + 1], l2e, (f2){bv.z, bv.w});
+                s2 = add2(s2, (f2){fast_exp2(t0.x), fast_exp2(t0.y)});
+                s2 = add2(s2, (f2){fast_exp2(t1.x), fast_exp2(t1.y)});
+            }
+            sum += s2.x + s2.y;
+            const int jb = blank - 32 * c;
+            if (jb >= 0 && jb < 32) {
+                const int rb = acc_reg_of(jb, half);
+                if (rb >= 0) {
+                    zb = tree_pick(a2, rb) + bias[32 * c + jb];
+                    fb = true;
+                }
+            }
+            const int jl = q.lab - 32 * c;
+            const int rl = acc_reg_of(jl & 31, half);
+            const bool mine = q.lab >= 0 && jl >= 0 && jl < 32 && rl >= 0;
+            if (__ballot(mine)) {
+                const float x = tree_pick(a2, rl) + bias[32 * c + (jl & 31)];
+                if (mine) {
+                    ze = x;
+                    fe = true;
+                }
+            }
+            if (c == 0) FWD_MARK(3);
+        });
+    } else if (plain) {
         chunk_loop<KS, NB, NW, RG, TR>(j, V, wsh, bfr, lane, 0, [&](const f32x16 &acc, int c) {
             f2 z[8];
             logits2(acc, bias, c, half, z);
@@ -528,6 +588,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
             capture(z, c);
             if (c == 0) FWD_MARK(3);
         });
+    }
+    if (plain) {
         sum += __shfl_xor(sum, 32);
         const float zb2 = __shfl_xor(zb, 32), ze2 = __shfl_xor(ze, 32);
         const int fb2 = __shfl_xor((int)fb, 32), fe2 = __shfl_xor((int)fe, 32);
@@ -1213,11 +1275,15 @@ static hipError_t launch_knw(const DevProblem &p, const JointArgs &j, size_t lds
 // and the label logit as a dot product.)
 template <int KS, int MF, bool BWD>
 static hipError_t launch_kt(const DevProblem &p, const JointArgs &j, hipStream_t stream) {
-    // the 16x16x32 backward with dbias keeps one row of column sums per wave (8) behind the bias
-    const size_t bias = sizeof(float) * ((p.V + 31) / 32 * 32) * ((MF == 16 && BWD && j.dbias) ? 9 : 1);
-    if (j.dbias && !(MF == 16 && BWD)) return hipErrorInvalidValue;
+    // the 16x16x32 backward with dbias keeps one row of column sums per wave (8) behind the bias; the forward a
+    // bias * log2 e row (JointArgs::opt bit 1) where both rows fit, the unscaled epilogue otherwise
+    const size_t row = sizeof(float) * ((p.V + 31) / 32 * 32);
     const size_t tile = sizeof(unsigned short) * WTile<KS>::ELEMS;
-    if (2 * tile + bias <= 160 * 1024) return launch_knw<KS, 2, 8, MF, BWD, 2>(p, j, 2 * tile + bias, stream);
+    JointArgs jj = j;
+    if (!BWD && 2 * tile + 2 * row > 160 * 1024) jj.opt &= ~2;
+    const size_t bias = row * ((MF == 16 && BWD && j.dbias) ? 9 : (!BWD && (jj.opt & 2)) ? 2 : 1);
+    if (j.dbias && !(MF == 16 && BWD)) return hipErrorInvalidValue;
+    if (2 * tile + bias <= 160 * 1024) return launch_knw<KS, 2, 8, MF, BWD, 2>(p, jj, 2 * tile + bias, stream);
     return hipErrorInvalidValue;
 }
 

@@ -45,23 +45,34 @@ walkprobe)
   done
   for pr in 4 5 6 7; do echo == probe $pr; grep "alpha walk" $O/walk_p1_probe$pr.txt; done; exit 0 ;;
 chase)
-  W="python tools/walk_trace.py"
   timeout -k 10 400 python -u -m pytest tests/test_gpu_chase.py -x -q -rs --timeout 120 --timeout-method thread > $O/pytest_chase.log 2>&1
   rc=$?; tail -n 3 $O/pytest_chase.log; [ $rc -eq 0 ] || exit $rc
-  timeout -k 10 200 $W $O/walk_p3.json chase_pair=3 > $O/walk_p3.txt 2>&1 && \
-  timeout -k 10 200 $W $O/walk_p3_noring.json chase_pair=3 chase_probe=4 > $O/walk_p3_noring.txt 2>&1 && \
-  timeout -k 10 300 python tools/kbench.py --config c2 --rounds 40 --variants '[{"chase_pair":1,"chase_early_free":0,"chase_ring":16},{"chase_pair":2},{"chase_pair":3}]' > $O/kbench_c2_pair3.json 2> $O/kbench.err && \
-  timeout -k 10 300 python bench.py --config c2 --graph --steps 2000 --warmup 200 > $O/bench_c2_graph.json 2> $O/bench_c2_graph.err && \
-  cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/rocprof_c2 -o run --output-format csv -- python3 $R/bench.py --config c2 --graph --steps 2000 --warmup 200 --no-cpu > $O/bench_c2_graph_prof.json 2> $O/bench_c2_graph_prof.err
-  rc=$?; cd $R; echo rc=$rc; for f in p3 p3_noring; do echo == $f; tail -n 4 $O/walk_$f.txt; done
-  python3 -c "
-import json;d=json.load(open('$O/kbench_c2_pair3.json'))
-for v in d['variants']: print(v['knobs'], {k: round(x*1e3,2) for k,x in v['median_ms'].items() if x})
-b=json.load(open('$O/bench_c2_graph.json')); print('c2 graph', b['value'], b['ms_per_step'], b.get('kernels',{}).get('chase'))"
-  find $O/rocprof_c2 -name "*kernel_stats.csv" -exec head -5 {} \; ; exit $rc ;;
-joint)
-  timeout -k 10 600 python -u -m pytest tests/test_gpu_joint.py -x -q -rs --timeout 300 --timeout-method thread > $O/pytest_joint.log 2>&1
-  rc=$?; tail -n 5 $O/pytest_joint.log; exit $rc ;;
+  VARS="cur r05chase" TAG=$TAG/var MODE=chasevar bash $R/tools/gpu_r06.sh; exit $? ;;
+chaseprod)
+  cd /tmp && export TMPDIR=/tmp
+  for i in 1 2; do
+    for v in new old; do
+      if [ $v = old ]; then export MRNNT_LIB_PATH=$R/monotonic-rnnt_amd/abl/libmonotonic_rnnt_amd_r05chase.so; else unset MRNNT_LIB_PATH; fi
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_${v}_$i -o run --output-format csv -- python3 $R/bench.py --config c2 --graph --steps 2000 --warmup 200 --no-cpu > $O/c2_${v}_$i.json 2> $O/c2_${v}_$i.err || exit 1
+    done
+  done
+  unset MRNNT_LIB_PATH; cd $R
+  for f in $O/prof_*; do echo == $f; find $f -name "*kernel_stats.csv" -exec grep chase {} \; | cut -d, -f1-4; done
+  exit 0 ;;
+chasevar)
+  cd /tmp && export TMPDIR=/tmp
+  for i in 1 2; do
+    for v in ${VARS:-cur r05chase p3r16 p2r16 p1r16 p2r32}; do
+      if [ $v = cur ]; then unset MRNNT_LIB_PATH; else export MRNNT_LIB_PATH=$R/monotonic-rnnt_amd/abl/libmonotonic_rnnt_amd_$v.so; fi
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_${v}_$i -o run --output-format csv -- python3 $R/bench.py --config c2 --graph --steps 2000 --warmup 200 --no-cpu > $O/c2_${v}_$i.json 2> $O/c2_${v}_$i.err || exit 1
+    done
+  done
+  unset MRNNT_LIB_PATH; cd $R
+  for f in $O/prof_*; do python3 -c "
+import csv,json
+r={x['Name'].split('(')[0].split('<')[-1][:40]:round(float(x['AverageNs'])/1000,2) for x in csv.DictReader(open('$f/run_kernel_stats.csv')) if 'chase' in x['Name']}
+print('$f'.split('/')[-1], r)"; done
+  exit 0 ;;
 full)
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rs --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 && \
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && \
