@@ -1057,6 +1057,9 @@ __attribute__((visibility("default"))) int mrnnt_chase_walk_trace(unsigned long 
     return chase_walk_trace(out, n);
 }
 __attribute__((visibility("default"))) int mrnnt_joint_trace(unsigned long long *out, int n) { return joint_trace(out, n); }
+__attribute__((visibility("default"))) int mrnnt_joint_reduce_trace(unsigned long long *out, int n) {
+    return joint_reduce_trace(out, n);
+}
 
 // launch knobs: exported by the development build only (libmonotonic_rnnt_amd_dev.so, `make dev`)
 __attribute__((visibility("default"))) int mrnnt_tune(const char *key, int value) {

@@ -102,7 +102,8 @@ struct JointArgs {
                                  // from loop-invariant per-lane offsets, bit 1 log2 e folded into a prescaled bias row
     int probe;                   // development build, timing probes (results wrong): forward bit 0 every row's
                                  // activation reads pred row s = 0, bit 1 enc row t = 0, bit 3 the running-max
-                                 // epilogue whatever the weight bound; reduce bit 2 no frame barriers / d_enc sum
+                                 // epilogue whatever the weight bound; reduce bit 2 no frame barriers / d_enc sum, bit 4 its
+                                 // timeline stamps (g_reduce_trace)
 };
 
 // Row lists over the lattice: mode 0 = every in-band row, mode 1 = live rows (needs alpha/beta/ll).
@@ -289,6 +290,7 @@ unsigned long long chase_helped(bool reset);
 int chase_trace(unsigned long long *out, int n);  // development build: the chase launch timeline
 int chase_walk_trace(unsigned long long *out, int n);  // development build: walk / loader progress (probe bit 8)
 int joint_trace(unsigned long long *out, int n);  // development build: the fused joint forward's wave timeline
+int joint_reduce_trace(unsigned long long *out, int n);  // development build: the joint reduce's timeline
 hipError_t launch_chase(const DevProblem &p, const ChaseArgs &c, int elem, int S_max, int with_beta, int producers,
                         float *costs, hipStream_t stream);
 hipError_t launch_grad(const DevProblem &p, int elem, const float *scale, void *grads, int grid, hipStream_t stream);

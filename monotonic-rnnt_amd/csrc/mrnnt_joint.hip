@@ -32,6 +32,11 @@ namespace mrnnt {
 // chunk 0: after the DMA wait, after the barrier, after the MFMAs
 constexpr int kJointTraceWgs = 4096;
 __device__ unsigned long long g_joint_trace[kJointTraceWgs * 64];
+// development build, joint_probe bit 4: the reduce's timeline -- thread 0 of the first kRedTraceWgs workgroups stamps
+// [0] start, [1] setup done, [2 + 2f] frame f's rows summed, [3 + 2f] frame f's barriers passed (f < 6), [14] frame
+// loop done, [15] flush done (s_memrealtime, 10 ns)
+constexpr int kRedTraceWgs = 8192;
+__device__ unsigned long long g_reduce_trace[kRedTraceWgs * 16];
 #define JOINT_MARK(i)                                                                                         \
     do {                                                                                                      \
         if ((threadIdx.x & 63) == 0 && blockIdx.x < (unsigned)kJointTraceWgs && threadIdx.x < 512)            \
@@ -641,6 +646,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
 }
 
 #ifdef MRNNT_DEVTOOLS
+int joint_reduce_trace(unsigned long long *out, int n) {
+    n = std::min(n, kRedTraceWgs * 16);
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_reduce_trace), sizeof(unsigned long long) * n) != hipSuccess) return -1;
+    return n;
+}
+
 int joint_trace(unsigned long long *out, int n) {
     n = std::min(n, kJointTraceWgs * 64);
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_joint_trace), sizeof(unsigned long long) * n) != hipSuccess) return -1;
@@ -990,6 +1001,14 @@ __global__ __launch_bounds__(256) void joint_reduce_kernel(DevProblem p, JointAr
         return;
     }
     const int hl = (tid % TPR) * 4, rsub = tid / TPR;
+#ifdef MRNNT_DEVTOOLS
+    const bool trace = (j.probe & 16) && blockIdx.x < (unsigned)kRedTraceWgs;
+#define RED_MARK(i) \
+    do { if (trace && tid == 0) g_reduce_trace[blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define RED_MARK(i) ((void)0)
+#endif
+    RED_MARK(0);
     float *acc = lds;
     float *red = lds + (S + 1) * AP;
     const int64_t tslots = j.enc_sb / H, sslots = j.pred_sb / H;
@@ -998,6 +1017,10 @@ __global__ __launch_bounds__(256) void joint_reduce_kernel(DevProblem p, JointAr
     // last row of each column bound them (a few labels under an alignment restriction, the band otherwise); only
     // that slice of the d_pred accumulator is cleared and flushed (min / max: order-independent)
     __shared__ int srange[2];
+    // the block's list offsets, read once here (kReduceTT frames): the frame loop then starts each frame's row loads
+    // without first waiting for a global load of its offsets
+    __shared__ int64_t soff[kReduceTT + 1];
+    const bool staged_off = t1 - t0 <= kReduceTT;
     if (tid == 0) {
         srange[0] = S + 1;
         srange[1] = -1;
@@ -1006,6 +1029,10 @@ __global__ __launch_bounds__(256) void joint_reduce_kernel(DevProblem p, JointAr
     for (int t = t0 + tid; t < t1; t += 256) {
         const int64_t col = p.col_off[b] + t;
         const int64_t r0 = off[col], r1 = off[col + 1];
+        if (staged_off) {
+            soff[t - t0] = r0;
+            if (t == t1 - 1) soff[t1 - t0] = r1;
+        }
         if (r1 > r0) {
             atomicMin(&srange[0], j.ls[r0]);
             atomicMax(&srange[1], j.ls[r1 - 1]);
@@ -1024,9 +1051,10 @@ __global__ __launch_bounds__(256) void joint_reduce_kernel(DevProblem p, JointAr
         }
     }
     __syncthreads();
+    RED_MARK(1);
     for (int t = t0; t < t1; ++t) {
         const int64_t col = p.col_off[b] + t;
-        const int64_t r0 = off[col], r1 = off[col + 1];
+        const int64_t r0 = staged_off ? soff[t - t0] : off[col], r1 = staged_off ? soff[t - t0 + 1] : off[col + 1];
         float e0 = 0.0f, e1 = 0.0f, e2 = 0.0f, e3 = 0.0f;
         uint2 ev = make_uint2(0u, 0u);
         if constexpr (SRC == kRedTanh)
@@ -1072,6 +1100,7 @@ __global__ __launch_bounds__(256) void joint_reduce_kernel(DevProblem p, JointAr
             }
             continue;
         }
+        if (t - t0 < 6) RED_MARK(2 + 2 * (t - t0));
         float *rr = red + rsub * AP + hl;
         rr[0] = e0;
         rr[1] = e1;
@@ -1085,7 +1114,9 @@ __global__ __launch_bounds__(256) void joint_reduce_kernel(DevProblem p, JointAr
             d_enc[((int64_t)b * tslots + t) * H + h0 + tid] = sum;
         }
         __syncthreads();
+        if (t - t0 < 6) RED_MARK(3 + 2 * (t - t0));
     }
+    RED_MARK(14);
     if (!part) {  // one block per utterance: this workgroup is the one writer
         for (int i = s_lo * HS + tid; i < (s_hi + 1) * HS; i += 256)
             d_pred[((int64_t)b * sslots + i / HS) * H + h0 + i % HS] += acc[i / HS * AP + i % HS];
@@ -1098,6 +1129,8 @@ __global__ __launch_bounds__(256) void joint_reduce_kernel(DevProblem p, JointAr
         rng[2 * bx] = s_lo;
         rng[2 * bx + 1] = s_hi;
     }
+    RED_MARK(15);
+#undef RED_MARK
 }
 
 // d_pred[b, s, :] += the blocks' sums of label position s, in block order (the blocks whose range holds s)

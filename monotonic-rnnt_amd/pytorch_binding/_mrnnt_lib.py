@@ -170,6 +170,7 @@ def _bind(path: str, dev: bool = False) -> ctypes.CDLL:
         sig["mrnnt_chase_trace"] = (i, [ctypes.POINTER(ctypes.c_ulonglong), i])
         sig["mrnnt_chase_walk_trace"] = (i, [ctypes.POINTER(ctypes.c_ulonglong), i])
         sig["mrnnt_joint_trace"] = (i, [ctypes.POINTER(ctypes.c_ulonglong), i])
+        sig["mrnnt_joint_reduce_trace"] = (i, [ctypes.POINTER(ctypes.c_ulonglong), i])
     for name, (res, args) in sig.items():
         fn = getattr(lib, name, None)
         if fn is None and path == HOST_ONLY_PATH and not name.startswith(("mrnnt_cpu", "mrnnt_lattice", "mrnnt_last",
