@@ -1020,7 +1020,7 @@ __global__ __launch_bounds__(256) void joint_reduce_kernel(DevProblem p, JointAr
     // the block's list offsets, read once here (kReduceTT frames): the frame loop then starts each frame's row loads
     // without first waiting for a global load of its offsets
     __shared__ int64_t soff[kReduceTT + 1];
-    const bool staged_off = t1 - t0 <= kReduceTT;
+    const bool staged_off = t1 - t0 <= kReduceTT && !(kVariants && (j.probe & 64));  // (probe bit 6: A/B)
     if (tid == 0) {
         srange[0] = S + 1;
         srange[1] = -1;

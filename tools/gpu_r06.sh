@@ -77,12 +77,13 @@ reducetrace)
   timeout -k 10 600 python -u -m pytest tests/test_gpu_joint.py -x -q -rs --timeout 300 --timeout-method thread > $O/pytest_joint.log 2>&1
   rc=$?; tail -n 2 $O/pytest_joint.log; [ $rc -eq 0 ] || exit $rc
   timeout -k 10 300 python tools/reduce_trace.py $O/reduce_trace.json > $O/reduce_trace.txt 2>&1 && \
-  timeout -k 10 600 python tools/joint_bench.py --no-unfused > $O/joint_h512.json 2> $O/joint_h512.err && \
+  timeout -k 10 600 python tools/joint_bench.py --no-unfused --ab '[{"joint_probe":64},{"joint_probe":0}]' --ab-rounds 9 > $O/joint_h512.json 2> $O/joint_h512.err && \
   MRNNT_JOINT_CAPTURABLE=1 timeout -k 10 600 python tools/joint_bench.py --no-unfused > $O/joint_h512_capturable.json 2> $O/joint_h512_capturable.err
   rc=$?; tail -n 1 $O/reduce_trace.txt | cut -c1-600; python3 -c "
 import json
 for f in ('joint_h512','joint_h512_capturable'):
-    d=json.load(open('$O/%s.json'%f)); print(f, d['fused']['ms_per_step'], d['fused']['kernels_ms'])"; exit $rc ;;
+    d=json.load(open('$O/%s.json'%f)); print(f, d['fused']['ms_per_step'], d['fused']['kernels_ms'])
+for v in json.load(open('$O/joint_h512.json'))['ab']: print(v['knobs'], v['step_ms_median'], v['median_ms'])"; exit $rc ;;
 full)
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rs --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 && \
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && \
