@@ -84,6 +84,30 @@ import json
 for f in ('joint_h512','joint_h512_capturable'):
     d=json.load(open('$O/%s.json'%f)); print(f, d['fused']['ms_per_step'], d['fused']['kernels_ms'])
 for v in json.load(open('$O/joint_h512.json'))['ab']: print(v['knobs'], v['step_ms_median'], v['median_ms'])"; exit $rc ;;
+benches)
+  b() { n=$1; shift; timeout -k 10 400 python bench.py "$@" > $O/bench_$n.json 2> $O/bench_$n.err || { echo "bench $n failed"; exit 1; }; \
+        python3 -c "import json;d=json.load(open('$O/bench_$n.json'));print('$n', d['value'], d['unit'], d['ms_per_step'], (d.get('roofline') or {}).get('frac'), (d.get('roofline') or {}).get('traffic'))"; }
+  b headline
+  b headline_uniform --acts-dist uniform
+  b headline_allrows --tune occ_skip=0 --no-cpu
+  b headline_uniform_allrows --acts-dist uniform --tune occ_skip=0 --no-cpu
+  b c2_graph --config c2 --graph --steps 2000 --warmup 200 --no-cpu
+  b c2_eager --config c2 --steps 200 --warmup 20 --no-cpu
+  b headline_bf16 --acts-dtype bf16 --no-cpu
+  b ragged64 --config ragged64 --no-cpu
+  b align_k2 --align-k 2 --no-cpu
+  b c5 --config c5 --steps 2 --warmup 1 --no-cpu
+  timeout -k 10 600 python tools/joint_bench.py > $O/joint_h512.json 2> $O/joint_h512.err || exit 1
+  MRNNT_JOINT_CAPTURABLE=1 timeout -k 10 600 python tools/joint_bench.py --no-unfused > $O/joint_h512_capturable.json 2> $O/joint_h512_capturable.err || exit 1
+  timeout -k 10 600 python tools/joint_bench.py --H 256 --no-unfused > $O/joint_h256.json 2> $O/joint_h256.err || exit 1
+  python3 -c "
+import json
+for f in ('joint_h512','joint_h512_capturable','joint_h256'):
+    d=json.load(open('$O/%s.json'%f)); print(f, d['fused']['ms_per_step'], d['fused']['utt_per_s'], d['fused']['kernels_ms'], (d.get('unfused') or {}).get('ms_per_step'))"
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/rocprof_c2 -o run --output-format csv -- python3 $R/bench.py --config c2 --graph --steps 500 --warmup 100 --no-cpu > $O/bench_c2_graph_rocprof.json 2> $O/bench_c2_graph_rocprof.err && \
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/rocprof_joint -o run --output-format csv -- python3 $R/tools/joint_bench.py --no-unfused --steps 3 --warmup 1 > $O/joint_h512_rocprof.json 2> $O/joint_h512_rocprof.err
+  rc=$?; rm -f $O/rocprof_c2/run_kernel_trace.csv $O/rocprof_joint/run_kernel_trace.csv; exit $rc ;;
 full)
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rs --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 && \
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && \
