@@ -108,6 +108,21 @@ for f in ('joint_h512','joint_h512_capturable','joint_h256'):
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/rocprof_c2 -o run --output-format csv -- python3 $R/bench.py --config c2 --graph --steps 500 --warmup 100 --no-cpu > $O/bench_c2_graph_rocprof.json 2> $O/bench_c2_graph_rocprof.err && \
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/rocprof_joint -o run --output-format csv -- python3 $R/tools/joint_bench.py --no-unfused --steps 3 --warmup 1 > $O/joint_h512_rocprof.json 2> $O/joint_h512_rocprof.err
   rc=$?; rm -f $O/rocprof_c2/run_kernel_trace.csv $O/rocprof_joint/run_kernel_trace.csv; exit $rc ;;
+sweeps)
+  sha() { python3 -c "import hashlib,sys;print(hashlib.sha256(open(sys.argv[1],'rb').read()).hexdigest())" $1; }
+  L="library $(sha monotonic-rnnt_amd/libmonotonic_rnnt_amd.so)"
+  P="python -u -m pytest -q -rs --timeout 600 --timeout-method thread"
+  f() { n=$1; shift; echo "$L" > $O/$n.log; timeout -k 10 900 env "$@" >> $O/$n.log 2>&1; rc=$?; tail -n 1 $O/$n.log; [ $rc -eq 0 ] || exit $rc; }
+  if [ "${SET:-a}" = b ]; then
+  [ -z "$ONLY_C5" ] && f full_batch_headline_64utt MRNNT_FULL_BATCH=1 $P tests/test_gpu_fullsize.py -k full_batch
+  [ -z "$ONLY_C5" ] && f c4_full_batch_costs_512utt MRNNT_FULL_BATCH=1 $P tests/test_gpu_c4_shards.py
+  f c5_full_batch_costs_64utt MRNNT_FULL_BATCH=1 $P -s -v tests/test_gpu_c5_chunks.py
+  exit 0; fi
+  f fuzz_1000_seed200000 MRNNT_FUZZ_CASES=1000 MRNNT_FUZZ_FIRST=200000 $P tests/test_gpu_fuzz.py -k test_random_case_vs_oracle
+  f fuzz_500_seed210000_chase_pair3 MRNNT_FUZZ_CASES=500 MRNNT_FUZZ_FIRST=210000 MRNNT_FUZZ_TUNE=chase_pair=3 $P tests/test_gpu_fuzz.py -k test_random_case_vs_oracle
+  f fuzz_500_seed220000_chase_pair2 MRNNT_FUZZ_CASES=500 MRNNT_FUZZ_FIRST=220000 MRNNT_FUZZ_TUNE=chase_pair=2 $P tests/test_gpu_fuzz.py -k test_random_case_vs_oracle
+  f joint_fuzz_120_seed11000 MRNNT_JOINT_CASES=120 MRNNT_FUZZ_FIRST=11000 $P tests/test_gpu_joint.py -k random_cases
+  exit 0 ;;
 full)
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rs --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 && \
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && \
