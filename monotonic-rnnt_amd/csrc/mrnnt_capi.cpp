@@ -1074,6 +1074,7 @@ __attribute__((visibility("default"))) int mrnnt_tune(const char *key, int value
     else if (!std::strcmp(key, "dp_lean")) slot = &t.dp_lean;
     else if (!std::strcmp(key, "joint_reduce_sparse")) slot = &t.joint_reduce_sparse;
     else if (!std::strcmp(key, "joint_dpre_nw")) slot = &t.joint_dpre_nw;
+    else if (!std::strcmp(key, "joint_dpre_abl")) slot = &t.joint_dpre_abl;
     else if (!std::strcmp(key, "joint_reduce_hact")) slot = &t.joint_reduce_hact;
     else if (!std::strcmp(key, "joint_probe")) slot = &t.joint_probe;
     else if (!std::strcmp(key, "joint_opt")) slot = &t.joint_opt;

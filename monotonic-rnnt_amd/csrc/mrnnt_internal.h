@@ -181,10 +181,15 @@ struct Tuning {
     int joint_reduce_pad = 1;     // joint reduce: accumulator LDS pitch HS + 1 (0: HS, development A/B; bit-identical)
     int joint_trace = 0;          // development build: the joint forward with its timeline stamps (tools/joint_trace.py)
     int joint_probe = 0;          // development probe: JointArgs::probe of the joint forward (results wrong)
-    int joint_dpre_nw = 0;        // joint dpre GEMM (mrnnt_joint_gemm.hip): 0 -> persistent, G loaded straight into
-                                  // registers, W^T through LDS (8 waves, 32 rows x 256 h each); development build: 1 the
-                                  // same tile one workgroup per tile; both operands through LDS with 8 (two per SIMD,
-                                  // 128 h x 64 rows each) or 4 waves (128 x 128)
+    int joint_dpre_nw = 0;        // joint dpre GEMM (mrnnt_joint_gemm.hip): 0 -> the 16x16x32 form (8 waves, 256 rows x
+                                  // 256 h per workgroup, both operands through LDS, fragments a chunk ahead, DMA issue
+                                  // interleaved with the MFMA groups, LDS-staged epilogue); development build: 1 / 2
+                                  // the 32x32x16 direct / persistent forms (G straight to registers, round 5), 4 / 8 /
+                                  // 42 / 81 / 421 / ... staged 32x32x16 tile shapes (tens digit: waves, then row tiles,
+                                  // stages; trailing 1: LDS epilogue, 2: plain dH), 160-167 the 16x16x32 form's
+                                  // stage / priority / interleave / Hact-prefetch A/Bs
+    int joint_dpre_abl = 0;       // development ablations of the staged dpre forms: bit 0 no epilogue, bit 1 G rows
+                                  // from one L2-resident row tile per XCD (results wrong)
     int col_xcd = 0;              // XCD-chunked column order (visit_col, col_mul < 0; overrides col_scatter): bit 0
                                   // log-softmax, bit 1 gradient
 };

@@ -23,12 +23,11 @@ namespace mrnnt {
 
 typedef __bf16 gbf16x8 __attribute__((ext_vector_type(8)));
 typedef float gf32x16 __attribute__((ext_vector_type(16)));
+typedef float gf32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kGT = 256;          // rows and hidden units per workgroup tile
 constexpr int kGKC = 32;          // k per LDS stage
-constexpr int kGStages = 4;       // LDS stages (3 chunks of DMA in flight beside the MFMAs)
 constexpr int kGImage = kGT * kGKC * 2;              // bytes of one [256][32] bf16 image (16 KiB)
-constexpr int kGStageBytes = 2 * kGImage;            // G image + W^T image
 
 __device__ __forceinline__ float bf16_lo_f(unsigned u) { return __uint_as_float(u << 16); }
 __device__ __forceinline__ float bf16_hi_f(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
@@ -41,6 +40,14 @@ __device__ __forceinline__ void gemm_dma(__amdgpu_buffer_rsrc_t rs, unsigned cha
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)dst, 16, voff, soff, 0, 0);
 }
 
+// The workgroup barrier of the chunk loops: LDS reads of this wave retired (the stage refilled after the barrier is
+// the one every wave read in the previous chunk), then a raw s_barrier. __syncthreads() would also wait vmcnt(0) --
+// its fence covers the LDS-DMA still in flight -- and drain the stages staged ahead at every chunk.
+__device__ __forceinline__ void gemm_barrier() {
+    __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0), vmcnt / expcnt untouched
+    __builtin_amdgcn_s_barrier();
+}
+
 // wait until at most N vector-memory operations of this wave are outstanding (issue order = completion order)
 template <int N>
 __device__ __forceinline__ void gemm_wait_vm() {
@@ -48,15 +55,22 @@ __device__ __forceinline__ void gemm_wait_vm() {
     __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
 
-// NW = 8: two waves per SIMD (256 registers each), wave w computes 128 h (w & 1) x 64 rows (w >> 1) -- one wave's
-// LDS-DMA issue and epilogue run beside the other's MFMAs; NW = 4: one wave per SIMD, 128 h x 128 rows (development
-// build). The fragments, their k order and every accumulation are the same in both: bit-identical results.
-template <int NW>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4, NW / 4))) void joint_dpre_kernel(
+// Both operands through LDS (LDS-DMA), NS stages of 32 k. NW waves; wave w computes 128 h (w & 1) x 32 RT rows
+// (w >> 1), so a workgroup tile is TR = 16 NW RT rows x 256 h. NW = 8, RT = 2: two waves per SIMD, 256 rows;
+// NW = 4, RT = 4: one wave per SIMD, 256 rows; NW = 4, RT = 2, NS = 3: 128 rows in 72 KiB of LDS and 256 registers,
+// so two workgroups share a CU and one's epilogue runs beside the other's MFMAs (WPE = waves per SIMD the register
+// budget allows). The fragments, their k order and every accumulation are the same in all: bit-identical results.
+template <int NW, int RT, int NS, int WPE, int EPI>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void joint_dpre_kernel(
     const unsigned short *__restrict__ G, const unsigned short *__restrict__ Wt, const unsigned short *__restrict__ Hact,
-    int64_t hact_ld, unsigned short *__restrict__ dpre, int64_t n, int V, int H) {
-    constexpr int RT = 4 * 4 / NW;             // 32-row tiles per wave (4 or 2)
-    constexpr int DPI = kGImage / 1024 / NW;   // LDS-DMA wave-instructions per image per wave (4 or 2)
+    int64_t hact_ld, unsigned short *__restrict__ dpre, int64_t n, int V, int H, int abl) {
+    constexpr int TR = 16 * NW * RT;           // rows per tile
+    constexpr int GI = TR * kGKC * 2;          // G image bytes per stage
+    constexpr int WI = kGImage;                // W^T image bytes per stage (256 h)
+    constexpr int SB = GI + WI;
+    constexpr int DG = GI / 1024 / NW;         // LDS-DMA wave-instructions per stage per wave: G, W^T
+    constexpr int DW = WI / 1024 / NW;
+    static_assert(DG >= 1 && DW >= 1 && NS >= 2, "tile shape");
     extern __shared__ __attribute__((aligned(16))) unsigned char glds[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -66,33 +80,40 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4,
     const int64_t xcd = b & 7, j = b >> 3;
     const int hh = (int)(j % nh);
     const int64_t rt = (j / nh) * 8 + xcd;
-    const int64_t r0 = rt * kGT;
+    const int64_t r0 = rt * TR;
     if (r0 >= n) return;
     const int h0 = hh * kGT;
-    const int rows = (int)min<int64_t>(kGT, n - r0);
+    const int rows = (int)min<int64_t>(TR, n - r0);
+    if ((abl & 4) && b >= 256 && b < 512) {  // development: the second workgroup of each CU starts ~half a tile late
+        for (int i = 0; i < 2; ++i) __builtin_amdgcn_s_sleep(127);
+    }
     // buffer resources over this tile's rows of G (rows past n read as zero) and of W^T
+    // development ablation (joint_dpre_abl bit 1): every tile reads the G rows of row tile xcd (L2-resident)
+    const int64_t rg0 = (abl & 2) ? (int64_t)xcd * TR : r0;
     const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<unsigned short *>(G) + r0 * V, (short)0, rows * V * 2, 0x00020000);
+        const_cast<unsigned short *>(G) + rg0 * V, (short)0, rows * V * 2, 0x00020000);
     const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<unsigned short *>(Wt) + (int64_t)h0 * V, (short)0, kGT * V * 2, 0x00020000);
-    unsigned voff[DPI];
-#pragma unroll
-    for (int i = 0; i < DPI; ++i) {
-        const int row = 16 * (DPI * wave + i) + (lane >> 2);
+    auto src_off = [&](int piece16) {  // 16-row piece of an image -> this lane's source offset (swizzle on the source)
+        const int row = 16 * piece16 + (lane >> 2);
         const int p = (lane & 3) ^ ((row >> 2) & 3);
-        voff[i] = (unsigned)(row * V + 8 * p) * 2u;
-    }
+        return (unsigned)(row * V + 8 * p) * 2u;
+    };
+    unsigned goff[DG], woff[DW];
+#pragma unroll
+    for (int i = 0; i < DG; ++i) goff[i] = src_off(DG * wave + i);
+#pragma unroll
+    for (int i = 0; i < DW; ++i) woff[i] = src_off(DW * wave + i);
     const int nch = (V + kGKC - 1) / kGKC;
     auto stage = [&](int c) {
-        unsigned char *s = glds + (c % kGStages) * kGStageBytes;
+        unsigned char *s = glds + (c % NS) * SB;
 #pragma unroll
-        for (int i = 0; i < DPI; ++i) {
-            gemm_dma(rg, s + 1024 * (DPI * wave + i), voff[i] + (unsigned)(c * kGKC * 2), 0u);
-            gemm_dma(rw, s + kGImage + 1024 * (DPI * wave + i), voff[i] + (unsigned)(c * kGKC * 2), 0u);
-        }
+        for (int i = 0; i < DG; ++i) gemm_dma(rg, s + 1024 * (DG * wave + i), goff[i] + (unsigned)(c * kGKC * 2), 0u);
+#pragma unroll
+        for (int i = 0; i < DW; ++i) gemm_dma(rw, s + GI + 1024 * (DW * wave + i), woff[i] + (unsigned)(c * kGKC * 2), 0u);
     };
 #pragma unroll
-    for (int c = 0; c < kGStages - 1; ++c)
+    for (int c = 0; c < NS - 1; ++c)
         if (c < nch) stage(c);
 
     const int wh = wave & 1, wr = wave >> 1;  // this wave: h 128 wh .. +128, rows 32 RT wr .. +32 RT of the tile
@@ -106,15 +127,17 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4,
             for (int e = 0; e < 16; ++e) acc[a][q][e] = 0.0f;
 
     for (int c = 0; c < nch; ++c) {
-        // chunk c landed for this wave (its later chunks' DMA stays in flight), then for every wave
-        constexpr int kPer = 2 * DPI;
-        if (c + 2 < nch) gemm_wait_vm<2 * kPer>();
-        else if (c + 1 < nch) gemm_wait_vm<kPer>();
+        // chunk c landed for this wave (the chunks staged after it stay in flight), then for every wave
+        constexpr int kPer = DG + DW;
+        const int later = min(NS - 2, nch - 1 - c);
+        if (later >= 3) gemm_wait_vm<(NS - 2 >= 3 ? 3 : 0) * kPer>();
+        else if (later == 2) gemm_wait_vm<2 * kPer>();
+        else if (later == 1) gemm_wait_vm<kPer>();
         else gemm_wait_vm<0>();
-        __syncthreads();
-        if (c + kGStages - 1 < nch) stage(c + kGStages - 1);  // into the stage every wave finished with at c - 1
-        const unsigned char *s = glds + (c % kGStages) * kGStageBytes;
-        const unsigned char *gi = s, *wi = s + kGImage;
+        gemm_barrier();
+        if (c + NS - 1 < nch) stage(c + NS - 1);  // into the stage every wave finished with at c - 1
+        const unsigned char *s = glds + (c % NS) * SB;
+        const unsigned char *gi = s, *wi = s + GI;
         const bool tail = (c + 1) * kGKC > V;  // k past V in this chunk: those fragments are zeroed (both operands)
 #pragma unroll
         for (int ks = 0; ks < kGKC / 16; ++ks) {
@@ -140,6 +163,90 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4,
         }
     }
 
+    if constexpr (EPI == 2) {
+        // development: plain dH (no tanh derivative, no Hact read) through the LDS-staged copy-out
+        constexpr int EI = TR / 2 / NW;
+        gemm_barrier();
+#pragma unroll
+        for (int q = 0; q < RT; ++q) {
+            const int row = 32 * RT * wr + 32 * q + l32;
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int U = 16 * wh + 4 * a + g;
+                    *reinterpret_cast<uint2 *>(glds + row * 512 + ((U ^ (row & 15)) << 4) + half * 8) =
+                        make_uint2(IoBF16::pack2(acc[a][q][4 * g], acc[a][q][4 * g + 1]),
+                                   IoBF16::pack2(acc[a][q][4 * g + 2], acc[a][q][4 * g + 3]));
+                }
+        }
+        gemm_barrier();
+#pragma unroll
+        for (int i = 0; i < EI; ++i) {
+            const int row = 2 * (EI * wave + i) + (lane >> 5);
+            const uint4 v = *reinterpret_cast<const uint4 *>(glds + 1024 * (EI * wave + i) + 16 * lane);
+            if (row < rows)
+                *reinterpret_cast<uint4 *>(dpre + (r0 + row) * H + h0 + 8 * ((lane & 31) ^ (row & 15))) = v;
+        }
+        return;
+    }
+    if constexpr (EPI == 1) {
+        // The epilogue through LDS (the stages are free once every wave is past its last chunk): the tile's Hact rows
+        // land by LDS-DMA, 2 rows of 256 h per wave-instruction, the 16-byte unit u of row r stored at slot
+        // u ^ (r & 15); each lane turns its own 8-byte Hact pieces into dpre in place (a lane reads and writes only
+        // its pieces); then every wave copies 2 whole rows per 16-byte-per-lane store.
+        static_assert(TR * kGT * 2 <= NS * SB, "the Hact tile fits the stages");
+        constexpr int EI = TR / 2 / NW;  // 1 KiB pieces per wave
+        gemm_barrier();
+        const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<unsigned short *>(Hact) + r0 * hact_ld, (short)0, (int)(rows * hact_ld * 2), 0x00020000);
+#pragma unroll
+        for (int i = 0; i < EI; ++i) {
+            const int row = 2 * (EI * wave + i) + (lane >> 5);
+            const int u = (lane & 31) ^ (row & 15);
+            gemm_dma(rh, glds + 1024 * (EI * wave + i), (unsigned)(row * hact_ld + h0 + 8 * u) * 2u, 0u);
+        }
+        gemm_wait_vm<0>();
+        gemm_barrier();
+#pragma unroll
+        for (int q = 0; q < RT; ++q) {
+            const int row = 32 * RT * wr + 32 * q + l32;
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int U = 16 * wh + 4 * a + g;
+                    uint2 *pp = reinterpret_cast<uint2 *>(glds + row * 512 + ((U ^ (row & 15)) << 4) + half * 8);
+                    const uint2 hv = *pp;
+                    const float h0v = bf16_lo_f(hv.x), h1v = bf16_hi_f(hv.x);
+                    const float h2v = bf16_lo_f(hv.y), h3v = bf16_hi_f(hv.y);
+                    const float d0 = acc[a][q][4 * g] * (1.0f - h0v * h0v), d1 = acc[a][q][4 * g + 1] * (1.0f - h1v * h1v);
+                    const float d2 = acc[a][q][4 * g + 2] * (1.0f - h2v * h2v);
+                    const float d3 = acc[a][q][4 * g + 3] * (1.0f - h3v * h3v);
+                    *pp = make_uint2(IoBF16::pack2(d0, d1), IoBF16::pack2(d2, d3));
+                }
+        }
+        gemm_barrier();
+#pragma unroll
+        for (int i = 0; i < EI; ++i) {
+            const int row = 2 * (EI * wave + i) + (lane >> 5);
+            const uint4 v = *reinterpret_cast<const uint4 *>(glds + 1024 * (EI * wave + i) + 16 * lane);
+            if (row < rows)
+                *reinterpret_cast<uint4 *>(dpre + (r0 + row) * H + h0 + 8 * ((lane & 31) ^ (row & 15))) = v;
+        }
+        return;
+    }
+    if (abl & 1) {  // development ablation (joint_dpre_abl bit 0): no epilogue, the accumulators kept live
+        float sum = 0.0f;
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int q = 0; q < RT; ++q)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) sum += acc[a][q][e];
+        if (sum == 1.25e30f) dpre[r0 * H] = 1;
+        return;
+    }
     // epilogue: lane (l32, half) holds row r = r0 + 32 RT wr + 32 q + l32 and, in register 4 g + e of tile (a, q),
     // hidden unit h = h0 + 128 wh + 32 a + 8 g + 4 half + e
 #pragma unroll
@@ -161,6 +268,235 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4,
                 *reinterpret_cast<uint2 *>(orow + h) = make_uint2(IoBF16::pack2(d0, d1), IoBF16::pack2(d2, d3));
             }
     }
+}
+
+// The 16x16x32 form (joint_dpre_nw = 16x): v_mfma_f32_16x16x32_bf16 (the shape that holds the clock better on random
+// operands), both operands through LDS by LDS-DMA in NS stages of 32 k, tile 256 rows x 256 h, 8 waves (two per SIMD)
+// of 64 rows x 128 h: per chunk a wave issues 12 ds_read_b128 (8 W^T + 4 G fragments) and 32 MFMAs. A chunk's
+// fragments are read one chunk ahead: the wait and barrier of chunk c retire chunk c + 1's DMA, so the reads of c + 1
+// go out beside the MFMAs of c and the MFMA stream does not stop at the barrier for an LDS round trip. The image of
+// a 32-k chunk holds row r's 16-byte piece p at slot p ^ (3 ((r >> 3) & 1)): the 16 lanes of every ds_read_b128 group
+// (rows l & 15, pieces l >> 4) land on 16 distinct bank quads. PRIO: s_setprio 1 around each MFMA cluster.
+__device__ __forceinline__ int k16_swz(int row) { return 3 * ((row >> 3) & 1); }
+
+template <int NS, bool PRIO, bool IL, bool HP>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void joint_dpre_k16_kernel(
+    const unsigned short *__restrict__ G, const unsigned short *__restrict__ Wt, const unsigned short *__restrict__ Hact,
+    int64_t hact_ld, unsigned short *__restrict__ dpre, int64_t n, int V, int H) {
+    constexpr int NW = 8, TR = kGT;
+    constexpr int GI = TR * kGKC * 2, WI = kGT * kGKC * 2, SB = GI + WI;  // 16 + 16 KiB per stage
+    constexpr int DG = GI / 1024 / NW, DW = WI / 1024 / NW;              // 2 + 2 DMA wave-instructions per stage
+    static_assert(NS >= 4 && TR * kGT * 2 <= NS * SB, "the Hact tile of the epilogue fits the stages");
+    static_assert(!HP || NS == 4, "the Hact prefetch maps its four quarters onto the four stage slots");
+    extern __shared__ __attribute__((aligned(16))) unsigned char glds[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nh = H / kGT;
+    const int64_t b = blockIdx.x;
+    const int64_t xcd = b & 7, j = b >> 3;
+    const int hh = (int)(j % nh);
+    const int64_t r0 = ((j / nh) * 8 + xcd) * TR;
+    if (r0 >= n) return;
+    const int h0 = hh * kGT;
+    const int rows = (int)min<int64_t>(TR, n - r0);
+    const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<unsigned short *>(G) + r0 * V, (short)0, rows * V * 2, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<unsigned short *>(Wt) + (int64_t)h0 * V, (short)0, kGT * V * 2, 0x00020000);
+    auto src_off = [&](int piece16) {
+        const int row = 16 * piece16 + (lane >> 2);
+        return (unsigned)(row * V + 8 * ((lane & 3) ^ k16_swz(row))) * 2u;
+    };
+    unsigned goff[DG], woff[DW];
+#pragma unroll
+    for (int i = 0; i < DG; ++i) goff[i] = src_off(DG * wave + i);
+#pragma unroll
+    for (int i = 0; i < DW; ++i) woff[i] = src_off(DW * wave + i);
+    const int nch = (V + kGKC - 1) / kGKC;
+    auto stage = [&](int c) {
+        unsigned char *st = glds + (c % NS) * SB;
+#pragma unroll
+        for (int i = 0; i < DG; ++i) gemm_dma(rg, st + 1024 * (DG * wave + i), goff[i] + (unsigned)(c * kGKC * 2), 0u);
+#pragma unroll
+        for (int i = 0; i < DW; ++i) gemm_dma(rw, st + GI + 1024 * (DW * wave + i), woff[i] + (unsigned)(c * kGKC * 2), 0u);
+    };
+    constexpr int kPer = DG + DW;
+    // wait until chunk `want` of this wave landed, given chunks up to `issued` were staged (in order)
+    auto wait_chunk = [&](int want, int issued) {
+        const int later = min(issued, nch - 1) - want;
+        if (later >= 3) gemm_wait_vm<3 * kPer>();
+        else if (later == 2) gemm_wait_vm<2 * kPer>();
+        else if (later == 1) gemm_wait_vm<kPer>();
+        else gemm_wait_vm<0>();
+    };
+    const int wh = wave & 1, wr = wave >> 1;  // this wave: h 128 wh .. +128, rows 64 wr .. +64 of the tile
+    const int l16 = lane & 15, pc = lane >> 4;
+    // fragment offsets inside an image: row 16 t + l16 (t = tile), piece pc; the swizzle depends on l16 alone
+    const int foff = l16 * 64 + ((pc ^ k16_swz(l16)) << 4);
+    const int aoff = GI + (128 * wh) * 64 + foff;  // W^T rows 128 wh + 16 a + l16: + 1024 a
+    const int boff = (64 * wr) * 64 + foff;        // G rows 64 wr + 16 q + l16: + 1024 q
+    const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<unsigned short *>(Hact) + r0 * hact_ld, (short)0, (int)(rows * hact_ld * 2), 0x00020000);
+    // one 1 KiB piece (2 rows of 256 h) of the epilogue's Hact image: the 16-byte unit u of row r at slot u ^ (r & 15)
+    auto hact_piece = [&](int P) {
+        const int row = 2 * P + (lane >> 5);
+        const int u = (lane & 31) ^ (row & 15);
+        gemm_dma(rh, glds + 1024 * P, (unsigned)(row * hact_ld + h0 + 8 * u) * 2u, 0u);
+    };
+    // HP: the Hact image is staged during the last three chunks, quarter Q (64 rows, 32 KiB) into stage slot Q as
+    // soon as that slot's chunk is in registers: two quarters at chunk nch - 3, one at each of the last two
+    const bool hp = HP && nch >= NS;
+    gf32x4 acc[8][4];
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[a][q] = (gf32x4){0.0f, 0.0f, 0.0f, 0.0f};
+    auto read_frags = [&](int c, gbf16x8 (&fa)[8], gbf16x8 (&fb)[4]) {
+        const unsigned char *st = glds + (c % NS) * SB;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) fb[q] = *reinterpret_cast<const gbf16x8 *>(st + boff + 1024 * q);
+#pragma unroll
+        for (int a = 0; a < 8; ++a) fa[a] = *reinterpret_cast<const gbf16x8 *>(st + aoff + 1024 * a);
+    };
+    auto mma = [&](int c, gbf16x8 (&fa)[8], gbf16x8 (&fb)[4]) {
+        if ((c + 1) * kGKC > V && c * kGKC + 8 * pc >= V) {  // k past V: zero both operands
+#pragma unroll
+            for (int a = 0; a < 8; ++a) fa[a] = (gbf16x8){};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) fb[q] = (gbf16x8){};
+        }
+        if (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int a = 0; a < 8; ++a)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[a][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], fb[q], acc[a][q], 0, 0, 0);
+        if (PRIO) __builtin_amdgcn_s_setprio(0);
+    };
+#pragma unroll
+    for (int c = 0; c < NS - 1; ++c)
+        if (c < nch) stage(c);
+    wait_chunk(0, NS - 2);
+    gemm_barrier();
+    gbf16x8 fa0[8], fb0[4], fa1[8], fb1[4];
+    read_frags(0, fa0, fb0);
+    // iteration c: chunk c + 1 retired and visible (wait + barrier), chunk c + NS - 1 staged into the slot read last
+    // at c - 1, chunk c + 1's fragments read, chunk c's MFMAs
+    // IL: the chunk's 4 DMA pieces and 12 fragment reads issued between its 4 groups of 8 MFMAs (an LDS-DMA issue
+    // costs ~60-185 cycles of the issuing wave; issued together after the barrier, both waves of a SIMD stall there)
+    auto step = [&](int c, gbf16x8 (&fa)[8], gbf16x8 (&fb)[4], gbf16x8 (&na)[8], gbf16x8 (&nb)[4]) {
+        if (c + 1 < nch) {
+            if (hp && c == nch - 2) gemm_wait_vm<8>();  // chunk nch - 1; the two Hact quarters issued after it fly on
+            else wait_chunk(c + 1, c + NS - 2);
+        }
+        gemm_barrier();
+        if constexpr (!IL) {
+            if (c + NS - 1 < nch) stage(c + NS - 1);
+            if (c + 1 < nch) read_frags(c + 1, na, nb);
+            mma(c, fa, fb);
+        } else {
+            const bool st = c + NS - 1 < nch, rd = c + 1 < nch;
+            unsigned char *sd = glds + ((c + NS - 1) % NS) * SB;
+            const unsigned char *sr = glds + ((c + 1) % NS) * SB;
+            const unsigned ko = (unsigned)((c + NS - 1) * kGKC * 2);
+            if ((c + 1) * kGKC > V && c * kGKC + 8 * pc >= V) {  // k past V: zero both operands
+#pragma unroll
+                for (int a = 0; a < 8; ++a) fa[a] = (gbf16x8){};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) fb[q] = (gbf16x8){};
+            }
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                if (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+                for (int a = 2 * g; a < 2 * g + 2; ++a)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        acc[a][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], fb[q], acc[a][q], 0, 0, 0);
+                if (PRIO) __builtin_amdgcn_s_setprio(0);
+                __builtin_amdgcn_sched_barrier(0);
+                if (st) {
+                    if (g < 2) gemm_dma(rg, sd + 1024 * (DG * wave + g), goff[g] + ko, 0u);
+                    else gemm_dma(rw, sd + GI + 1024 * (DW * wave + g - 2), woff[g - 2] + ko, 0u);
+                } else if (hp && c >= nch - 3) {
+                    // quarter Q = slot: pieces 32 Q + 4 wave + i of the image
+                    if (c == nch - 3) {
+                        hact_piece(32 * ((c - 1) % NS) + 4 * wave + g);
+                        hact_piece(32 * (c % NS) + 4 * wave + g);
+                    } else {
+                        hact_piece(32 * (c % NS) + 4 * wave + g);
+                    }
+                }
+                if (rd) {
+                    if (g == 0) {
+#pragma unroll
+                        for (int q = 0; q < 3; ++q) nb[q] = *reinterpret_cast<const gbf16x8 *>(sr + boff + 1024 * q);
+                    } else if (g == 1) {
+                        nb[3] = *reinterpret_cast<const gbf16x8 *>(sr + boff + 3072);
+                        na[0] = *reinterpret_cast<const gbf16x8 *>(sr + aoff);
+                        na[1] = *reinterpret_cast<const gbf16x8 *>(sr + aoff + 1024);
+                    } else {
+#pragma unroll
+                        for (int a = 3 * g - 4; a < 3 * g - 1; ++a)
+                            na[a] = *reinterpret_cast<const gbf16x8 *>(sr + aoff + 1024 * a);
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+    };
+    int c = 0;
+    for (; c + 1 < nch; c += 2) {
+        step(c, fa0, fb0, fa1, fb1);
+        step(c + 1, fa1, fb1, fa0, fb0);
+    }
+    if (c < nch) step(c, fa0, fb0, fa1, fb1);
+
+    // epilogue through LDS, as joint_dpre_kernel's EPI = 1: lane (l16, pc) holds row 64 wr + 16 q + l16 and, in
+    // register e of tile (a, q), hidden unit 128 wh + 16 a + 4 pc + e
+    constexpr int EI = TR / 2 / NW;
+    gemm_barrier();
+    if (!hp) {
+#pragma unroll
+        for (int i = 0; i < EI; ++i) hact_piece(EI * wave + i);
+    }
+    gemm_wait_vm<0>();
+    gemm_barrier();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int row = 64 * wr + 16 * q + l16;
+#pragma unroll
+        for (int a = 0; a < 8; ++a) {
+            const int U = 16 * wh + 2 * a + (pc >> 1);
+            uint2 *pp = reinterpret_cast<uint2 *>(glds + row * 512 + ((U ^ (row & 15)) << 4) + (pc & 1) * 8);
+            const uint2 hv = *pp;
+            const float h0v = bf16_lo_f(hv.x), h1v = bf16_hi_f(hv.x), h2v = bf16_lo_f(hv.y), h3v = bf16_hi_f(hv.y);
+            const float d0 = acc[a][q][0] * (1.0f - h0v * h0v), d1 = acc[a][q][1] * (1.0f - h1v * h1v);
+            const float d2 = acc[a][q][2] * (1.0f - h2v * h2v), d3 = acc[a][q][3] * (1.0f - h3v * h3v);
+            *pp = make_uint2(IoBF16::pack2(d0, d1), IoBF16::pack2(d2, d3));
+        }
+    }
+    gemm_barrier();
+#pragma unroll
+    for (int i = 0; i < EI; ++i) {
+        const int row = 2 * (EI * wave + i) + (lane >> 5);
+        const uint4 v = *reinterpret_cast<const uint4 *>(glds + 1024 * (EI * wave + i) + 16 * lane);
+        if (row < rows) *reinterpret_cast<uint4 *>(dpre + (r0 + row) * H + h0 + 8 * ((lane & 31) ^ (row & 15))) = v;
+    }
+}
+
+template <int NS, bool PRIO, bool IL, bool HP = false>
+static hipError_t launch_dpre_k16(const unsigned short *G, const unsigned short *Wt, const unsigned short *Hact,
+                                  int64_t hact_ld, unsigned short *dpre, int64_t n, int V, int H, hipStream_t stream) {
+    const size_t lds = (size_t)NS * 2 * kGT * kGKC * 2;
+    const int64_t rtiles = (n + kGT - 1) / kGT;
+    const int64_t blocks = ((rtiles + 7) / 8) * 8 * (H / kGT);
+    if (blocks > 0x7fffffff / 512) return hipErrorInvalidValue;
+    auto kern = joint_dpre_k16_kernel<NS, PRIO, IL, HP>;
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    kern<<<(unsigned)blocks, 512, lds, stream>>>(G, Wt, Hact, hact_ld, dpre, n, V, H);
+    return hipGetLastError();
 }
 
 // Every buffer access below puts the whole offset (row, piece and k chunk) in voffset, none in soffset: a raw buffer's
@@ -289,7 +625,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         } else {
             gemm_wait_vm<0>();
         }
-        __syncthreads();
+        gemm_barrier();
         if (c + kDStages - 1 < nch) stage(c + kDStages - 1);
         dchunk_mma<TAILV>(glds + (c % kDStages) * kDImage, aoff, gc, acc, c * kDKC, hf, V);
     };
@@ -321,14 +657,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         }
 }
 
-template <int NW>
+template <int NW, int RT, int NS, int WPE, int EPI>
 static hipError_t launch_dpre_nw(const unsigned short *G, const unsigned short *Wt, const unsigned short *Hact,
-                                 int64_t hact_ld, unsigned short *dpre, int64_t n, int V, int H, int64_t blocks,
-                                 size_t lds, hipStream_t stream) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(joint_dpre_kernel<NW>),
+                                 int64_t hact_ld, unsigned short *dpre, int64_t n, int V, int H, hipStream_t stream) {
+    constexpr int TR = 16 * NW * RT;
+    const size_t lds = (size_t)NS * (TR + kGT) * kGKC * 2;
+    const int64_t rtiles = (n + TR - 1) / TR;
+    const int64_t blocks = ((rtiles + 7) / 8) * 8 * (H / kGT);  // (row tile, h-half) pairs in XCD order; extras exit
+    if (blocks > 0x7fffffff / 512) return hipErrorInvalidValue;
+    auto kern = joint_dpre_kernel<NW, RT, NS, WPE, EPI>;
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    joint_dpre_kernel<NW><<<(unsigned)blocks, 64 * NW, lds, stream>>>(G, Wt, Hact, hact_ld, dpre, n, V, H);
+    kern<<<(unsigned)blocks, 64 * NW, lds, stream>>>(G, Wt, Hact, hact_ld, dpre, n, V, H, tuning().joint_dpre_abl);
     return hipGetLastError();
 }
 
@@ -431,7 +772,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         else if (after >= 8) gemm_wait_vm<8>();
         else if (after >= 4) gemm_wait_vm<4>();
         else gemm_wait_vm<0>();
-        __syncthreads();
+        gemm_barrier();
         stage(q + kDStages - 1);
         const int k = q / nch, c = q - k * nch;
         dchunk_mma<TAILV>(glds + (q % kDStages) * kDImage, aoff, gc, acc, c * kDKC, hf, V);
@@ -510,18 +851,39 @@ hipError_t launch_joint_dpre(const unsigned short *G, const unsigned short *Wt, 
     const int64_t rtiles = (n + kGT - 1) / kGT;
     const int64_t blocks = ((rtiles + 7) / 8) * 8 * nh;  // (row tile, h-half) pairs in XCD order; extras exit
     if (blocks > 0x7fffffff / 512) return hipErrorInvalidValue;
-    const size_t lds = (size_t)kGStages * kGStageBytes;
     if constexpr (kVariants) {
-        if (tuning().joint_dpre_nw == 4) return launch_dpre_nw<4>(G, Wt, Hact, hact_ld, dpre, n, V, H, blocks, lds, stream);
-        if (tuning().joint_dpre_nw == 8) return launch_dpre_nw<8>(G, Wt, Hact, hact_ld, dpre, n, V, H, blocks, lds, stream);
+        switch (tuning().joint_dpre_nw) {
+        case 4: return launch_dpre_nw<4, 4, 4, 1, 0>(G, Wt, Hact, hact_ld, dpre, n, V, H, stream);
+        case 8: return launch_dpre_nw<8, 2, 4, 2, 0>(G, Wt, Hact, hact_ld, dpre, n, V, H, stream);
+        case 81: return launch_dpre_nw<8, 2, 4, 2, 1>(G, Wt, Hact, hact_ld, dpre, n, V, H, stream);
+        case 42: return launch_dpre_nw<4, 2, 3, 2, 0>(G, Wt, Hact, hact_ld, dpre, n, V, H, stream);
+        case 421: return launch_dpre_nw<4, 2, 3, 2, 1>(G, Wt, Hact, hact_ld, dpre, n, V, H, stream);
+        case 431: return launch_dpre_nw<4, 2, 4, 2, 1>(G, Wt, Hact, hact_ld, dpre, n, V, H, stream);
+        case 851: return launch_dpre_nw<8, 2, 5, 2, 1>(G, Wt, Hact, hact_ld, dpre, n, V, H, stream);
+        case 812: return launch_dpre_nw<8, 2, 4, 2, 2>(G, Wt, Hact, hact_ld, dpre, n, V, H, stream);
+        case 4212: return launch_dpre_nw<4, 2, 3, 2, 2>(G, Wt, Hact, hact_ld, dpre, n, V, H, stream);
+        case 160: return launch_dpre_k16<4, false, false>(G, Wt, Hact, hact_ld, dpre, n, V, H, stream);
+        case 161: return launch_dpre_k16<4, true, false>(G, Wt, Hact, hact_ld, dpre, n, V, H, stream);
+        case 162: return launch_dpre_k16<5, false, false>(G, Wt, Hact, hact_ld, dpre, n, V, H, stream);
+        case 163: return launch_dpre_k16<5, true, false>(G, Wt, Hact, hact_ld, dpre, n, V, H, stream);
+        case 164: return launch_dpre_k16<4, false, true>(G, Wt, Hact, hact_ld, dpre, n, V, H, stream);
+        case 165: return launch_dpre_k16<4, true, true>(G, Wt, Hact, hact_ld, dpre, n, V, H, stream);
+        case 166: return launch_dpre_k16<5, false, true>(G, Wt, Hact, hact_ld, dpre, n, V, H, stream);
+        case 167: return launch_dpre_k16<4, true, true, true>(G, Wt, Hact, hact_ld, dpre, n, V, H, stream);
+        default: break;
+        }
     }
     if constexpr (kVariants) {
         if (tuning().joint_dpre_nw == 1)
             return V % kDKC ? launch_dpre_direct<true>(G, Wt, Hact, hact_ld, dpre, n, V, H, blocks, stream)
                             : launch_dpre_direct<false>(G, Wt, Hact, hact_ld, dpre, n, V, H, blocks, stream);
+        if (tuning().joint_dpre_nw == 2)  // round 5's default
+            return V % kDKC ? launch_dpre_persist<true>(G, Wt, Hact, hact_ld, dpre, n, V, H, blocks, stream)
+                            : launch_dpre_persist<false>(G, Wt, Hact, hact_ld, dpre, n, V, H, blocks, stream);
     }
-    return V % kDKC ? launch_dpre_persist<true>(G, Wt, Hact, hact_ld, dpre, n, V, H, blocks, stream)
-                    : launch_dpre_persist<false>(G, Wt, Hact, hact_ld, dpre, n, V, H, blocks, stream);
+    // the default (round 6): 16x16x32 tiles, fragments read a chunk ahead, DMA and reads interleaved with the MFMA
+    // groups at s_setprio 1, the LDS-staged epilogue (profiles/r06/dpre/: 6.3 -> 4.85 ms at the headline size)
+    return launch_dpre_k16<4, true, true>(G, Wt, Hact, hact_ld, dpre, n, V, H, stream);
 }
 
 }  // namespace mrnnt

@@ -301,6 +301,37 @@ def test_joint_dpre_kernel_vs_torch(jop, dev, H, V, ld):
     assert torch.equal(prep.dpre(G, Hw), out)
 
 
+@pytest.mark.parametrize("nw", [0, 1, 2, 8, 81, 42, 421, 431, 851, 160, 161, 162, 163, 164, 165, 166, 167])
+@pytest.mark.parametrize("H,V,ld", [(512, 1024, 512), (256, 1000, 288)])
+def test_joint_dpre_variants_vs_torch(jop, dev, nw, H, V, ld):
+    """Every launch variant of mrnnt_joint_dpre (development build, knob joint_dpre_nw: tile shapes, LDS stages, the
+    LDS-staged epilogue, the 16x16x32 forms) against torch on the same operands, as above, over 5,000 rows (a partial
+    last row tile of every tile height); the 32x32x16 staged forms equal each other bit for bit (same fragments, same
+    k order)."""
+    enc, pred, w, _, labels, T, S = make_case(9, 4, (150, 200), 60, H, V)
+    prep = jop._JointPrepared(enc.to(dev), pred.to(dev), w.to(dev), None, torch.from_numpy(labels).to(dev),
+                              torch.from_numpy(T), torch.from_numpy(S), 0)
+    n = 5000
+    g = torch.Generator(device=dev).manual_seed(H + V + ld + 1)
+    G = (torch.randn(n, V, device=dev, generator=g) * 1e-2).to(torch.bfloat16)
+    Hw = torch.tanh(torch.randn(n, ld, device=dev, generator=g)).to(torch.bfloat16)
+    prep.problem.hact_ld = ld
+    with knobs(joint_dpre_nw=nw):
+        out = prep.dpre(G, Hw)
+        again = prep.dpre(G, Hw)
+    with knobs(joint_dpre_nw=8):
+        staged = prep.dpre(G, Hw)
+    torch.cuda.synchronize()
+    h = Hw[:, :H].float()
+    ref = (G.float() @ prep.weight.float()) * (1.0 - h * h)
+    err = (out.float() - ref).abs()
+    lim = 2.0 ** -7 * ref.abs() + 1e-3 * ref.abs().max()
+    assert bool((err <= lim).all()), (nw, err.max().item(), ref.abs().max().item())
+    assert torch.equal(again, out)
+    if nw in (8, 81, 42, 421, 431, 851):
+        assert torch.equal(staged, out)
+
+
 def test_joint_dpre_path_matches_library_gemm_path(jop, dev, monkeypatch):
     """The backward through mrnnt_joint_dpre + the reduce on dpre equals the hipBLASLt dH + reduce-with-Hact path
     within the bf16 rounding of dH / dpre (both against the same fp64 host reference: test above; here path vs path)."""

@@ -29,7 +29,7 @@ def main():
     ap.add_argument("--V", type=int, default=1024)
     ap.add_argument("--H", type=int, default=512)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--variants", default='[{"joint_dpre_nw": 0}, {"joint_dpre_nw": 1}]')
+    ap.add_argument("--variants", default='[{"joint_dpre_nw": 0}, {"joint_dpre_nw": 2}, {"joint_dpre_nw": 1}]')
     a = ap.parse_args()
     import _mrnnt_lib as L
     L.select_dev()
