@@ -124,6 +124,7 @@ sweeps)
   f joint_fuzz_120_seed11000 MRNNT_JOINT_CASES=120 MRNNT_FUZZ_FIRST=11000 $P tests/test_gpu_joint.py -k random_cases
   exit 0 ;;
 full)
+  sha monotonic-rnnt_amd/libmonotonic_rnnt_amd.so > $O/lib_sha256.txt
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rs --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 && \
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && \
   timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err && \
