@@ -279,7 +279,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
 // (rows l & 15, pieces l >> 4) land on 16 distinct bank quads. PRIO: s_setprio 1 around each MFMA cluster.
 __device__ __forceinline__ int k16_swz(int row) { return 3 * ((row >> 3) & 1); }
 
-template <int NS, bool PRIO, bool IL, bool HP, int ABL = 0>
+template <int NS, bool PRIO, bool IL, bool HP>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void joint_dpre_k16_kernel(
     const unsigned short *__restrict__ G, const unsigned short *__restrict__ Wt, const unsigned short *__restrict__ Hact,
     int64_t hact_ld, unsigned short *__restrict__ dpre, int64_t n, int V, int H) {
@@ -388,15 +388,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             if (hp && c == nch - 2) gemm_wait_vm<8>();  // chunk nch - 1; the two Hact quarters issued after it fly on
             else wait_chunk(c + 1, c + NS - 2);
         }
-        // development ablations (ABL, results wrong): 2 no DMA in the loop, 4 no barrier, 8 no MFMAs
-        if constexpr (ABL & 4) __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));
-        else gemm_barrier();
+        gemm_barrier();
         if constexpr (!IL) {
             if (c + NS - 1 < nch) stage(c + NS - 1);
             if (c + 1 < nch) read_frags(c + 1, na, nb);
             mma(c, fa, fb);
         } else {
-            const bool st = !(ABL & 2) && c + NS - 1 < nch, rd = c + 1 < nch;
+            const bool st = c + NS - 1 < nch, rd = c + 1 < nch;
             unsigned char *sd = glds + ((c + NS - 1) % NS) * SB;
             const unsigned char *sr = glds + ((c + 1) % NS) * SB;
             const unsigned ko = (unsigned)((c + NS - 1) * kGKC * 2);
@@ -412,13 +410,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
                 for (int a = 2 * g; a < 2 * g + 2; ++a)
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        if constexpr (ABL & 8) {
-                            asm volatile("" ::"v"(fa[a]), "v"(fb[q]));
-                        } else {
-                            acc[a][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], fb[q], acc[a][q], 0, 0, 0);
-                        }
-                    }
+                    for (int q = 0; q < 4; ++q)
+                        acc[a][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], fb[q], acc[a][q], 0, 0, 0);
                 if (PRIO) __builtin_amdgcn_s_setprio(0);
                 __builtin_amdgcn_sched_barrier(0);
                 if (st) {
@@ -458,15 +451,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
     if (c < nch) step(c, fa0, fb0, fa1, fb1);
 
-    if constexpr (ABL & 1) {  // development ablation: no epilogue, the accumulators kept live
-        float sum = 0.0f;
-#pragma unroll
-        for (int a = 0; a < 8; ++a)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) sum += acc[a][q][0] + acc[a][q][1] + acc[a][q][2] + acc[a][q][3];
-        if (sum == 1.25e30f) dpre[r0 * H] = 1;
-        return;
-    }
     // epilogue through LDS, as joint_dpre_kernel's EPI = 1: lane (l16, pc) holds row 64 wr + 16 q + l16 and, in
     // register e of tile (a, q), hidden unit 128 wh + 16 a + 4 pc + e
     constexpr int EI = TR / 2 / NW;
@@ -500,14 +484,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
 }
 
-template <int NS, bool PRIO, bool IL, bool HP = false, int ABL = 0>
+template <int NS, bool PRIO, bool IL, bool HP = false>
 static hipError_t launch_dpre_k16(const unsigned short *G, const unsigned short *Wt, const unsigned short *Hact,
                                   int64_t hact_ld, unsigned short *dpre, int64_t n, int V, int H, hipStream_t stream) {
     const size_t lds = (size_t)NS * 2 * kGT * kGKC * 2;
     const int64_t rtiles = (n + kGT - 1) / kGT;
     const int64_t blocks = ((rtiles + 7) / 8) * 8 * (H / kGT);
     if (blocks > 0x7fffffff / 512) return hipErrorInvalidValue;
-    auto kern = joint_dpre_k16_kernel<NS, PRIO, IL, HP, ABL>;
+    auto kern = joint_dpre_k16_kernel<NS, PRIO, IL, HP>;
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
@@ -886,12 +870,6 @@ hipError_t launch_joint_dpre(const unsigned short *G, const unsigned short *Wt, 
         case 165: return launch_dpre_k16<4, true, true>(G, Wt, Hact, hact_ld, dpre, n, V, H, stream);
         case 166: return launch_dpre_k16<5, false, true>(G, Wt, Hact, hact_ld, dpre, n, V, H, stream);
         case 167: return launch_dpre_k16<4, true, true, true>(G, Wt, Hact, hact_ld, dpre, n, V, H, stream);
-        case 171: return launch_dpre_k16<4, true, true, false, 1>(G, Wt, Hact, hact_ld, dpre, n, V, H, stream);
-        case 173: return launch_dpre_k16<4, true, true, false, 3>(G, Wt, Hact, hact_ld, dpre, n, V, H, stream);
-        case 175: return launch_dpre_k16<4, true, true, false, 5>(G, Wt, Hact, hact_ld, dpre, n, V, H, stream);
-        case 177: return launch_dpre_k16<4, true, true, false, 7>(G, Wt, Hact, hact_ld, dpre, n, V, H, stream);
-        case 179: return launch_dpre_k16<4, true, true, false, 9>(G, Wt, Hact, hact_ld, dpre, n, V, H, stream);
-        case 1711: return launch_dpre_k16<4, true, true, false, 11>(G, Wt, Hact, hact_ld, dpre, n, V, H, stream);
         default: break;
         }
     }
